@@ -1,0 +1,182 @@
+"""Benchmark: Shadow routing-table build (all-pairs RoutingInfo) on MI355X.
+
+Workload (BASELINE.json metric, config C3): 10,000-vertex Atlas-like complete GML graph
+(shadow_amd.synth.atlas_like(10000, seed=10000); 49,995,000 undirected edges + 10,000
+self-loops), all 10,000 nodes used.  One step = srg_compute_shortest_paths_device on the
+edge list already resident in HBM -> every (latency_ns, packet_loss) of the 10^8 used pairs
+written to HBM (dense W build, blocked FW, tight-DAG loss pass, extraction).
+
+value = source-SSSPs/s over the whole job (sources routed per second, all ranks).
+N > 1 (round 1): independent replicas, one full 10k-vertex APSP per rank per step
+("scaling": "weak"); the RCCL pivot-broadcast FW is the planned strong-scaling path.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "APSP wall time + source-SSSPs/sec, 10k-vertex GML graph, 1/2/4/8 MI355X"
+# VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md chip table: wave64
+# issues over 2 cycles on a SIMD-32) = 78.6 T int32 lane-ops/s.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# minimal VALU ops per relaxation on gfx950: u32 = v_add_u32 clamp + 1/2 v_min3_u32;
+# u64 = v_lshl_add_u64 + v_cmp_lt_u64 + 2 v_cndmask
+OPS_PER_RELAX = {0: 1.5, 1: 4.0}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(edges, target_s, threads):
+    """Reference-equivalent CPU pipeline (oracle, 'port') on a bounded sample of sources."""
+    import numpy as np
+    import oracle
+    g = edges.as_tuple()
+    nodes = np.arange(edges.num_vertices, dtype=np.uint32)
+    rng = np.random.default_rng(12345)
+    done, spent = 0, 0.0
+    k = threads
+    while spent < target_s:
+        sample = rng.choice(edges.num_vertices, size=k, replace=False).astype(np.uint32)
+        spent += oracle.time_sources(g, nodes, sample, nthreads=threads)
+        done += k
+        log(f"cpu baseline: {done} sources in {spent:.1f}s")
+        if spent > 0:
+            k = max(threads, min(4 * k, int(threads * max(1.0, (target_s - spent) / max(spent / done * threads, 1e-3)))))
+            k = min(k, edges.num_vertices)
+    return done / spent, done, spent
+
+
+def load_traffic(kernel_substr):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    p = os.path.join(ROOT, "profiles", "fw_pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), d.get("source")
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--vertices", type=int, default=10000)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from shadow_amd import Router, synth
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device, set_profiling
+
+    V = args.vertices
+    seed = args.seed if args.seed is not None else V
+    t0 = time.time()
+    edges = synth.atlas_like(V, seed=seed)
+    log(f"[rank {rank}] generated atlas_like({V}, seed={seed}): {edges.num_edges} edges in {time.time()-t0:.1f}s")
+    dg = DeviceGraph(edges, dev)
+    nodes = torch.arange(V, dtype=torch.int32, device=dev)
+    out_lat = torch.empty((V, V), dtype=torch.int64, device=dev)
+    out_loss = torch.empty((V, V), dtype=torch.float32, device=dev)
+    router = Router(local)
+
+    def step():
+        return compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
+
+    for i in range(args.warmup):
+        s = step()
+        log(f"[rank {rank}] warmup {i}: {s['ms_total']:.2f} ms (fw {s['ms_fw']:.2f}, loss {s['ms_loss']:.2f}, "
+            f"rounds {s['loss_rounds']}, multi {s['multi_pred_pairs']}, kind {s['path_kind']})")
+    set_profiling(router, not args.no_profile)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    agg = {}
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        s = step()
+        for k, v in s.items():
+            if isinstance(v, (int, float)):
+                agg[k] = agg.get(k, 0) + v
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * V * args.steps / elapsed
+
+    kind = s["path_kind"]
+    roofline = None
+    if agg.get("prof_launches"):
+        avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
+        relax = agg["prof_relaxations"] / agg["prof_launches"]
+        achieved = relax * OPS_PER_RELAX.get(kind, 1.5) / (avg_ms * 1e-3) / 1e12
+        traffic, tsrc = load_traffic("fw_product")
+        roofline = {"bound": "valu", "kernel": "fw_product (FW phase 3)", "achieved": round(achieved, 3),
+                    "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
+                    "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
+                    "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
+                    "ops_per_relaxation": OPS_PER_RELAX.get(kind, 1.5),
+                    "traffic_source": tsrc}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except Exception:
+            aff = os.cpu_count() or 1
+        threads = max(1, min(16, aff))
+        v, k, sec = cpu_baseline(edges, args.cpu_seconds, threads)
+        cpu = {"value": round(v, 3), "unit": "source-SSSPs/s", "cores": threads, "kind": "port",
+               "sample": f"{k} random sources of the same 10k-vertex graph, reference-equivalent pipeline "
+                         f"(HashMap-score Dijkstra + linear nodes.contains + HashMap merge), {sec:.1f}s"}
+
+    if rank == 0:
+        n = args.steps
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "source-SSSPs/s", "n_gpus": world, "steps": n,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32+f32" if kind == 0 else "u64+f32",
+            "data": "synthetic",
+            "config": {"workload": f"C3 atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph, "
+                                   f"all {V} nodes used, edge list resident in HBM",
+                       "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
+                       "parallelism": "replicas" if world > 1 else "single"},
+            "apsp_wall_ms": round(ms_per_step, 3),
+            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_loss", "ms_extract")},
+            "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * shadow_routing.h — C ABI of the MI355X routing-table builder for Shadow.
+ *
+ * Drop-in boundary for ONE reference path: Shadow's all-pairs routing-table build
+ *   NetworkGraph::compute_shortest_paths(&self, nodes: &[NodeIndex])
+ *       -> Result<HashMap<(NodeIndex, NodeIndex), PathProperties>, NetGraphError>
+ *   (/root/reference/src/main/network/graph/mod.rs:183-228)
+ * and its use_shortest_path=false sibling
+ *   NetworkGraph::get_direct_paths  (mod.rs:230-252, get_edge_weight mod.rs:254-293)
+ * plus the ingest step in front of it
+ *   NetworkGraph::parse              (mod.rs:134-181, gml-parser/src/parser.rs:44-281,
+ *                                     ShadowNode/ShadowEdge mod.rs:28-111, units.rs:377-439)
+ *
+ * Plain C types only (no torch, no C++ types).  Every function is noexcept: errors are
+ * integer status codes plus a message written to a caller buffer, formatted like the
+ * reference's error strings so the Rust wrapper can forward them verbatim.
+ *
+ * Output layout: dense row-major num_nodes x num_nodes, indexed by POSITION in `nodes`
+ * (out[i*num_nodes + j] = path nodes[i] -> nodes[j]).  The reference returns a HashMap
+ * keyed by (NodeIndex, NodeIndex); the Rust-side binding in INTEGRATION.md rebuilds that
+ * map (or, per SURVEY f1, keeps the dense arrays).  PathProperties is split SoA:
+ * latency_ns (u64) + packet_loss (f32), because the Rust struct is not repr(C).
+ */
+#ifndef SHADOW_ROUTING_H
+#define SHADOW_ROUTING_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------- */
+#define SRG_OK 0
+#define SRG_ERR_ARG 1           /* bad argument (null pointer, index out of range, duplicate node) */
+#define SRG_ERR_NO_EDGE 2       /* "No edge connecting node {src_id} to {dst_id}"       mod.rs:266-268 */
+#define SRG_ERR_MULTI_EDGE 3    /* "More than one edge connecting node {a} to {b}"      mod.rs:269-274 */
+#define SRG_ERR_UNREACHABLE 4   /* assert_eq!(paths.len(), nodes.len().pow(2)) panics   mod.rs:219 */
+#define SRG_ERR_LATENCY_RANGE 5 /* latency.convert(Nano).unwrap() overflow (mod.rs:336) or a
+                                   path sum beyond 2^62 ns (reference would wrap u64) */
+#define SRG_ERR_HIP 6           /* HIP runtime failure (no device, launch failure) */
+#define SRG_ERR_OOM 7           /* device allocation failed */
+#define SRG_ERR_PARSE 8         /* GML / attribute error from NetworkGraph::parse (mod.rs:134-181) */
+#define SRG_ERR_RCCL 9          /* collective failure (multi-GPU) */
+#define SRG_ERR_INTERNAL 10     /* invariant violated inside the builder (a bug) */
+
+/* ---- graph as the Rust side would marshal it from petgraph ------------------------- */
+/* One entry per petgraph edge, in graph.raw_edges() order (== GML edge order).
+ * src/dst are NodeIndex values (dense 0..num_vertices-1, GML node order, mod.rs:157-162).
+ * Self-loops and parallel edges are allowed exactly as in the reference.                */
+typedef struct srg_edge_list {
+    uint32_t num_vertices;
+    uint32_t directed;          /* 1 = petgraph::Directed, 0 = Undirected (GML default 0) */
+    uint64_t num_edges;
+    const uint32_t* src;        /* [num_edges] */
+    const uint32_t* dst;        /* [num_edges] */
+    const uint64_t* latency_ns; /* [num_edges] latency.convert(Nano) (mod.rs:336) */
+    const float* packet_loss;   /* [num_edges] raw f32 in [0,1] (mod.rs:95-103) */
+    const uint32_t* node_ids;   /* [num_vertices] GML id per NodeIndex, for error text; may be NULL */
+} srg_edge_list;
+
+/* Timing / path report for one call (all fields written when the pointer is non-NULL). */
+typedef struct srg_stats {
+    double ms_total;            /* entry -> return wall time */
+    double ms_h2d;              /* host -> device copies (host entry points only) */
+    double ms_build;            /* dense weight-matrix build + validation kernels */
+    double ms_fw;               /* blocked Floyd-Warshall on latency */
+    double ms_loss;             /* tight-predecessor scan + left-fold loss pass */
+    double ms_extract;          /* used x used sub-matrix + diagonal self-loop overwrite */
+    double ms_d2h;              /* device -> host copies (host entry points only) */
+    int32_t path_kind;          /* SRG_PATH_* below */
+    int32_t loss_rounds;        /* max fold rounds over rows (DAG depth + 1) */
+    uint64_t multi_pred_pairs;  /* (s,t) pairs with >1 tight predecessor (slow path) */
+    uint64_t relaxations;       /* min-plus relaxations issued by the FW kernels */
+    /* filled only when profiling is enabled (srg_set_profiling): HIP events recorded on the
+     * launch stream around every launch of the dominant kernel (FW phase-3 product).      */
+    uint64_t prof_launches;     /* profiled launches */
+    double prof_kernel_ms;      /* sum of their event-measured durations */
+    uint64_t prof_relaxations;  /* relaxations those launches performed */
+} srg_stats;
+
+#define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */
+#define SRG_PATH_DENSE_U64 1    /* dense FW, u64 latency keys */
+#define SRG_PATH_DIRECT 2       /* get_direct_paths */
+
+typedef struct srg_ctx srg_ctx; /* opaque: owns device workspace; one HIP device */
+
+/* Create a context bound to HIP device `device` (one process per GPU). */
+int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen);
+void srg_destroy(srg_ctx* ctx);
+
+/* Enable (1) / disable (0) per-launch HIP-event timing of the dominant kernel. */
+int srg_set_profiling(srg_ctx* ctx, int enable);
+
+/* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).
+ * Host pointers in, host pointers out.  out_* are caller-allocated num_nodes^2.
+ * Diagonal = raw self-loop weight (mod.rs:210-217); errors in `nodes` order.           */
+int srg_compute_shortest_paths(srg_ctx* ctx, const srg_edge_list* graph,
+                               const uint32_t* nodes, uint32_t num_nodes,
+                               uint64_t* out_latency_ns, float* out_packet_loss,
+                               srg_stats* stats, char* errbuf, size_t errlen);
+
+/* Same computation with every array already resident in device memory (HBM):
+ * graph->src/dst/latency_ns/packet_loss/node_ids, nodes and out_* are device pointers;
+ * `hip_stream` is a hipStream_t (NULL = default stream).  Returns after the stream work
+ * is complete.  This is the entry the benchmark times (inputs resident in HBM).        */
+int srg_compute_shortest_paths_device(srg_ctx* ctx, const srg_edge_list* graph_dev,
+                                      const uint32_t* nodes_dev, uint32_t num_nodes,
+                                      uint64_t* out_latency_ns_dev, float* out_packet_loss_dev,
+                                      void* hip_stream, srg_stats* stats,
+                                      char* errbuf, size_t errlen);
+
+/* Replaces NetworkGraph::get_direct_paths (mod.rs:230-252): every used pair <- the single
+ * edge src->dst (undirected: either orientation), error unless exactly one exists.     */
+int srg_get_direct_paths(srg_ctx* ctx, const srg_edge_list* graph,
+                         const uint32_t* nodes, uint32_t num_nodes,
+                         uint64_t* out_latency_ns, float* out_packet_loss,
+                         srg_stats* stats, char* errbuf, size_t errlen);
+
+/* ---- ingest: GML text -> graph (NetworkGraph::parse, mod.rs:134-181) --------------- */
+typedef struct srg_graph srg_graph;  /* opaque host-side parsed graph */
+
+int srg_graph_parse_gml(const char* text, size_t len, srg_graph** out,
+                        char* errbuf, size_t errlen);
+void srg_graph_free(srg_graph* g);
+/* Borrowed view of the edge list (valid until srg_graph_free). */
+void srg_graph_edge_list(const srg_graph* g, srg_edge_list* out);
+uint32_t srg_graph_num_vertices(const srg_graph* g);
+uint64_t srg_graph_num_edges(const srg_graph* g);
+int srg_graph_directed(const srg_graph* g);
+/* node_id_to_index (mod.rs:126-128): SRG_OK or SRG_ERR_ARG if the id is unknown. */
+int srg_graph_node_index(const srg_graph* g, uint32_t gml_id, uint32_t* out_index);
+/* node_index_to_id (mod.rs:130-132). */
+uint32_t srg_graph_node_id(const srg_graph* g, uint32_t index);
+/* ShadowNode bandwidths in bit/s (mod.rs:34-57); has_* = 0 when the key was absent.   */
+void srg_graph_node_bandwidth(const srg_graph* g, uint32_t index,
+                              uint64_t* down_bits, int* has_down,
+                              uint64_t* up_bits, int* has_up);
+
+/* Library build/version string. */
+const char* srg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHADOW_ROUTING_H */

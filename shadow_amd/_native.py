@@ -1,0 +1,129 @@
+"""ctypes binding of libshadow_routing.so (C ABI: include/shadow_routing.h).
+
+The library is built in-tree by shadow_amd/build.py.  There is no CPU fallback anywhere in
+the product: if the library is missing, importing the routing entry points raises, and on a
+machine without a HIP device srg_create() returns SRG_ERR_HIP, which surfaces as HipError.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libshadow_routing.so")
+
+SRG_OK = 0
+SRG_ERR_ARG = 1
+SRG_ERR_NO_EDGE = 2
+SRG_ERR_MULTI_EDGE = 3
+SRG_ERR_UNREACHABLE = 4
+SRG_ERR_LATENCY_RANGE = 5
+SRG_ERR_HIP = 6
+SRG_ERR_OOM = 7
+SRG_ERR_PARSE = 8
+SRG_ERR_RCCL = 9
+SRG_ERR_INTERNAL = 10
+
+SRG_PATH_DENSE_U32 = 0
+SRG_PATH_DENSE_U64 = 1
+SRG_PATH_DIRECT = 2
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_f32p = ctypes.POINTER(ctypes.c_float)
+
+
+class EdgeList(ctypes.Structure):
+    _fields_ = [
+        ("num_vertices", ctypes.c_uint32),
+        ("directed", ctypes.c_uint32),
+        ("num_edges", ctypes.c_uint64),
+        ("src", ctypes.c_void_p),
+        ("dst", ctypes.c_void_p),
+        ("latency_ns", ctypes.c_void_p),
+        ("packet_loss", ctypes.c_void_p),
+        ("node_ids", ctypes.c_void_p),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("ms_total", ctypes.c_double),
+        ("ms_h2d", ctypes.c_double),
+        ("ms_build", ctypes.c_double),
+        ("ms_fw", ctypes.c_double),
+        ("ms_loss", ctypes.c_double),
+        ("ms_extract", ctypes.c_double),
+        ("ms_d2h", ctypes.c_double),
+        ("path_kind", ctypes.c_int32),
+        ("loss_rounds", ctypes.c_int32),
+        ("multi_pred_pairs", ctypes.c_uint64),
+        ("relaxations", ctypes.c_uint64),
+        ("prof_launches", ctypes.c_uint64),
+        ("prof_kernel_ms", ctypes.c_double),
+        ("prof_relaxations", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every function declared in include/shadow_routing.h (checked by tests/test_abi.py)
+EXPORTS = [
+    "srg_create", "srg_destroy", "srg_set_profiling", "srg_compute_shortest_paths", "srg_compute_shortest_paths_device",
+    "srg_get_direct_paths", "srg_graph_parse_gml", "srg_graph_free", "srg_graph_edge_list",
+    "srg_graph_num_vertices", "srg_graph_num_edges", "srg_graph_directed", "srg_graph_node_index",
+    "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version",
+]
+
+_lib = None
+
+
+def lib():
+    """Load the native library; raises (never falls back) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python shadow_amd/build.py` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    L.srg_create.restype = c.c_int
+    L.srg_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.c_char_p, c.c_size_t]
+    L.srg_set_profiling.restype = c.c_int
+    L.srg_set_profiling.argtypes = [c.c_void_p, c.c_int]
+    L.srg_destroy.restype = None
+    L.srg_destroy.argtypes = [c.c_void_p]
+    host_sig = [c.c_void_p, c.POINTER(EdgeList), c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p,
+                c.POINTER(Stats), c.c_char_p, c.c_size_t]
+    L.srg_compute_shortest_paths.restype = c.c_int
+    L.srg_compute_shortest_paths.argtypes = host_sig
+    L.srg_get_direct_paths.restype = c.c_int
+    L.srg_get_direct_paths.argtypes = host_sig
+    L.srg_compute_shortest_paths_device.restype = c.c_int
+    L.srg_compute_shortest_paths_device.argtypes = [
+        c.c_void_p, c.POINTER(EdgeList), c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p,
+        c.POINTER(Stats), c.c_char_p, c.c_size_t]
+    L.srg_graph_parse_gml.restype = c.c_int
+    L.srg_graph_parse_gml.argtypes = [c.c_char_p, c.c_size_t, c.POINTER(c.c_void_p), c.c_char_p, c.c_size_t]
+    L.srg_graph_free.restype = None
+    L.srg_graph_free.argtypes = [c.c_void_p]
+    L.srg_graph_edge_list.restype = None
+    L.srg_graph_edge_list.argtypes = [c.c_void_p, c.POINTER(EdgeList)]
+    L.srg_graph_num_vertices.restype = c.c_uint32
+    L.srg_graph_num_vertices.argtypes = [c.c_void_p]
+    L.srg_graph_num_edges.restype = c.c_uint64
+    L.srg_graph_num_edges.argtypes = [c.c_void_p]
+    L.srg_graph_directed.restype = c.c_int
+    L.srg_graph_directed.argtypes = [c.c_void_p]
+    L.srg_graph_node_index.restype = c.c_int
+    L.srg_graph_node_index.argtypes = [c.c_void_p, c.c_uint32, _u32p]
+    L.srg_graph_node_id.restype = c.c_uint32
+    L.srg_graph_node_id.argtypes = [c.c_void_p, c.c_uint32]
+    L.srg_graph_node_bandwidth.restype = None
+    L.srg_graph_node_bandwidth.argtypes = [c.c_void_p, c.c_uint32, _u64p, c.POINTER(c.c_int), _u64p,
+                                           c.POINTER(c.c_int)]
+    L.srg_version.restype = c.c_char_p
+    L.srg_version.argtypes = []
+    _lib = L
+    return L

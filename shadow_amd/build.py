@@ -1,0 +1,51 @@
+"""Build the native routing library in-tree: shadow_amd/libshadow_routing.so (gfx950).
+
+hipcc compiles the HIP kernels + C ABI (routing.hip) and the host-side GML ingest
+(gml.cpp) into one shared object with a plain C ABI (include/shadow_routing.h).
+-ffp-contract=off: Rust never contracts `1 - x*y` (mod.rs:328) into an FMA, so neither may we.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libshadow_routing.so")
+SOURCES = [os.path.join(CSRC, "routing.hip"), os.path.join(CSRC, "gml.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "kernels.hip.h"), os.path.join(ROOT, "include", "shadow_routing.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SRG_OFFLOAD_ARCH", "gfx950")
+
+
+def needs_build():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force=False, verbose=True):
+    if not force and not needs_build():
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        cmd = [HIPCC, "-c", "-fPIC", "-O3", "-std=c++17", "-ffp-contract=off", "-Wall",
+               "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
+        if src.endswith(".hip"):
+            cmd += ["-x", "hip", "--offload-arch=" + ARCH]
+        cmd += [src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

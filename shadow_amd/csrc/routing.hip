@@ -1,0 +1,775 @@
+// routing.hip — MI355X routing-table builder: device pipeline + C ABI (include/shadow_routing.h).
+//
+// Replaces NetworkGraph::compute_shortest_paths (src/main/network/graph/mod.rs:183-228) and
+// NetworkGraph::get_direct_paths (mod.rs:230-252) with a dense device pipeline:
+//   1. k_edge_scan       validate endpoints, count self-loops per vertex, record the raw
+//                        self-loop weight (diagonal, mod.rs:210-217), max edge latency
+//   2. k_w_lat/k_w_loss  dense W = lexicographic min over parallel edges (mod.rs:305-313)
+//   3. fw_phase1/fw_product   blocked min-plus Floyd-Warshall on latency (exact u32-sat or u64)
+//   4. tight_scan        per used source, the tight predecessors of every vertex
+//   5. k_loss_round      left-fold loss over the tight DAG, Jacobi rounds to a fixpoint
+//                        == petgraph Dijkstra's lexicographic (latency, loss) scores
+//   6. k_extract         used x used outputs, diagonal <- raw self-loop, unreachable check
+// No CPU fallback: every entry point fails loudly (status code) when HIP is unavailable.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/shadow_routing.h"
+#include "kernels.hip.h"
+
+using namespace srg;
+
+namespace {
+
+struct Failure {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& m) { throw Failure{code, m}; }
+
+#define HIP_CHECK(expr)                                                                           \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            if (e_ == hipErrorOutOfMemory)                                                        \
+                fail(SRG_ERR_OOM, std::string("device allocation failed: ") + hipGetErrorString(e_)); \
+            fail(SRG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+        }                                                                                         \
+    } while (0)
+
+void set_err(char* buf, size_t len, const std::string& m) {
+    if (buf && len) std::snprintf(buf, len, "%s", m.c_str());
+}
+
+// grow-only device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void* get(size_t need) {
+        if (need <= bytes) return p;
+        if (p) HIP_CHECK(hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        HIP_CHECK(hipMalloc(&p, need ? need : 16));
+        bytes = need;
+        return p;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct EdgeStats {
+    unsigned long long max_lat;   // max latency over non-self-loop edges
+    uint32_t bad_endpoint;        // an endpoint >= V
+    uint32_t lat_overflow;        // a non-self-loop latency == UINT64_MAX (ns conversion overflow)
+};
+
+struct Flags {
+    uint32_t changed;
+    uint32_t inf_in_used_row;
+    uint32_t unreachable_used_pair;
+    uint32_t bad_node;
+    unsigned long long first_bad;  // direct paths: first (i*n+j) with edge count != 1
+};
+
+constexpr int kThreads = 256;
+
+inline unsigned grid_for(size_t work, size_t cap = 256 * 16) {
+    size_t g = (work + kThreads - 1) / kThreads;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// ---------------------------------------------------------------------------------------
+__global__ void k_check_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                              uint32_t* __restrict__ mark, Flags* flags) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t v = nodes[i];
+        if (v >= V) {
+            atomicOr(&flags->bad_node, 1u);
+            continue;
+        }
+        if (atomicAdd(&mark[v], 1u) != 0) atomicOr(&flags->bad_node, 2u);
+    }
+}
+
+__global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                            const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t V,
+                            uint32_t* __restrict__ selfcnt, uint64_t* __restrict__ self_lat,
+                            float* __restrict__ self_loss, EdgeStats* st) {
+    unsigned long long mx = 0;
+    uint32_t bad = 0, ovf = 0;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s >= V || t >= V) {
+            bad = 1;
+            continue;
+        }
+        const uint64_t l = lat[e];
+        if (s == t) {
+            atomicAdd(&selfcnt[s], 1u);
+            self_lat[s] = l;      // meaningful only when the count ends at exactly 1
+            self_loss[s] = loss[e];
+        } else {
+            mx = l > mx ? l : mx;
+            ovf |= (l == UINT64_MAX);
+        }
+    }
+    // wave reduction then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_down(mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_lat, mx);
+    if (bad) atomicOr(&st->bad_endpoint, 1u);
+    if (ovf) atomicOr(&st->lat_overflow, 1u);
+}
+
+template <class K>
+__global__ void k_fill(K* __restrict__ p, size_t count, K v) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+template <class K>
+__device__ __forceinline__ K to_key(uint64_t l) {
+    if constexpr (sizeof(K) == 4) return l >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)l;
+    else return (K)l;
+}
+
+template <class K>
+__global__ void k_w_lat(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                        const uint64_t* __restrict__ lat, int directed, K* __restrict__ W, size_t ld) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s == t) continue;  // self-loops never shorten a path; kept for the diagonal only
+        const K l = to_key<K>(lat[e]);
+        atomicMin(&W[(size_t)s * ld + t], l);
+        if (!directed) atomicMin(&W[(size_t)t * ld + s], l);
+    }
+}
+
+template <class K>
+__global__ void k_w_loss(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                         const uint64_t* __restrict__ lat, const float* __restrict__ loss, int directed,
+                         const K* __restrict__ W, uint32_t* __restrict__ WL, size_t ld) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s == t) continue;
+        const K l = to_key<K>(lat[e]);
+        // -0.0 compares equal to 0.0 (partial_cmp) and folds identically: normalise it
+        const uint32_t bits = __float_as_uint(loss[e] + 0.0f);
+        if (W[(size_t)s * ld + t] == l) atomicMin(&WL[(size_t)s * ld + t], bits);
+        if (!directed && W[(size_t)t * ld + s] == l) atomicMin(&WL[(size_t)t * ld + s], bits);
+    }
+}
+
+template <class K>
+__global__ void k_init_d(const K* __restrict__ W, K* __restrict__ D, size_t ld) {
+    const size_t total = ld * ld;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / ld, c = i - r * ld;
+        D[i] = (r == c) ? (K)0 : W[i];
+    }
+}
+
+// INF anywhere in a used row (u32 certification) -- t < V only
+template <class K>
+__global__ void k_certify(const K* __restrict__ D, size_t ld, const uint32_t* __restrict__ nodes, uint32_t n,
+                          uint32_t V, Flags* flags) {
+    const size_t total = (size_t)n * V;
+    uint32_t hit = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / V, t = i - r * V;
+        hit |= D[(size_t)nodes[r] * ld + t] == KeyOps<K>::INF;
+    }
+    if (hit) atomicOr(&flags->inf_in_used_row, 1u);
+}
+
+template <class K>
+__global__ void k_loss_round(const uint32_t* __restrict__ PRED, const K* __restrict__ D, const K* __restrict__ W,
+                             const uint32_t* __restrict__ WL, const uint32_t* __restrict__ nodes, uint32_t n,
+                             uint32_t V, size_t ld, const float* __restrict__ Lin, float* __restrict__ Lout,
+                             Flags* flags) {
+    const size_t total = (size_t)n * V;
+    uint32_t changed = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / V, t = i - r * V;
+        const uint32_t s = nodes[r];
+        const uint32_t p = PRED[r * ld + t];
+        const float* Lrow = Lin + r * ld;
+        float v;
+        if (t == s) {
+            v = 0.0f;  // Dijkstra start score PathProperties::default() (mod.rs:297)
+        } else if (p == PRED_NONE) {
+            v = 1.0f;  // unreachable: never read by a reachable vertex
+        } else if (p != PRED_MULTI) {
+            const float pl = __uint_as_float(WL[(size_t)p * ld + t]);
+            v = fold_loss(Lrow[p], __fsub_rn(1.0f, pl));
+        } else {
+            // several latency-tight predecessors: Dijkstra keeps the smallest loss
+            const K dst_st = D[(size_t)s * ld + t];
+            const K* Ds = D + (size_t)s * ld;
+            v = 1.0f;
+            for (uint32_t u = 0; u < V; ++u) {
+                if (KeyOps<K>::add(Ds[u], W[(size_t)u * ld + t]) != dst_st) continue;
+                const float pl = __uint_as_float(WL[(size_t)u * ld + t]);
+                const float c = fold_loss(Lrow[u], __fsub_rn(1.0f, pl));
+                v = c < v ? c : v;
+            }
+        }
+        Lout[r * ld + t] = v;
+        changed |= (v != Lrow[t]);
+    }
+    if (changed) atomicOr(&flags->changed, 1u);
+}
+
+__global__ void k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uint32_t V, size_t ld,
+                              unsigned long long* out) {
+    const size_t total = (size_t)n * V;
+    unsigned long long c = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / V, t = i - r * V;
+        c += PRED[r * ld + t] == PRED_MULTI;
+    }
+    if (c) atomicAdd(out, c);
+}
+
+template <class K>
+__global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, size_t ld,
+                          const uint32_t* __restrict__ nodes, uint32_t n, const uint64_t* __restrict__ self_lat,
+                          const float* __restrict__ self_loss, uint64_t* __restrict__ out_lat,
+                          float* __restrict__ out_loss, Flags* flags) {
+    const size_t total = (size_t)n * n;
+    uint32_t unreach = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t a = i / n, b = i - a * n;
+        const uint32_t s = nodes[a], t = nodes[b];
+        if (a == b) {
+            out_lat[i] = self_lat[s];  // raw self-loop weight, no 1-(1-p) rounding
+            out_loss[i] = self_loss[s];
+        } else {
+            const K d = D[(size_t)s * ld + t];
+            unreach |= d == KeyOps<K>::INF;
+            out_lat[i] = (uint64_t)d;
+            out_loss[i] = L[a * ld + t];
+        }
+    }
+    if (unreach) atomicOr(&flags->unreachable_used_pair, 1u);
+}
+
+__global__ void k_positions(const uint32_t* __restrict__ nodes, uint32_t n, int32_t* __restrict__ pos) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        pos[nodes[i]] = (int32_t)i;
+}
+
+__global__ void k_direct(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                         const uint64_t* __restrict__ lat, const float* __restrict__ loss, int directed,
+                         const int32_t* __restrict__ pos, uint32_t n, uint32_t* __restrict__ cnt,
+                         uint64_t* __restrict__ out_lat, float* __restrict__ out_loss) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const int32_t ps = pos[src[e]], pt = pos[dst[e]];
+        if (ps < 0 || pt < 0) continue;
+        size_t k = (size_t)ps * n + pt;
+        if (atomicAdd(&cnt[k], 1u) == 0) {
+            out_lat[k] = lat[e];
+            out_loss[k] = loss[e];
+        }
+        if (!directed && ps != pt) {
+            k = (size_t)pt * n + ps;
+            if (atomicAdd(&cnt[k], 1u) == 0) {
+                out_lat[k] = lat[e];
+                out_loss[k] = loss[e];
+            }
+        }
+    }
+}
+
+__global__ void k_direct_check(const uint32_t* __restrict__ cnt, uint32_t n, Flags* flags) {
+    const size_t total = (size_t)n * n;
+    unsigned long long first = ~0ull;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+        if (cnt[i] != 1 && i < first) first = i;
+    if (first != ~0ull) atomicMin(&flags->first_bad, first);
+}
+
+// ---------------------------------------------------------------------------------------
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+struct srg_ctx {
+    int device = 0;
+    bool profiling = false;
+    std::vector<hipEvent_t> prof_events;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
+    DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
+    DevBuf b_stats, b_flags, b_multi, b_pos, b_cnt;
+    ~srg_ctx() {
+        for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
+                          &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
+                          &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt})
+            b->release();
+        for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+struct DevGraph {
+    uint32_t V;
+    int directed;
+    uint64_t E;
+    const uint32_t* src;
+    const uint32_t* dst;
+    const uint64_t* lat;
+    const float* loss;
+    const uint32_t* ids_dev;    // may be null
+    const uint32_t* ids_host;   // may be null (host entry)
+};
+
+uint32_t node_gml_id(const DevGraph& g, uint32_t v, hipStream_t st) {
+    if (g.ids_host) return g.ids_host[v];
+    if (!g.ids_dev) return v;
+    uint32_t id = v;
+    HIP_CHECK(hipMemcpyAsync(&id, g.ids_dev + v, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return id;
+}
+
+template <class F>
+void set_lds(F func, size_t bytes) {
+    static_assert(sizeof(F) > 0, "");
+    if (bytes > 65536)
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(func),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+// Common validation: nodes in range & unique, edge endpoints, self-loop counts, latency range.
+struct Prelude {
+    EdgeStats es;
+    uint32_t* selfcnt;
+    uint64_t* selflat;
+    float* selfloss;
+    Flags* flags;
+};
+
+Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, hipStream_t st,
+                bool check_selfloops) {
+    Prelude P{};
+    const uint32_t V = g.V;
+    uint32_t* mark = (uint32_t*)c.b_mark.get((size_t)V * 4);
+    P.selfcnt = (uint32_t*)c.b_selfcnt.get((size_t)V * 4);
+    P.selflat = (uint64_t*)c.b_selflat.get((size_t)V * 8);
+    P.selfloss = (float*)c.b_selfloss.get((size_t)V * 4);
+    EdgeStats* es = (EdgeStats*)c.b_stats.get(sizeof(EdgeStats));
+    P.flags = (Flags*)c.b_flags.get(sizeof(Flags));
+    HIP_CHECK(hipMemsetAsync(mark, 0, (size_t)V * 4, st));
+    HIP_CHECK(hipMemsetAsync(P.selfcnt, 0, (size_t)V * 4, st));
+    HIP_CHECK(hipMemsetAsync(es, 0, sizeof(EdgeStats), st));
+    HIP_CHECK(hipMemsetAsync(P.flags, 0, sizeof(Flags), st));
+    if (n) k_check_nodes<<<grid_for(n), kThreads, 0, st>>>(nodes, n, V, mark, P.flags);
+    if (g.E)
+        k_edge_scan<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, V, P.selfcnt,
+                                                       P.selflat, P.selfloss, es);
+    HIP_CHECK(hipGetLastError());
+    Flags fl;
+    HIP_CHECK(hipMemcpyAsync(&P.es, es, sizeof(EdgeStats), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (P.es.bad_endpoint) fail(SRG_ERR_ARG, "edge endpoint out of range (>= num_vertices)");
+    if (fl.bad_node & 1) fail(SRG_ERR_ARG, "node index out of range (>= num_vertices)");
+    if (fl.bad_node & 2) fail(SRG_ERR_ARG, "duplicate node index in `nodes`");
+    if (check_selfloops) {
+        if (P.es.lat_overflow)
+            fail(SRG_ERR_LATENCY_RANGE, "The resulting value is outside of the bounds [0, 18446744073709551615]");
+        // there must be a single self-loop for each node (mod.rs:215-216), in `nodes` order
+        std::vector<uint32_t> cnt(V), nd(n);
+        HIP_CHECK(hipMemcpyAsync(cnt.data(), P.selfcnt, (size_t)V * 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(nd.data(), nodes, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t v = nd[i];
+            if (cnt[v] == 1) continue;
+            const uint32_t id = node_gml_id(g, v, st);
+            if (cnt[v] == 0)
+                fail(SRG_ERR_NO_EDGE, "No edge connecting node " + std::to_string(id) + " to " + std::to_string(id));
+            fail(SRG_ERR_MULTI_EDGE,
+                 "More than one edge connecting node " + std::to_string(id) + " to " + std::to_string(id));
+        }
+    }
+    return P;
+}
+
+struct Timer {
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t0;
+    explicit Timer(hipStream_t s) : st(s) { t0 = std::chrono::steady_clock::now(); }
+    double lap() {
+        HIP_CHECK(hipStreamSynchronize(st));
+        double m = ms_since(t0);
+        t0 = std::chrono::steady_clock::now();
+        return m;
+    }
+};
+
+constexpr int KC = 32;
+
+// Dense path for key type K. Returns false (u32 only) when certification fails.
+template <class K, int T>
+bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
+               float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats) {
+    const uint32_t V = g.V;
+    const size_t Vp = ((size_t)V + T - 1) / T * T;
+    const int nb = (int)(Vp / T);
+    const size_t VV = Vp * Vp;
+    Timer tm(st);
+
+    K* W = (K*)c.b_W.get(VV * sizeof(K));
+    uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
+    K* D = (K*)c.b_D.get(VV * sizeof(K));
+    if (sizeof(K) == 4) HIP_CHECK(hipMemsetAsync(W, 0xFF, VV * 4, st));
+    else k_fill<K><<<grid_for(VV), kThreads, 0, st>>>(W, VV, KeyOps<K>::INF);
+    HIP_CHECK(hipMemsetAsync(WL, 0xFF, VV * 4, st));
+    if (g.E) {
+        k_w_lat<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.directed, W, Vp);
+        k_w_loss<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, W, WL, Vp);
+    }
+    k_init_d<K><<<grid_for(VV), kThreads, 0, st>>>(W, D, Vp);
+    HIP_CHECK(hipGetLastError());
+    const double ms_build = tm.lap();
+
+    // ---- blocked Floyd-Warshall ----
+    constexpr int VE = 16 / (int)sizeof(K);
+    const size_t lds1 = (size_t)T * (T + VE) * sizeof(K);
+    const size_t lds2 = (size_t)2 * KC * (T + VE) * sizeof(K);
+    set_lds(fw_phase1<K, T>, lds1);
+    set_lds(fw_product<K, T, KC>, lds2);
+    const bool prof = c.profiling && nb > 1;
+    if (prof) {
+        while (c.prof_events.size() < (size_t)2 * nb) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            c.prof_events.push_back(e);
+        }
+    }
+    for (int kb = 0; kb < nb; ++kb) {
+        fw_phase1<K, T><<<1, 256, lds1, st>>>(D, Vp, kb);
+        if (nb > 1) {
+            fw_product<K, T, KC><<<2 * (nb - 1), 256, lds2, st>>>(D, Vp, kb, nb, 2);
+            if (prof) HIP_CHECK(hipEventRecord(c.prof_events[2 * kb], st));
+            fw_product<K, T, KC><<<dim3(nb - 1, nb - 1), 256, lds2, st>>>(D, Vp, kb, nb, 3);
+            if (prof) HIP_CHECK(hipEventRecord(c.prof_events[2 * kb + 1], st));
+        }
+    }
+    HIP_CHECK(hipGetLastError());
+    const double ms_fw = tm.lap();
+    if (prof && stats) {
+        double sum = 0;
+        for (int kb = 0; kb < nb; ++kb) {
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, c.prof_events[2 * kb], c.prof_events[2 * kb + 1]));
+            sum += ms;
+        }
+        stats->prof_launches += nb;
+        stats->prof_kernel_ms += sum;
+        stats->prof_relaxations += (uint64_t)nb * (nb - 1) * (nb - 1) * T * T * T;
+    }
+
+    Flags fl{};
+    if (n) {
+        k_certify<K><<<grid_for((size_t)n * V), kThreads, 0, st>>>(D, Vp, nodes, n, V, P.flags);
+        HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
+    if (sizeof(K) == 4 && fl.inf_in_used_row) return false;  // saturated or unreachable: redo in u64
+
+    // ---- tight-predecessor scan + loss rounds ----
+    constexpr int TS = 64;
+    uint32_t* PRED = (uint32_t*)c.b_PRED.get((size_t)std::max<uint32_t>(n, 1) * Vp * 4);
+    float* L0 = (float*)c.b_L0.get((size_t)std::max<uint32_t>(n, 1) * Vp * 4);
+    float* L1 = (float*)c.b_L1.get((size_t)std::max<uint32_t>(n, 1) * Vp * 4);
+    unsigned long long* multi = (unsigned long long*)c.b_multi.get(8);
+    int rounds = 0;
+    unsigned long long nmulti = 0;
+    float* Lfin = L0;
+    if (n) {
+        const size_t lds3 = (size_t)2 * KC * (TS + VE) * sizeof(K);
+        set_lds(tight_scan<K, TS, KC>, lds3);
+        tight_scan<K, TS, KC><<<dim3((unsigned)(Vp / TS), (n + TS - 1) / TS), 256, lds3, st>>>(D, W, Vp, nodes, n,
+                                                                                             PRED);
+        HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
+        k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
+        k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+        HIP_CHECK(hipGetLastError());
+        float* Lin = L0;
+        float* Lout = L1;
+        for (;;) {
+            HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
+            k_loss_round<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(PRED, D, W, WL, nodes, n, V, Vp,
+                                                                                   Lin, Lout, P.flags);
+            HIP_CHECK(hipGetLastError());
+            ++rounds;
+            uint32_t ch = 0;
+            HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            std::swap(Lin, Lout);
+            if (!ch) break;
+            if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
+        }
+        Lfin = Lin;
+        HIP_CHECK(hipMemcpyAsync(&nmulti, multi, 8, hipMemcpyDeviceToHost, st));
+    }
+    const double ms_loss = tm.lap();
+
+    if (n) {
+        HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
+        k_extract<K><<<grid_for((size_t)n * n), kThreads, 0, st>>>(D, Lfin, Vp, nodes, n, P.selflat, P.selfloss,
+                                                                   out_lat, out_loss, P.flags);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
+    }
+    const double ms_extract = tm.lap();
+    if (n && fl.unreachable_used_pair)
+        fail(SRG_ERR_UNREACHABLE,
+             "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
+             "from another used node)");
+    if (stats) {
+        stats->ms_build += ms_build;
+        stats->ms_fw += ms_fw;
+        stats->ms_loss += ms_loss;
+        stats->ms_extract += ms_extract;
+        stats->path_kind = sizeof(K) == 4 ? SRG_PATH_DENSE_U32 : SRG_PATH_DENSE_U64;
+        stats->loss_rounds = rounds;
+        stats->multi_pred_pairs = nmulti;
+        stats->relaxations = (uint64_t)Vp * Vp * Vp;
+    }
+    return true;
+}
+
+void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
+                    float* out_loss, hipStream_t st, srg_stats* stats) {
+    if (g.V == 0) {
+        if (n) fail(SRG_ERR_ARG, "nodes given for an empty graph");
+        return;
+    }
+    Prelude P = prelude(c, g, nodes, n, st, true);
+    if (n == 0) return;
+    // u64 path requires every path sum < 2^62 (INF); reference would wrap a u64 (mod.rs:327)
+    const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (g.V > 1 ? g.V - 1 : 1);
+    if (bound >= ((unsigned __int128)1 << 62))
+        fail(SRG_ERR_LATENCY_RANGE, "path latency sum could exceed 2^62 ns (max edge latency " +
+                                        std::to_string(P.es.max_lat) + " ns)");
+    if (P.es.max_lat < 0xFFFFFFFFull) {
+        if (run_dense<uint32_t, 128>(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
+    }
+    run_dense<uint64_t, 64>(c, g, nodes, n, out_lat, out_loss, st, P, stats);
+}
+
+void direct_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
+                   float* out_loss, hipStream_t st) {
+    Prelude P = prelude(c, g, nodes, n, st, false);
+    if (n == 0) return;
+    int32_t* pos = (int32_t*)c.b_pos.get((size_t)g.V * 4);
+    uint32_t* cnt = (uint32_t*)c.b_cnt.get((size_t)n * n * 4);
+    HIP_CHECK(hipMemsetAsync(pos, 0xFF, (size_t)g.V * 4, st));
+    HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)n * n * 4, st));
+    HIP_CHECK(hipMemsetAsync(&P.flags->first_bad, 0xFF, 8, st));
+    k_positions<<<grid_for(n), kThreads, 0, st>>>(nodes, n, pos);
+    if (g.E)
+        k_direct<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, pos, n, cnt,
+                                                     out_lat, out_loss);
+    k_direct_check<<<grid_for((size_t)n * n), kThreads, 0, st>>>(cnt, n, P.flags);
+    HIP_CHECK(hipGetLastError());
+    Flags fl;
+    HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (fl.first_bad != ~0ull) {
+        const size_t k = fl.first_bad;
+        uint32_t cv = 0, a = 0, b = 0;
+        HIP_CHECK(hipMemcpy(&cv, cnt + k, 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(&a, nodes + k / n, 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(&b, nodes + k % n, 4, hipMemcpyDeviceToHost));
+        const std::string ia = std::to_string(node_gml_id(g, a, st)), ib = std::to_string(node_gml_id(g, b, st));
+        if (cv == 0) fail(SRG_ERR_NO_EDGE, "No edge connecting node " + ia + " to " + ib);
+        fail(SRG_ERR_MULTI_EDGE, "More than one edge connecting node " + ia + " to " + ib);
+    }
+    // get_direct_paths converts every used edge to ns with unwrap (mod.rs:240, 336)
+    if (P.es.lat_overflow || P.es.max_lat == UINT64_MAX) {
+        // only an error when an overflowing edge is among the outputs
+        std::vector<uint64_t> lat((size_t)n * n);
+        HIP_CHECK(hipMemcpy(lat.data(), out_lat, lat.size() * 8, hipMemcpyDeviceToHost));
+        for (uint64_t v : lat)
+            if (v == UINT64_MAX)
+                fail(SRG_ERR_LATENCY_RANGE, "The resulting value is outside of the bounds [0, 18446744073709551615]");
+    }
+}
+
+template <class T>
+T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
+    T* d = (T*)b.get(std::max<size_t>(count, 1) * sizeof(T));
+    if (count) HIP_CHECK(hipMemcpyAsync(d, host, count * sizeof(T), hipMemcpyHostToDevice, st));
+    return d;
+}
+
+int guard(char* errbuf, size_t errlen, const std::function<void()>& body) {
+    try {
+        body();
+        if (errbuf && errlen) errbuf[0] = 0;
+        return SRG_OK;
+    } catch (const Failure& f) {
+        set_err(errbuf, errlen, f.msg);
+        return f.code;
+    } catch (const std::bad_alloc&) {
+        set_err(errbuf, errlen, "out of host memory");
+        return SRG_ERR_OOM;
+    } catch (const std::exception& e) {
+        set_err(errbuf, errlen, std::string("internal error: ") + e.what());
+        return SRG_ERR_INTERNAL;
+    } catch (...) {
+        set_err(errbuf, errlen, "internal error");
+        return SRG_ERR_INTERNAL;
+    }
+}
+
+int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32_t num_nodes, uint64_t* out_lat,
+               float* out_loss, srg_stats* stats, char* errbuf, size_t errlen, bool direct) {
+    if (!c || !g || (num_nodes && (!nodes || !out_lat || !out_loss)) ||
+        (g->num_edges && (!g->src || !g->dst || !g->latency_ns || !g->packet_loss))) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    return guard(errbuf, errlen, [&]() {
+        auto t0 = std::chrono::steady_clock::now();
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        HIP_CHECK(hipSetDevice(c->device));
+        hipStream_t st = c->stream;
+        const size_t E = g->num_edges, n = num_nodes, nn = n * n;
+        DevGraph dg{g->num_vertices, (int)g->directed, g->num_edges, nullptr, nullptr, nullptr, nullptr,
+                    nullptr, g->node_ids};
+        dg.src = stage_in(c->b_src, g->src, E, st);
+        dg.dst = stage_in(c->b_dst, g->dst, E, st);
+        dg.lat = stage_in(c->b_lat, g->latency_ns, E, st);
+        dg.loss = stage_in(c->b_loss, g->packet_loss, E, st);
+        const uint32_t* dn = stage_in(c->b_nodes, nodes, n, st);
+        uint64_t* dol = (uint64_t*)c->b_olat.get(std::max<size_t>(nn, 1) * 8);
+        float* dos = (float*)c->b_oloss.get(std::max<size_t>(nn, 1) * 4);
+        HIP_CHECK(hipStreamSynchronize(st));
+        const double ms_h2d = ms_since(t0);
+        if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
+        else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats);
+        auto t1 = std::chrono::steady_clock::now();
+        if (nn) {
+            HIP_CHECK(hipMemcpyAsync(out_lat, dol, nn * 8, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(out_loss, dos, nn * 4, hipMemcpyDeviceToHost, st));
+        }
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (stats) {
+            stats->ms_h2d = ms_h2d;
+            stats->ms_d2h = ms_since(t1);
+            stats->ms_total = ms_since(t0);
+            if (direct) stats->path_kind = SRG_PATH_DIRECT;
+        }
+    });
+}
+}  // namespace
+
+extern "C" {
+
+int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
+    if (!out) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    *out = nullptr;
+    srg_ctx* c = nullptr;
+    int rc = guard(errbuf, errlen, [&]() {
+        int count = 0;
+        hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess || count == 0)
+            fail(SRG_ERR_HIP, std::string("no HIP device available (") + hipGetErrorString(e) +
+                                  "); the routing builder has no CPU fallback");
+        if (device < 0 || device >= count) fail(SRG_ERR_ARG, "device index out of range");
+        c = new srg_ctx();
+        c->device = device;
+        HIP_CHECK(hipSetDevice(device));
+        HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    });
+    if (rc != SRG_OK) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return SRG_OK;
+}
+
+int srg_set_profiling(srg_ctx* ctx, int enable) {
+    if (!ctx) return SRG_ERR_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->profiling = enable != 0;
+    return SRG_OK;
+}
+
+void srg_destroy(srg_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    delete ctx;
+}
+
+int srg_compute_shortest_paths(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
+                               uint64_t* out_latency_ns, float* out_packet_loss, srg_stats* stats, char* errbuf,
+                               size_t errlen) {
+    return host_entry(ctx, graph, nodes, num_nodes, out_latency_ns, out_packet_loss, stats, errbuf, errlen, false);
+}
+
+int srg_get_direct_paths(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
+                         uint64_t* out_latency_ns, float* out_packet_loss, srg_stats* stats, char* errbuf,
+                         size_t errlen) {
+    return host_entry(ctx, graph, nodes, num_nodes, out_latency_ns, out_packet_loss, stats, errbuf, errlen, true);
+}
+
+int srg_compute_shortest_paths_device(srg_ctx* ctx, const srg_edge_list* g, const uint32_t* nodes_dev,
+                                      uint32_t num_nodes, uint64_t* out_lat_dev, float* out_loss_dev,
+                                      void* hip_stream, srg_stats* stats, char* errbuf, size_t errlen) {
+    if (!ctx || !g || (num_nodes && (!nodes_dev || !out_lat_dev || !out_loss_dev))) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return guard(errbuf, errlen, [&]() {
+        auto t0 = std::chrono::steady_clock::now();
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        HIP_CHECK(hipSetDevice(ctx->device));
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+        DevGraph dg{g->num_vertices, (int)g->directed, g->num_edges, g->src, g->dst, g->latency_ns,
+                    g->packet_loss, g->node_ids, nullptr};
+        compute_device(*ctx, dg, nodes_dev, num_nodes, out_lat_dev, out_loss_dev, st, stats);
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (stats) stats->ms_total = ms_since(t0);
+    });
+}
+
+const char* srg_version(void) { return "shadow_amd routing 0.1 (gfx950, dense FW u32/u64 + tight-DAG loss)"; }
+
+}  // extern "C"

@@ -1,0 +1,334 @@
+"""Host-side mirror of Shadow's network-graph interface for the routing path.
+
+Same names, argument meaning and error behaviour as the reference:
+  PathProperties                 src/main/network/graph/mod.rs:296-340
+  NetworkGraph.parse             mod.rs:134-181    (GML ingest, native C++ parser)
+  NetworkGraph.node_id_to_index  mod.rs:126-128
+  NetworkGraph.node_index_to_id  mod.rs:130-132
+  NetworkGraph.compute_shortest_paths   mod.rs:183-228  (HIP, gfx950 — no CPU fallback)
+  NetworkGraph.get_direct_paths  mod.rs:230-252  (HIP)
+  RoutingInfo                    mod.rs:428-477
+  generate_routing_info          src/main/core/sim_config.rs:425-462
+
+The reference returns HashMap<(NodeIndex, NodeIndex), PathProperties>; here the result is a
+dense PathTable (row-major by position in `nodes`) that behaves like that map
+(`table[(src, dst)]`, `len`, `items()`, `to_dict()`), because building 10^8 Python dict
+entries would dwarf the GPU computation.
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _native as N
+
+
+class NetGraphError(Exception):
+    """Box<dyn Error> returned by NetworkGraph methods (mod.rs:18)."""
+
+    def __init__(self, code, message):
+        super().__init__(message)
+        self.code = code
+        self.message = message
+
+
+class RoutingPanic(NetGraphError):
+    """The reference panics here (assert_eq! at mod.rs:219: an unreachable used pair)."""
+
+
+class HipError(RuntimeError):
+    """No usable HIP device / runtime failure.  The routing builder never falls back to CPU."""
+
+    def __init__(self, code, message):
+        super().__init__(message)
+        self.code = code
+
+
+def _raise(code, msg):
+    if code == N.SRG_ERR_UNREACHABLE:
+        raise RoutingPanic(code, msg)
+    if code in (N.SRG_ERR_HIP, N.SRG_ERR_OOM, N.SRG_ERR_RCCL, N.SRG_ERR_INTERNAL):
+        raise HipError(code, msg)
+    raise NetGraphError(code, msg)
+
+
+class PathProperties:
+    """Network characteristics for a path (mod.rs:296-340).
+
+    Ordering is lexicographic (latency_ns, then packet_loss); `+` composes two paths with
+    loss = 1 - (1-a)*(1-b) in float32, each operation rounded separately (no FMA)."""
+
+    __slots__ = ("latency_ns", "packet_loss")
+
+    def __init__(self, latency_ns=0, packet_loss=0.0):
+        self.latency_ns = int(latency_ns)
+        self.packet_loss = float(np.float32(packet_loss))
+
+    def _key(self):
+        return (self.latency_ns, self.packet_loss)
+
+    def __lt__(self, o):
+        return self._key() < o._key()
+
+    def __le__(self, o):
+        return self._key() <= o._key()
+
+    def __gt__(self, o):
+        return self._key() > o._key()
+
+    def __ge__(self, o):
+        return self._key() >= o._key()
+
+    def __eq__(self, o):
+        return isinstance(o, PathProperties) and self._key() == o._key()
+
+    def __hash__(self):
+        return hash(self._key())
+
+    def __add__(self, o):
+        f = np.float32
+        one = f(1.0)
+        loss = one - (one - f(self.packet_loss)) * (one - f(o.packet_loss))
+        return PathProperties((self.latency_ns + o.latency_ns) & 0xFFFFFFFFFFFFFFFF, loss)
+
+    def __repr__(self):
+        return f"PathProperties(latency_ns={self.latency_ns}, packet_loss={self.packet_loss!r})"
+
+
+class PathTable:
+    """Dense result of compute_shortest_paths / get_direct_paths for `nodes` (NodeIndex)."""
+
+    def __init__(self, nodes, latency_ns, packet_loss, stats=None):
+        self.nodes = np.asarray(nodes, dtype=np.uint32)
+        self.latency_ns = latency_ns
+        self.packet_loss = packet_loss
+        self.stats = stats
+        self._pos = {int(v): i for i, v in enumerate(self.nodes)}
+
+    def __len__(self):
+        return len(self.nodes) ** 2
+
+    def __contains__(self, key):
+        a, b = key
+        return a in self._pos and b in self._pos
+
+    def __getitem__(self, key):
+        a, b = key
+        i, j = self._pos[a], self._pos[b]
+        return PathProperties(int(self.latency_ns[i, j]), self.packet_loss[i, j])
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def items(self):
+        for i, a in enumerate(self.nodes):
+            for j, b in enumerate(self.nodes):
+                yield (int(a), int(b)), PathProperties(int(self.latency_ns[i, j]), self.packet_loss[i, j])
+
+    def to_dict(self):
+        return dict(self.items())
+
+
+class Router:
+    """One srg_ctx (device workspace) per HIP device; thread-safe (the C side serialises)."""
+
+    _default = {}
+    _lock = threading.Lock()
+
+    def __init__(self, device=0):
+        L = N.lib()
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        rc = L.srg_create(ctypes.byref(h), int(device), err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+        self._h = h
+        self.device = device
+
+    @classmethod
+    def default(cls, device=0):
+        with cls._lock:
+            r = cls._default.get(device)
+            if r is None:
+                r = cls._default[device] = Router(device)
+            return r
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().srg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _run(self, fn, edges, nodes):
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        n = len(nodes)
+        out_lat = np.zeros((n, n), dtype=np.uint64)
+        out_loss = np.zeros((n, n), dtype=np.float32)
+        st = N.Stats()
+        err = ctypes.create_string_buffer(1024)
+        el = edges.as_struct()
+        rc = fn(self._h, ctypes.byref(el), nodes.ctypes.data, n, out_lat.ctypes.data, out_loss.ctypes.data,
+                ctypes.byref(st), err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+        return PathTable(nodes, out_lat, out_loss, st.as_dict())
+
+    def compute_shortest_paths(self, edges, nodes):
+        return self._run(N.lib().srg_compute_shortest_paths, edges, nodes)
+
+    def get_direct_paths(self, edges, nodes):
+        return self._run(N.lib().srg_get_direct_paths, edges, nodes)
+
+
+class Edges:
+    """Edge list in petgraph raw_edges() order (the C-ABI's srg_edge_list, host memory)."""
+
+    def __init__(self, num_vertices, src, dst, latency_ns, packet_loss, directed=False, node_ids=None):
+        self.num_vertices = int(num_vertices)
+        self.directed = bool(directed)
+        self.src = np.ascontiguousarray(src, dtype=np.uint32)
+        self.dst = np.ascontiguousarray(dst, dtype=np.uint32)
+        self.latency_ns = np.ascontiguousarray(latency_ns, dtype=np.uint64)
+        self.packet_loss = np.ascontiguousarray(packet_loss, dtype=np.float32)
+        self.node_ids = None if node_ids is None else np.ascontiguousarray(node_ids, dtype=np.uint32)
+        assert len(self.src) == len(self.dst) == len(self.latency_ns) == len(self.packet_loss)
+
+    @property
+    def num_edges(self):
+        return len(self.src)
+
+    def as_struct(self):
+        return N.EdgeList(self.num_vertices, int(self.directed), self.num_edges, self.src.ctypes.data,
+                          self.dst.ctypes.data, self.latency_ns.ctypes.data, self.packet_loss.ctypes.data,
+                          None if self.node_ids is None else self.node_ids.ctypes.data)
+
+    def as_tuple(self):
+        """(V, directed, src, dst, lat, loss, node_ids) -- the oracle's graph argument."""
+        return (self.num_vertices, self.directed, self.src, self.dst, self.latency_ns, self.packet_loss,
+                self.node_ids)
+
+
+class NetworkGraph:
+    """A network graph: the parsed GML graph plus GML-id <-> NodeIndex maps (mod.rs:113-181)."""
+
+    def __init__(self, edges, bandwidth_down=None, bandwidth_up=None):
+        self.edges = edges
+        ids = edges.node_ids if edges.node_ids is not None else np.arange(edges.num_vertices, dtype=np.uint32)
+        self._ids = ids
+        self._id_to_index = {}
+        for i, gid in enumerate(ids.tolist()):
+            self._id_to_index[gid] = i  # later duplicates win (HashMap::insert, mod.rs:161)
+        self.bandwidth_down = bandwidth_down
+        self.bandwidth_up = bandwidth_up
+
+    @staticmethod
+    def parse(graph_text):
+        """NetworkGraph::parse (mod.rs:134-181) via the native GML parser."""
+        L = N.lib()
+        data = graph_text.encode("utf-8") if isinstance(graph_text, str) else bytes(graph_text)
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(2048)
+        rc = L.srg_graph_parse_gml(data, len(data), ctypes.byref(h), err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+        try:
+            el = N.EdgeList()
+            L.srg_graph_edge_list(h, ctypes.byref(el))
+            V, E = el.num_vertices, el.num_edges
+
+            def arr(ptr, ctype, count, dtype):
+                if count == 0:
+                    return np.zeros(0, dtype=dtype)
+                return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctype)), shape=(count,)).copy()
+
+            edges = Edges(V, arr(el.src, ctypes.c_uint32, E, np.uint32), arr(el.dst, ctypes.c_uint32, E, np.uint32),
+                          arr(el.latency_ns, ctypes.c_uint64, E, np.uint64),
+                          arr(el.packet_loss, ctypes.c_float, E, np.float32), bool(el.directed),
+                          arr(el.node_ids, ctypes.c_uint32, V, np.uint32))
+            down, up = [], []
+            for i in range(V):
+                d, u = ctypes.c_uint64(), ctypes.c_uint64()
+                hd, hu = ctypes.c_int(), ctypes.c_int()
+                L.srg_graph_node_bandwidth(h, i, ctypes.byref(d), ctypes.byref(hd), ctypes.byref(u), ctypes.byref(hu))
+                down.append(d.value if hd.value else None)
+                up.append(u.value if hu.value else None)
+        finally:
+            L.srg_graph_free(h)
+        return NetworkGraph(edges, down, up)
+
+    @property
+    def directed(self):
+        return self.edges.directed
+
+    def num_nodes(self):
+        return self.edges.num_vertices
+
+    def node_id_to_index(self, gml_id):
+        return self._id_to_index.get(gml_id)
+
+    def node_index_to_id(self, index):
+        if 0 <= index < self.edges.num_vertices:
+            return int(self._ids[index])
+        return None
+
+    def compute_shortest_paths(self, nodes, router=None):
+        """NetworkGraph::compute_shortest_paths (mod.rs:183-228) on the GPU."""
+        return (router or Router.default()).compute_shortest_paths(self.edges, nodes)
+
+    def get_direct_paths(self, nodes, router=None):
+        """NetworkGraph::get_direct_paths (mod.rs:230-252) on the GPU."""
+        return (router or Router.default()).get_direct_paths(self.edges, nodes)
+
+
+class RoutingInfo:
+    """Routing information keyed by GML node ids (mod.rs:428-477), dense-backed."""
+
+    def __init__(self, table, ids):
+        self._table = table
+        self._ids = np.asarray(ids, dtype=np.uint32)
+        self._pos = {int(g): i for i, g in enumerate(self._ids)}
+        self._counters = {}
+        self._lock = threading.Lock()
+
+    def path(self, start, end):
+        i, j = self._pos.get(start), self._pos.get(end)
+        if i is None or j is None:
+            return None
+        return PathProperties(int(self._table.latency_ns[i, j]), self._table.packet_loss[i, j])
+
+    def increment_packet_count(self, start, end):
+        with self._lock:
+            k = (start, end)
+            self._counters[k] = min(self._counters.get(k, 0) + 1, 0xFFFFFFFFFFFFFFFF)
+
+    def packet_count(self, start, end):
+        return self._counters.get((start, end), 0)
+
+    def get_smallest_latency_ns(self):
+        if len(self._ids) == 0:
+            return None
+        return int(self._table.latency_ns.min())
+
+    def __len__(self):
+        return len(self._ids) ** 2
+
+
+def generate_routing_info(graph, nodes, use_shortest_paths=True, router=None):
+    """sim_config.rs:425-462: GML ids -> NodeIndex, shortest or direct paths, keyed by GML id."""
+    idx = [graph.node_id_to_index(x) for x in nodes]
+    if any(i is None for i in idx):
+        raise NetGraphError(N.SRG_ERR_ARG, "node id not in graph")
+    try:
+        if use_shortest_paths:
+            table = graph.compute_shortest_paths(idx, router)
+        else:
+            table = graph.get_direct_paths(idx, router)
+    except NetGraphError as e:
+        what = "compute shortest paths" if use_shortest_paths else "get the direct paths"
+        raise type(e)(e.code, f"Failed to {what} between graph nodes: {e.message}") from e
+    return RoutingInfo(table, [graph.node_index_to_id(i) for i in idx])

@@ -1,0 +1,137 @@
+"""CPU: native GML ingest (NetworkGraph::parse, mod.rs:134-181; parser.rs; units.rs)."""
+import numpy as np
+import pytest
+
+from shadow_amd import NetGraphError, NetworkGraph, synth
+from helpers import edge_gml, kat_gml, load_kats
+
+
+def test_kat_graph_parses():
+    for d in (True, False):
+        g = NetworkGraph.parse(kat_gml(d))
+        assert g.directed == d
+        assert g.edges.num_vertices == 3 and g.edges.num_edges == 7
+        assert g.edges.latency_ns.tolist() == [3333, 5555, 7777, 3, 5, 7, 11]
+        assert g.node_id_to_index(2) == 2 and g.node_index_to_id(1) == 1
+
+
+def test_kat_nonexistent_id():
+    """mod.rs:531-557: an edge to a missing node id is an error."""
+    k = load_kats()["test_nonexistent_id"]
+    tmpl = ("graph [\n  node [\n    id 1\n  ]\n  node [\n    id 3\n  ]\n  edge [\n    source 1\n"
+            "    target {}\n    latency \"1 ns\"\n  ]\n]")
+    for t in k["targets_ok"]:
+        NetworkGraph.parse(tmpl.format(t))
+    for t in k["targets_err"]:
+        with pytest.raises(NetGraphError, match="Edge target 2 doesn't exist"):
+            NetworkGraph.parse(tmpl.format(t))
+
+
+@pytest.mark.parametrize("s,ns", list(load_kats()["time_ok"].items()))
+def test_units_time_ok(s, ns):
+    g = NetworkGraph.parse(edge_gml(latency=f'"{s}"'))
+    assert int(g.edges.latency_ns[0]) == ns
+
+
+@pytest.mark.parametrize("s", load_kats()["time_err"])
+def test_units_time_err(s):
+    with pytest.raises(NetGraphError, match="Edge 'latency' is not a valid unit"):
+        NetworkGraph.parse(edge_gml(latency=f'"{s}"'))
+
+
+@pytest.mark.parametrize("s,bits", list(load_kats()["bits_ok"].items()))
+def test_units_bits_ok(s, bits):
+    txt = f'graph [\n  node [\n    id 0\n    host_bandwidth_up "{s}"\n  ]\n]\n'
+    g = NetworkGraph.parse(txt)
+    assert g.bandwidth_up[0] == bits and g.bandwidth_down[0] is None
+
+
+@pytest.mark.parametrize("s", load_kats()["bits_err"])
+def test_units_bits_err(s):
+    txt = f'graph [\n  node [\n    id 0\n    host_bandwidth_down "{s}"\n  ]\n]\n'
+    with pytest.raises(NetGraphError, match="Node 'host_bandwidth_down' is not a valid unit"):
+        NetworkGraph.parse(txt)
+
+
+@pytest.mark.parametrize("tok,msg", [
+    (None, "Edge 'latency' was not provided"),
+    ("5", "Edge 'latency' is not a string"),
+    ('"0 ms"', "Edge 'latency' must not be 0"),
+])
+def test_edge_latency_errors(tok, msg):
+    with pytest.raises(NetGraphError, match=msg):
+        NetworkGraph.parse(edge_gml(latency=tok))
+
+
+@pytest.mark.parametrize("tok,ok,val", [
+    ("0.25", True, 0.25), ("0", False, None), ("1.5", False, None), ("-0.5", False, None),
+    ("1", False, None), ("1e-3", True, 1e-3), (".5", True, 0.5), ("0.", True, 0.0), ('"0.1"', False, None),
+    ("-0.0", True, -0.0),
+])
+def test_packet_loss_token(tok, ok, val):
+    txt = edge_gml(latency='"1 ms"', packet_loss=tok)
+    if ok:
+        g = NetworkGraph.parse(txt)
+        assert np.float32(g.edges.packet_loss[0]) == np.float32(val)
+    else:
+        with pytest.raises(NetGraphError):
+            NetworkGraph.parse(txt)
+
+
+def test_jitter_validated_and_ignored():
+    NetworkGraph.parse(edge_gml(latency='"1 ms"', jitter='"3 ms"'))
+    with pytest.raises(NetGraphError, match="Edge 'jitter' is not a valid unit"):
+        NetworkGraph.parse(edge_gml(latency='"1 ms"', jitter='"3 parsecs"'))
+
+
+@pytest.mark.parametrize("txt", [
+    "graph [\n]\n",
+    "  \n graph [\n  directed 1\n]\n trailing garbage is ignored",
+    "graph [\n  label \"x\"\n  node [\n    id 0\n    label \"a b\"\n  ]\n]\n",
+    "graph [\r\n  node [\r\n    id 0\r\n  ]\r\n]\r\n",
+])
+def test_grammar_ok(txt):
+    NetworkGraph.parse(txt)
+
+
+@pytest.mark.parametrize("txt", [
+    "graph [ node [ id 0 ] ]",                       # newline required after '['
+    "graph [\n  directed 2\n]\n",                    # Bool must be 0 or 1
+    "graph [\n  directed 1\n  directed 0\n]\n",     # only once
+    "graph [\n  a 1\n  a 2\n]\n",                    # duplicate graph keys
+    "graph [\n  node [\n    id 0\n    id 1\n  ]\n]\n",  # duplicate node keys
+    "graph [\n  node [\n    id \"0\"\n  ]\n]\n",     # Incorrect 'id' type
+    "graph [\n  node [\n    label \"x\"\n  ]\n]\n",  # Node 'id' was not provided
+    "graph [\n  edge [\n    target 0\n  ]\n]\n",     # 'source' doesn't exist
+    "graph [\n  label \"\"\n]\n",                    # empty strings are not GML strings here
+    "graph [\n  node [\n    id 0\n  ]",              # no closing bracket
+    "grph [\n]\n",
+])
+def test_grammar_errors(txt):
+    with pytest.raises(NetGraphError):
+        NetworkGraph.parse(txt)
+
+
+def test_duplicate_node_ids_last_wins():
+    txt = ("graph [\n  node [\n    id 5\n  ]\n  node [\n    id 5\n  ]\n  edge [\n    source 5\n"
+           "    target 5\n    latency \"1 ms\"\n  ]\n]\n")
+    g = NetworkGraph.parse(txt)
+    assert g.edges.num_vertices == 2 and g.node_id_to_index(5) == 1
+    assert g.edges.src.tolist() == [1]
+
+
+def test_builtin_one_gbit_switch():
+    """configuration.rs:1355-1369 ONE_GBIT_SWITCH_GRAPH."""
+    txt = ('graph [\n  directed 0\n  node [\n    id 0\n    host_bandwidth_up "1 Gbit"\n'
+           '    host_bandwidth_down "1 Gbit"\n  ]\n  edge [\n    source 0\n    target 0\n'
+           '    latency "1 ms"\n    packet_loss 0.0\n  ]\n]')
+    g = NetworkGraph.parse(txt)
+    assert g.bandwidth_up == [10**9] and g.edges.latency_ns.tolist() == [10**6]
+
+
+def test_roundtrip_synthetic_gml():
+    e = synth.random_graph(30, 0.3, 4, directed=True, loss_hi=0.02)
+    g = NetworkGraph.parse(synth.to_gml(e))
+    assert np.array_equal(g.edges.src, e.src) and np.array_equal(g.edges.dst, e.dst)
+    assert np.array_equal(g.edges.latency_ns, e.latency_ns)
+    assert np.array_equal(g.edges.packet_loss.view(np.uint32), e.packet_loss.view(np.uint32))

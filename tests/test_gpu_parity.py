@@ -1,0 +1,175 @@
+"""GPU parity: HIP path (through the C ABI) vs the oracle / golden vectors.  Bit-exact on
+latency (u64) AND packet_loss (f32 bits) -- stricter than the north star's 1e-6 relative
+loss tolerance, which is asserted too (LOSS_RTOL) so a tolerance regression is visible."""
+import numpy as np
+import pytest
+
+import oracle
+from shadow_amd import NetGraphError, NetworkGraph, Router, RoutingPanic, generate_routing_info, synth
+from shadow_amd import _native as N
+from shadow_amd.graph import Edges
+from helpers import bits_equal, fixture_edges, fixture_expect, kat_gml, load_kats, load_vectors
+
+pytestmark = pytest.mark.gpu
+LOSS_RTOL = 1e-6  # north star: packet_loss within 1e-6 relative
+
+
+def assert_parity(table, lat, loss):
+    assert np.array_equal(table.latency_ns, lat), "latency_ns must be bit-exact"
+    got = table.packet_loss.astype(np.float64)
+    ref = np.asarray(loss, dtype=np.float32).astype(np.float64)
+    assert np.all(np.abs(got - ref) <= LOSS_RTOL * np.abs(ref)), "packet_loss beyond 1e-6 relative"
+    assert bits_equal(table.packet_loss, loss), "packet_loss not bit-exact"
+
+
+@pytest.mark.parametrize("fx", load_vectors(), ids=lambda f: f["name"])
+def test_golden_vectors(router, fx):
+    e = fixture_edges(fx)
+    if fx["expect_code"]:
+        with pytest.raises(NetGraphError) as ei:
+            router.compute_shortest_paths(e, fx["nodes"])
+        assert ei.value.code == fx["expect_code"]
+        return
+    lat, loss = fixture_expect(fx)
+    t = router.compute_shortest_paths(e, fx["nodes"])
+    assert_parity(t, lat, loss.view(np.float32))
+    if fx["name"] == "u64_latencies":
+        assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+
+
+@pytest.mark.parametrize("directed", [True, False])
+def test_kat_shortest_path_gpu(router, directed):
+    """mod.rs:559-647 test_shortest_path, end to end: GML text -> HIP."""
+    exp = load_kats()["test_shortest_path"]["expect_directed" if directed else "expect_undirected"]
+    g = NetworkGraph.parse(kat_gml(directed))
+    n0, n1, n2 = (g.node_id_to_index(i) for i in (0, 1, 2))
+    sp = g.compute_shortest_paths([n0, n1, n2], router)
+    assert len(sp) == 9
+    for k, v in exp.items():
+        a, b = (n0, n1, n2)[int(k[0])], (n0, n1, n2)[int(k[1])]
+        assert sp[(a, b)].latency_ns == v
+
+
+CASES = [
+    dict(V=50, density=0.2, seed=101, lat_hi=8),
+    dict(V=129, density=0.1, seed=102, directed=True, lat_hi=1000),
+    dict(V=130, density=0.3, seed=103, lat_hi=3, parallel=0.3),
+    dict(V=200, density=0.05, seed=104, directed=True, lat_hi=20, loss_hi=1e-6),
+    dict(V=257, density=0.5, seed=105, lat_hi=10**8, lat_lo=10**6),
+    dict(V=300, density=0.02, seed=106, lat_hi=50),
+    dict(V=70, density=0.4, seed=107, directed=True, lat_lo=2**31, lat_hi=2**34),
+]
+
+
+@pytest.mark.parametrize("kw", CASES, ids=lambda k: f"V{k['V']}_s{k['seed']}")
+def test_random_vs_oracle(router, kw):
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    nodes = list(range(V))
+    try:
+        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    except oracle.OracleError as e:
+        with pytest.raises(NetGraphError) as ei:
+            router.compute_shortest_paths(g, nodes)
+        assert ei.value.code == e.code
+        return
+    assert_parity(router.compute_shortest_paths(g, nodes), lat, loss)
+
+
+def test_subset_nodes_scrambled(router):
+    g = synth.random_graph(180, 0.1, 7, lat_hi=100)
+    rng = np.random.default_rng(1)
+    nodes = rng.permutation(180)[:77].tolist()
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    assert_parity(router.compute_shortest_paths(g, nodes), lat, loss)
+
+
+def test_deterministic_bytes(router):
+    g = synth.random_graph(150, 0.2, 9, lat_hi=4, parallel=0.2)
+    a = router.compute_shortest_paths(g, list(range(150)))
+    b = router.compute_shortest_paths(g, list(range(150)))
+    assert np.array_equal(a.latency_ns, b.latency_ns) and bits_equal(a.packet_loss, b.packet_loss)
+
+
+def test_error_messages(router):
+    g = NetworkGraph.parse(kat_gml(True))
+    e = g.edges
+    no_self = Edges(3, e.src[3:], e.dst[3:], e.latency_ns[3:], e.packet_loss[3:], True, e.node_ids)
+    with pytest.raises(NetGraphError, match="No edge connecting node 0 to 0"):
+        router.compute_shortest_paths(no_self, [0, 1, 2])
+    two = Edges(3, np.r_[e.src, 1], np.r_[e.dst, 1], np.r_[e.latency_ns, 9], np.r_[e.packet_loss, 0.0], True, e.node_ids)
+    with pytest.raises(NetGraphError, match="More than one edge connecting node 1 to 1"):
+        router.compute_shortest_paths(two, [0, 1, 2])
+    iso = Edges(4, [0, 1, 2, 3, 0], [0, 1, 2, 3, 1], [1, 1, 1, 1, 3], [0.0] * 5, False)
+    with pytest.raises(RoutingPanic):
+        router.compute_shortest_paths(iso, [0, 1, 2, 3])
+    t = router.compute_shortest_paths(iso, [0, 1])     # unreachable unused vertices are fine
+    assert t[(0, 1)].latency_ns == 3
+    with pytest.raises(NetGraphError):
+        router.compute_shortest_paths(iso, [0, 0])       # duplicate node
+
+
+def test_direct_paths_vs_oracle(router):
+    e = synth.complete_random(40, seed=11)
+    nodes = list(np.random.default_rng(2).permutation(40)[:25])
+    lat, loss = oracle.get_direct_paths(e.as_tuple(), nodes)
+    t = router.get_direct_paths(e, nodes)
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+    g = NetworkGraph.parse(kat_gml(True))
+    with pytest.raises(NetGraphError, match="No edge connecting node 1 to 2"):
+        router.get_direct_paths(g.edges, [0, 1, 2])
+
+
+def test_generate_routing_info_ids(router):
+    txt = synth.to_gml(synth.random_graph(20, 0.4, 3, lat_hi=9), node_ids=[100 + 3 * i for i in range(20)])
+    g = NetworkGraph.parse(txt)
+    ids = {100, 103, 130, 157}
+    ri = generate_routing_info(g, ids, True, router)
+    idx = [g.node_id_to_index(x) for x in ids]
+    lat, loss = oracle.compute_shortest_paths(g.edges.as_tuple(), idx)
+    for i, a in enumerate(ids):
+        for j, b in enumerate(ids):
+            p = ri.path(a, b)
+            assert p.latency_ns == int(lat[i, j]) and np.float32(p.packet_loss) == loss[i, j]
+    assert ri.get_smallest_latency_ns() == int(lat.min())
+
+
+def test_device_entry_matches_host(router):
+    import torch
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+    g = synth.atlas_like(300, seed=5)
+    dg = DeviceGraph(g)
+    nodes = torch.arange(300, dtype=torch.int32, device="cuda:0")
+    ol = torch.empty((300, 300), dtype=torch.int64, device="cuda:0")
+    os_ = torch.empty((300, 300), dtype=torch.float32, device="cuda:0")
+    compute_shortest_paths_device(router, dg, nodes, ol, os_)
+    torch.cuda.synchronize()
+    t = router.compute_shortest_paths(g, list(range(300)))
+    assert np.array_equal(ol.cpu().numpy().view(np.uint64), t.latency_ns)
+    assert bits_equal(os_.cpu().numpy(), t.packet_loss)
+
+
+@pytest.mark.slow
+def test_c1_full_vs_oracle(router):
+    """Config C1 (1000-vertex complete graph), every pair."""
+    e = synth.complete_random(1000, seed=1001)
+    nodes = list(range(1000))
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, nthreads=16)
+    assert_parity(router.compute_shortest_paths(e, nodes), lat, loss)
+
+
+@pytest.mark.slow
+def test_c2_sampled_rows(router):
+    """Config C2 (4096-vertex Atlas-like): full GPU matrix vs 24 seeded oracle rows, plus
+    size-independent properties (diagonal = self-loops, symmetric latency)."""
+    e = synth.atlas_like(4096, seed=4096)
+    nodes = list(range(4096))
+    t = router.compute_shortest_paths(e, nodes)
+    rows = np.random.default_rng(4096).choice(4096, 24, replace=False).tolist()
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, nthreads=16)
+    assert np.array_equal(t.latency_ns[rows], lat)
+    assert bits_equal(t.packet_loss[rows], loss)
+    assert np.array_equal(np.diag(t.latency_ns), e.latency_ns[:4096])
+    off = ~np.eye(4096, dtype=bool)
+    assert np.array_equal(t.latency_ns[off], t.latency_ns.T[off])
