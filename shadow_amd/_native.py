@@ -82,6 +82,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7).
+    # Loading torch first makes the dynamic linker reuse that runtime for our library too;
+    # loading ours first would pull /opt/rocm's copy and torch's HIP init would then fail.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python shadow_amd/build.py` "
