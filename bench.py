@@ -106,7 +106,8 @@ def main():
     for i in range(args.warmup):
         s = step()
         log(f"[rank {rank}] warmup {i}: {s['ms_total']:.2f} ms (fw {s['ms_fw']:.2f}, loss {s['ms_loss']:.2f}, "
-            f"rounds {s['loss_rounds']}, multi {s['multi_pred_pairs']}, kind {s['path_kind']})")
+            f"scan {s['ms_scan']:.2f}, rounds {s['loss_rounds']}, multi {s['multi_pred_pairs']}, kind {s['path_kind']}, "
+            f"ess {s['essential_edges']} ({s['essential_edges'] / V / V:.3f} of V^2), scan_kind {s['scan_kind']})")
     set_profiling(router, not args.no_profile)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -169,8 +170,9 @@ def main():
                        "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
                        "parallelism": "replicas" if world > 1 else "single"},
             "apsp_wall_ms": round(ms_per_step, 3),
-            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_loss", "ms_extract")},
+            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract")},
             "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
+            "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

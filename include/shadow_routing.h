@@ -66,14 +66,18 @@ typedef struct srg_stats {
     double ms_h2d;              /* host -> device copies (host entry points only) */
     double ms_build;            /* dense weight-matrix build + validation kernels */
     double ms_fw;               /* blocked Floyd-Warshall on latency */
-    double ms_loss;             /* tight-predecessor scan + left-fold loss pass */
+    double ms_scan;             /* essential-edge extraction + tight-predecessor scan */
+    double ms_loss;             /* left-fold loss rounds over the tight DAG */
     double ms_extract;          /* used x used sub-matrix + diagonal self-loop overwrite */
     double ms_d2h;              /* device -> host copies (host entry points only) */
     int32_t path_kind;          /* SRG_PATH_* below */
     int32_t loss_rounds;        /* max fold rounds over rows (DAG depth + 1) */
     uint64_t multi_pred_pairs;  /* (s,t) pairs with >1 tight predecessor (slow path) */
     uint64_t relaxations;       /* min-plus relaxations issued by the FW kernels */
-    /* filled only when profiling is enabled (srg_set_profiling): HIP events recorded on the
+    uint64_t essential_edges;   /* edges with W[u][t] == D[u][t] (candidates for tightness) */
+    int32_t scan_kind;          /* SRG_SCAN_* below */
+    int32_t reserved;
+    /* filled only when profiling is enabled (SRG_OPT_PROFILING): HIP events recorded on the
      * launch stream around every launch of the dominant kernel (FW phase-3 product).      */
     uint64_t prof_launches;     /* profiled launches */
     double prof_kernel_ms;      /* sum of their event-measured durations */
@@ -84,14 +88,23 @@ typedef struct srg_stats {
 #define SRG_PATH_DENSE_U64 1    /* dense FW, u64 latency keys */
 #define SRG_PATH_DIRECT 2       /* get_direct_paths */
 
+#define SRG_SCAN_NONE 0         /* no used sources */
+#define SRG_SCAN_SPARSE 1       /* tight scan over the essential edges (default) */
+#define SRG_SCAN_DENSE 2        /* tight scan over all (s,u,t) triples (essential-dense graphs) */
+
 typedef struct srg_ctx srg_ctx; /* opaque: owns device workspace; one HIP device */
 
 /* Create a context bound to HIP device `device` (one process per GPU). */
 int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen);
 void srg_destroy(srg_ctx* ctx);
 
-/* Enable (1) / disable (0) per-launch HIP-event timing of the dominant kernel. */
-int srg_set_profiling(srg_ctx* ctx, int enable);
+/* Context options.
+ *   SRG_OPT_PROFILING         1 = HIP-event timing of every dominant-kernel launch (stats.prof_*)
+ *   SRG_OPT_SPARSE_THRESHOLD  essential-edge density (E_ess / V^2) up to which the sparse
+ *                             tight scan is used (default 0.35; 0 forces the dense scan)      */
+#define SRG_OPT_PROFILING 1
+#define SRG_OPT_SPARSE_THRESHOLD 2
+int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).
  * Host pointers in, host pointers out.  out_* are caller-allocated num_nodes^2.

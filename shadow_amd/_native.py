@@ -26,6 +26,13 @@ SRG_PATH_DENSE_U32 = 0
 SRG_PATH_DENSE_U64 = 1
 SRG_PATH_DIRECT = 2
 
+SRG_OPT_PROFILING = 1
+SRG_OPT_SPARSE_THRESHOLD = 2
+
+SRG_SCAN_NONE = 0
+SRG_SCAN_SPARSE = 1
+SRG_SCAN_DENSE = 2
+
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -50,6 +57,7 @@ class Stats(ctypes.Structure):
         ("ms_h2d", ctypes.c_double),
         ("ms_build", ctypes.c_double),
         ("ms_fw", ctypes.c_double),
+        ("ms_scan", ctypes.c_double),
         ("ms_loss", ctypes.c_double),
         ("ms_extract", ctypes.c_double),
         ("ms_d2h", ctypes.c_double),
@@ -57,6 +65,9 @@ class Stats(ctypes.Structure):
         ("loss_rounds", ctypes.c_int32),
         ("multi_pred_pairs", ctypes.c_uint64),
         ("relaxations", ctypes.c_uint64),
+        ("essential_edges", ctypes.c_uint64),
+        ("scan_kind", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
         ("prof_launches", ctypes.c_uint64),
         ("prof_kernel_ms", ctypes.c_double),
         ("prof_relaxations", ctypes.c_uint64),
@@ -68,7 +79,7 @@ class Stats(ctypes.Structure):
 
 # every function declared in include/shadow_routing.h (checked by tests/test_abi.py)
 EXPORTS = [
-    "srg_create", "srg_destroy", "srg_set_profiling", "srg_compute_shortest_paths", "srg_compute_shortest_paths_device",
+    "srg_create", "srg_destroy", "srg_set_option", "srg_compute_shortest_paths", "srg_compute_shortest_paths_device",
     "srg_get_direct_paths", "srg_graph_parse_gml", "srg_graph_free", "srg_graph_edge_list",
     "srg_graph_num_vertices", "srg_graph_num_edges", "srg_graph_directed", "srg_graph_node_index",
     "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version",
@@ -97,8 +108,8 @@ def lib():
     c = ctypes
     L.srg_create.restype = c.c_int
     L.srg_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.c_char_p, c.c_size_t]
-    L.srg_set_profiling.restype = c.c_int
-    L.srg_set_profiling.argtypes = [c.c_void_p, c.c_int]
+    L.srg_set_option.restype = c.c_int
+    L.srg_set_option.argtypes = [c.c_void_p, c.c_int, c.c_double]
     L.srg_destroy.restype = None
     L.srg_destroy.argtypes = [c.c_void_p]
     host_sig = [c.c_void_p, c.POINTER(EdgeList), c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p,

@@ -26,6 +26,9 @@
 
 #include "../../include/shadow_routing.h"
 #include "kernels.hip.h"
+#include "tight_sparse.hip.h"
+
+#include <hipcub/hipcub.hpp>
 
 using namespace srg;
 
@@ -317,6 +320,7 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 struct srg_ctx {
     int device = 0;
+    double sparse_threshold = 0.35;  // essential-edge density above which the dense scan is used
     bool profiling = false;
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -324,10 +328,15 @@ struct srg_ctx {
     DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
     DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
     DevBuf b_stats, b_flags, b_multi, b_pos, b_cnt;
+    // sparse tight scan
+    DevBuf b_ecnt, b_gflag, b_eoff, b_goff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu,
+        b_grpe, b_cscent, b_gblk, b_DST, b_scantmp, b_small, b_entkw;
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
-                          &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt})
+                          &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_gflag, &b_eoff, &b_goff,
+                          &b_indeg, &b_cscoff, &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe,
+                          &b_cscent, &b_gblk, &b_DST, &b_scantmp, &b_small, &b_entkw})
             b->release();
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -506,38 +515,127 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
 
     // ---- tight-predecessor scan + loss rounds ----
     constexpr int TS = 64;
-    uint32_t* PRED = (uint32_t*)c.b_PRED.get((size_t)std::max<uint32_t>(n, 1) * Vp * 4);
-    float* L0 = (float*)c.b_L0.get((size_t)std::max<uint32_t>(n, 1) * Vp * 4);
-    float* L1 = (float*)c.b_L1.get((size_t)std::max<uint32_t>(n, 1) * Vp * 4);
+    const size_t nmax = std::max<uint32_t>(n, 1);
+    uint32_t* PRED = (uint32_t*)c.b_PRED.get(nmax * Vp * 4);
+    float* L0 = (float*)c.b_L0.get(nmax * Vp * 4);
+    float* L1 = (float*)c.b_L1.get(nmax * Vp * 4);
     unsigned long long* multi = (unsigned long long*)c.b_multi.get(8);
     int rounds = 0;
     unsigned long long nmulti = 0;
+    uint64_t n_ess = 0;
+    int scan_kind = SRG_SCAN_NONE;
     float* Lfin = L0;
+    double ms_scan = 0;
     if (n) {
-        const size_t lds3 = (size_t)2 * KC * (TS + VE) * sizeof(K);
-        set_lds(tight_scan<K, TS, KC>, lds3);
-        tight_scan<K, TS, KC><<<dim3((unsigned)(Vp / TS), (n + TS - 1) / TS), 256, lds3, st>>>(D, W, Vp, nodes, n,
-                                                                                             PRED);
-        HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
-        k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
-        k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+        // essential edges: W[u][t] == D[u][t], grouped in 32-target blocks
+        const uint32_t nw64 = (V + 63) / 64;
+        const uint32_t nbT = 2 * nw64;
+        const size_t NQ = (size_t)nbT * V;
+        uint32_t* ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
+        uint32_t* eoff = (uint32_t*)c.b_eoff.get(NQ * 4);
+        uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
+        uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
+        uint32_t* eblk = (uint32_t*)c.b_gblk.get(((size_t)nbT + 1) * 4);
+        HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
+        k_ess_count<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, nw64, ecnt, indeg);
         HIP_CHECK(hipGetLastError());
-        float* Lin = L0;
-        float* Lout = L1;
-        for (;;) {
-            HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
-            k_loss_round<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(PRED, D, W, WL, nodes, n, V, Vp,
-                                                                                   Lin, Lout, P.flags);
+        size_t tb0 = 0, tb2 = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ecnt, eoff, (int)NQ, st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, indeg, cscoff, (int)(nw64 * 64 + 1), st));
+        size_t tbytes = std::max(tb0, tb2);
+        void* tmp = c.b_scantmp.get(tbytes);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ecnt, eoff, (int)NQ, st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(nw64 * 64 + 1), st));
+        k_ess_blocks<<<1, 1, 0, st>>>(eoff, ecnt, V, nbT, eblk);
+        uint32_t tail[3];
+        HIP_CHECK(hipMemcpyAsync(&tail[0], eoff + NQ - 1, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tail[1], ecnt + NQ - 1, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tail[2], eblk + nbT, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        const uint64_t E_ess = (uint64_t)tail[0] + tail[1];
+        const uint64_t E_pad = tail[2];  // padded entry count (blocks rounded up to 64)
+        n_ess = E_ess;
+        const size_t npad = ((size_t)n + 63) / 64 * 64;
+        const size_t dst_bytes = (size_t)nw64 * 64 * npad * sizeof(K);
+        const bool sparse = (double)E_ess <= c.sparse_threshold * (double)V * (double)V &&
+                            E_pad + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
+        if (sparse) {
+            scan_kind = SRG_SCAN_SPARSE;
+            const size_t Eb = E_pad + 256;
+            uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
+            uint32_t* ent_ro = (uint32_t*)c.b_entkey.get(Eb * 4);
+            K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
+            uint32_t* ent_tl = (uint32_t*)c.b_grpu.get(Eb * 4);
+            uint32_t* ent_u = (uint32_t*)c.b_grpe.get(Eb * 4);
+            float* ent_b = (float*)c.b_entb.get(Eb * 4);
+            uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
+            HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+            k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
+                W, D, WL, Vp, V, nw64, npad, eoff, eblk, cscoff, cscfill, ent_ro, ent_w, ent_tl, ent_u, ent_b, cscent);
+            k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
+            const uint32_t nbS = (uint32_t)(npad / 64);
+            K* DST = (K*)c.b_DST.get(dst_bytes);
+            k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, nodes, n, DST, npad);
+            const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
+            if constexpr (sizeof(K) == 4) {
+                tight_sparse_u32<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, nodes, n, V,
+                                                      nbT, nbS, eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED,
+                                                      Vp);
+            } else {
+                tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, nodes, n, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
+                                                      PRED, Vp);
+            }
             HIP_CHECK(hipGetLastError());
-            ++rounds;
-            uint32_t ch = 0;
-            HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            std::swap(Lin, Lout);
-            if (!ch) break;
-            if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
+            HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
+            k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
+            k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+            HIP_CHECK(hipGetLastError());
+            ms_scan = tm.lap();
+            float* Lin = L0;
+            float* Lout = L1;
+            for (;;) {
+                HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
+                k_loss_round_sparse<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(
+                    PRED, Vp, DST, npad, nodes, n, V, ent_u, ent_w, ent_b, cscoff, cscent, Lin, Lout,
+                    &P.flags->changed);
+                HIP_CHECK(hipGetLastError());
+                ++rounds;
+                uint32_t ch = 0;
+                HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                std::swap(Lin, Lout);
+                if (!ch) break;
+                if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
+            }
+            Lfin = Lin;
+        } else {
+            scan_kind = SRG_SCAN_DENSE;
+            const size_t lds3 = (size_t)2 * KC * (TS + VE) * sizeof(K);
+            set_lds(tight_scan<K, TS, KC>, lds3);
+            tight_scan<K, TS, KC><<<dim3((unsigned)(Vp / TS), (n + TS - 1) / TS), 256, lds3, st>>>(D, W, Vp, nodes,
+                                                                                                 n, PRED);
+            HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
+            k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
+            k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+            HIP_CHECK(hipGetLastError());
+            ms_scan = tm.lap();
+            float* Lin = L0;
+            float* Lout = L1;
+            for (;;) {
+                HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
+                k_loss_round<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(PRED, D, W, WL, nodes, n, V,
+                                                                                       Vp, Lin, Lout, P.flags);
+                HIP_CHECK(hipGetLastError());
+                ++rounds;
+                uint32_t ch = 0;
+                HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                std::swap(Lin, Lout);
+                if (!ch) break;
+                if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
+            }
+            Lfin = Lin;
         }
-        Lfin = Lin;
         HIP_CHECK(hipMemcpyAsync(&nmulti, multi, 8, hipMemcpyDeviceToHost, st));
     }
     const double ms_loss = tm.lap();
@@ -557,12 +655,15 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
     if (stats) {
         stats->ms_build += ms_build;
         stats->ms_fw += ms_fw;
+        stats->ms_scan += ms_scan;
         stats->ms_loss += ms_loss;
         stats->ms_extract += ms_extract;
         stats->path_kind = sizeof(K) == 4 ? SRG_PATH_DENSE_U32 : SRG_PATH_DENSE_U64;
         stats->loss_rounds = rounds;
         stats->multi_pred_pairs = nmulti;
         stats->relaxations = (uint64_t)Vp * Vp * Vp;
+        stats->essential_edges = n_ess;
+        stats->scan_kind = scan_kind;
     }
     return true;
 }
@@ -724,11 +825,20 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
     return SRG_OK;
 }
 
-int srg_set_profiling(srg_ctx* ctx, int enable) {
+int srg_set_option(srg_ctx* ctx, int option, double value) {
     if (!ctx) return SRG_ERR_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->profiling = enable != 0;
-    return SRG_OK;
+    switch (option) {
+        case SRG_OPT_PROFILING:
+            ctx->profiling = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_THRESHOLD:
+            if (!(value >= 0.0)) return SRG_ERR_ARG;
+            ctx->sparse_threshold = value;
+            return SRG_OK;
+        default:
+            return SRG_ERR_ARG;
+    }
 }
 
 void srg_destroy(srg_ctx* ctx) {

@@ -1,0 +1,335 @@
+// tight_sparse.hip.h — tight-predecessor scan over the ESSENTIAL edges (gfx950).
+//
+// An edge (u,t) can be tight for some source s (D[s][u] + W[u][t] == D[s][t]) only if it is
+// itself a shortest path: W[u][t] == D[u][t]  (else D[s][u]+W[u][t] > D[s][u]+D[u][t] >= D[s][t]).
+// On Atlas-like graphs only ~8-15% of the V^2 edges are essential, so the scan walks them
+// instead of all V^3 (s,u,t) triples.
+//
+// Layout (all in HBM):
+//   DST [Vt x npad] K   DST[u][r] = D[nodes[r]][u]  (sources on the fast axis -> lanes)
+//   target blocks of TB = 32 targets; the entries of block b are u-sorted and occupy
+//   [eblk[b], eblk[b+1]), padded to a multiple of 64 with sentinels (w = INF, tl = 0, u = 0):
+//     ent_ro[e] = u * npad * sizeof(K)   (byte offset of DST row u: a buffer-load soffset)
+//     ent_w[e]  = W[u][t],  ent_tl[e] = t - 32*b,  ent_u[e] = u,  ent_b[e] = 1 - loss(u,t)
+//   csc_off[t] .. csc_off[t+1]: entry indices whose target is t (multi-predecessor slow path)
+//
+// Scan (u32 keys): one 64-lane wave per (target block b, source block c), lane = source.
+// d[tl] = D[s][32b+tl] is a register vector read with the wave-uniform tl (s_set_gpr_idx, no
+// LDS, no copies); a hit (rare) updates St[tl][lane] in LDS under a vcc-skipped branch.  The
+// entry stream arrives as coalesced 64-entry vector batches broadcast with v_readlane; every
+// entry gets its own row load (u-sorted, so repeats hit L1) through a buffer load whose SGPR
+// soffset is the precomputed row offset.  Loads are issued on a fully static schedule (two
+// 32-entry halves, statically indexed row buffers) so every s_waitcnt is a compile-time count
+// (vmcnt is in-order: a load issued under data-dependent control flow would drain the
+// prefetch), and the per-entry work is VALU + v_readlane, not SALU (one scalar unit per CU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hip.h"
+
+namespace srg {
+
+constexpr uint32_t TB = 32;  // targets per block of the sparse scan
+
+// ---- essential-edge extraction ---------------------------------------------------------
+// One wave per (u, 64-target window w64): lanes = targets; window w64 = blocks 2*w64, 2*w64+1.
+template <class K>
+__device__ __forceinline__ unsigned long long ess_mask(const K* __restrict__ W, const K* __restrict__ D,
+                                                      size_t ld, uint32_t V, uint32_t u, uint32_t w64,
+                                                      uint32_t lane) {
+    const uint32_t t = w64 * 64 + lane;
+    bool ess = false;
+    if (t < V && t != u) {
+        const K w = W[(size_t)u * ld + t];
+        ess = (w != KeyOps<K>::INF) && (w == D[(size_t)u * ld + t]);
+    }
+    return __ballot(ess);
+}
+
+// cnt[b*V + u] = essential edges u -> block b;  indeg[t] for the CSC lists.
+template <class K>
+__global__ void __launch_bounds__(256) k_ess_count(const K* __restrict__ W, const K* __restrict__ D, size_t ld,
+                                                    uint32_t V, uint32_t nw64, uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ indeg) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    const size_t total = (size_t)nw64 * V;
+    for (size_t q = wave; q < total; q += nwaves) {
+        const uint32_t w64 = (uint32_t)(q / V), u = (uint32_t)(q - (size_t)w64 * V);
+        const unsigned long long m = ess_mask<K>(W, D, ld, V, u, w64, lane);
+        if ((m >> lane) & 1ull) atomicAdd(&indeg[w64 * 64 + lane], 1u);
+        if (lane == 0) {
+            cnt[(size_t)(2 * w64) * V + u] = (uint32_t)__popcll(m & 0xFFFFFFFFull);
+            cnt[(size_t)(2 * w64 + 1) * V + u] = (uint32_t)__popcll(m >> 32);
+        }
+    }
+}
+
+// Padded block bases: eblk[b] = sum_{b' < b} roundup64(total(b')), total from the raw scan.
+__global__ void k_ess_blocks(const uint32_t* __restrict__ eoff, const uint32_t* __restrict__ cnt, uint32_t V,
+                             uint32_t nb, uint32_t* __restrict__ eblk) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    uint64_t acc = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        eblk[b] = (uint32_t)acc;
+        const size_t last = (size_t)b * V + (V - 1);
+        const uint64_t tot = (uint64_t)eoff[last] + cnt[last] - eoff[(size_t)b * V];
+        acc += (tot + 63) / 64 * 64;
+    }
+    eblk[nb] = (uint32_t)acc;
+}
+
+template <class K>
+__global__ void __launch_bounds__(256) k_ess_fill(const K* __restrict__ W, const K* __restrict__ D,
+                                                   const uint32_t* __restrict__ WL, size_t ld, uint32_t V,
+                                                   uint32_t nw64, size_t npad, const uint32_t* __restrict__ eoff,
+                                                   const uint32_t* __restrict__ eblk,
+                                                   const uint32_t* __restrict__ csc_off,
+                                                   uint32_t* __restrict__ csc_fill, uint32_t* __restrict__ ent_ro,
+                                                   K* __restrict__ ent_w, uint32_t* __restrict__ ent_tl,
+                                                   uint32_t* __restrict__ ent_u, float* __restrict__ ent_b,
+                                                   uint32_t* __restrict__ csc_ent) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    const size_t total = (size_t)nw64 * V;
+    for (size_t q = wave; q < total; q += nwaves) {
+        const uint32_t w64 = (uint32_t)(q / V), u = (uint32_t)(q - (size_t)w64 * V);
+        const unsigned long long m = ess_mask<K>(W, D, ld, V, u, w64, lane);
+        if (!((m >> lane) & 1ull)) continue;
+        const uint32_t t = w64 * 64 + lane;
+        const uint32_t hb = lane >> 5;  // which 32-target block of the window
+        const uint32_t b = 2 * w64 + hb;
+        const unsigned long long hm = hb ? (m >> 32) : (m & 0xFFFFFFFFull);
+        const uint32_t tl = lane & 31u;
+        const uint32_t rank = (uint32_t)__popcll(hm & ((1ull << tl) - 1ull));
+        const size_t qb = (size_t)b * V + u;
+        const uint32_t e = eblk[b] + (eoff[qb] - eoff[(size_t)b * V]) + rank;
+        ent_ro[e] = (uint32_t)((size_t)u * npad * sizeof(K));
+        ent_w[e] = W[(size_t)u * ld + t];
+        ent_tl[e] = tl;
+        ent_u[e] = u;
+        ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));
+        const uint32_t k = atomicAdd(&csc_fill[t], 1u);
+        csc_ent[csc_off[t] + k] = e;
+    }
+}
+
+// Sentinel entries: the block padding [eblk[b] + tot(b), eblk[b+1]) and 256 entries past the
+// end (the scan's batch loads run two batches ahead without guards).  grid = nb + 1 blocks.
+template <class K>
+__global__ void k_ess_pad(const uint32_t* __restrict__ eoff, const uint32_t* __restrict__ cnt,
+                          const uint32_t* __restrict__ eblk, uint32_t V, uint32_t nb, uint32_t* __restrict__ ent_ro,
+                          K* __restrict__ ent_w, uint32_t* __restrict__ ent_tl, uint32_t* __restrict__ ent_u,
+                          float* __restrict__ ent_b) {
+    const uint32_t b = blockIdx.x;
+    uint32_t beg, end;
+    if (b < nb) {
+        const size_t last = (size_t)b * V + (V - 1);
+        beg = eblk[b] + (eoff[last] + cnt[last] - eoff[(size_t)b * V]);
+        end = eblk[b + 1];
+    } else {
+        beg = eblk[nb];
+        end = beg + 256;
+    }
+    for (uint32_t e = beg + threadIdx.x; e < end; e += blockDim.x) {
+        ent_ro[e] = 0;
+        ent_w[e] = KeyOps<K>::INF;
+        ent_tl[e] = 0;
+        ent_u[e] = 0;
+        ent_b[e] = 1.0f;
+    }
+}
+
+// DST[u][r] = D[nodes[r]][u] for u < Vt, r < npad (r >= n -> nodes[n-1]); 64x64 LDS tiles.
+template <class K>
+__global__ void __launch_bounds__(256) k_build_dst(const K* __restrict__ D, size_t ld,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n,
+                                                    K* __restrict__ DST, size_t npad) {
+    __shared__ K tile[64][65];
+    const uint32_t ub = blockIdx.x, rb = blockIdx.y;
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    for (uint32_t i = ty; i < 64; i += 4) {
+        uint32_t r = rb * 64 + i;
+        const uint32_t s = nodes[r < n ? r : n - 1];
+        tile[i][tx] = D[(size_t)s * ld + ub * 64 + tx];
+    }
+    __syncthreads();
+    for (uint32_t j = ty; j < 64; j += 4) DST[(size_t)(ub * 64 + j) * npad + rb * 64 + tx] = tile[tx][j];
+}
+
+__device__ __forceinline__ void sparse_block_coords(uint32_t nbT, uint32_t& b, uint32_t& c) {
+    // XCD-aware placement: workgroups bid, bid+8, ... share an XCD (round-robin dispatch), so
+    // each XCD gets whole source blocks and re-reads the same DST columns from its own L2.
+    const uint32_t bid = blockIdx.x;
+    const uint32_t xcd = bid & 7, slot = bid >> 3;
+    c = xcd + 8 * (slot / nbT);
+    b = slot % nbT;
+}
+
+// ---- generic scan (u64 keys): LDS tile + LDS state, straightforward -------------------
+template <class K>
+__global__ void __launch_bounds__(64) tight_sparse(const K* __restrict__ DST, size_t npad,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                    uint32_t nbT, uint32_t nbS, const uint32_t* __restrict__ eblk,
+                                                    const uint32_t* __restrict__ ent_u, const K* __restrict__ ent_w,
+                                                    const uint32_t* __restrict__ ent_tl, uint32_t* __restrict__ PRED,
+                                                    size_t ldp) {
+    __shared__ K Dt[TB][64];
+    __shared__ uint32_t St[TB][64];
+    uint32_t b, c;
+    sparse_block_coords(nbT, b, c);
+    if (c >= nbS) return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t r = c * 64 + lane;
+    const K* col = DST + c * 64 + lane;
+    for (uint32_t tl = 0; tl < TB; ++tl) {
+        Dt[tl][lane] = col[(size_t)(b * TB + tl) * npad];
+        St[tl][lane] = PRED_NONE;
+    }
+    const uint32_t e0 = eblk[b], e1 = eblk[b + 1];
+    uint32_t cur_u = 0xFFFFFFFFu;
+    K a = 0;
+    for (uint32_t e = e0; e < e1; ++e) {
+        const uint32_t u = ent_u[e];
+        if (u != cur_u) {
+            cur_u = u;
+            a = col[(size_t)u * npad];
+        }
+        const uint32_t tl = ent_tl[e];
+        if (KeyOps<K>::add(a, ent_w[e]) == Dt[tl][lane]) {
+            const uint32_t st = St[tl][lane];
+            St[tl][lane] = (st == PRED_NONE) ? e : PRED_MULTI;
+        }
+    }
+    if (r >= n) return;
+    const uint32_t s = nodes[r];
+    for (uint32_t tl = 0; tl < TB; ++tl) {
+        const uint32_t t = b * TB + tl;
+        uint32_t v = St[tl][lane];
+        if (t >= V || t == s || Dt[tl][lane] == KeyOps<K>::INF) v = PRED_NONE;
+        PRED[(size_t)r * ldp + t] = v;
+    }
+}
+
+// ---- u32 scan: register tile, static load schedule (the hot variant) --------------------
+typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    // raw buffer: stride 0, num_records = bytes, gfx9 dword data format (0x00027000)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00027000);
+}
+
+#define SRG_HALF(ABUF, WV, TLV, LBASE, EBASE)                                                   \
+    _Pragma("unroll") for (int j = 0; j < 32; ++j) {                                            \
+        const uint32_t w_ = (uint32_t)__builtin_amdgcn_readlane((WV), (LBASE) + j);             \
+        const uint32_t tl_ = (uint32_t)__builtin_amdgcn_readlane((TLV), (LBASE) + j);           \
+        const uint32_t x_ = __builtin_elementwise_add_sat(ABUF[j], w_);                          \
+        if (x_ == d[tl_]) {                                                                      \
+            const uint32_t st_ = St[tl_][lane];                                                  \
+            St[tl_][lane] = (st_ == PRED_NONE) ? (EBASE) + j : PRED_MULTI;                       \
+        }                                                                                        \
+    }
+#define SRG_ROWS(ABUF, ROV, LBASE)                                                               \
+    _Pragma("unroll") for (int j = 0; j < 32; ++j) {                                            \
+        const uint32_t ro_ = (uint32_t)__builtin_amdgcn_readlane((ROV), (LBASE) + j);           \
+        ABUF[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, ro_, 0);                      \
+    }
+
+__global__ void __launch_bounds__(64) tight_sparse_u32(const uint32_t* __restrict__ DST, size_t npad,
+                                                        uint32_t dst_bytes, const uint32_t* __restrict__ nodes,
+                                                        uint32_t n, uint32_t V, uint32_t nbT, uint32_t nbS,
+                                                        const uint32_t* __restrict__ eblk,
+                                                        const uint32_t* __restrict__ ent_ro,
+                                                        const uint32_t* __restrict__ ent_w,
+                                                        const uint32_t* __restrict__ ent_tl,
+                                                        uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ uint32_t St[TB][64];
+    uint32_t b, c;
+    sparse_block_coords(nbT, b, c);
+    if (c >= nbS) return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t r = c * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t voff = r * 4u;  // this lane's column
+    v32u d;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (uint32_t)((b * TB + i) * npad * 4u), 0);
+        St[i][lane] = PRED_NONE;
+    }
+    const uint32_t e_beg = eblk[b], e_end = eblk[b + 1];  // a multiple of 64 apart
+    if (e_beg < e_end) {
+        uint32_t roc = ent_ro[e_beg + lane], wc = ent_w[e_beg + lane], tlc = ent_tl[e_beg + lane];
+        uint32_t ron = ent_ro[e_beg + 64 + lane], wn = ent_w[e_beg + 64 + lane], tln = ent_tl[e_beg + 64 + lane];
+        uint32_t A0[32], A1[32];
+        SRG_ROWS(A0, roc, 0)
+        SRG_ROWS(A1, roc, 32)
+        for (uint32_t e = e_beg; e < e_end; e += 64) {
+            const uint32_t ro2 = ent_ro[e + 128 + lane], w2 = ent_w[e + 128 + lane], tl2 = ent_tl[e + 128 + lane];
+            SRG_HALF(A0, wc, tlc, 0, e)
+            SRG_ROWS(A0, ron, 0)
+            SRG_HALF(A1, wc, tlc, 32, e + 32)
+            SRG_ROWS(A1, ron, 32)
+            roc = ron;
+            wc = wn;
+            tlc = tln;
+            ron = ro2;
+            wn = w2;
+            tln = tl2;
+        }
+    }
+    if (r >= n) return;
+    const uint32_t s = nodes[r];
+    uint32_t* out = PRED + (size_t)r * ldp + b * TB;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t t = b * TB + i;
+        uint32_t v = St[i][lane];
+        if (t >= V || t == s || d[i] == 0xFFFFFFFFu) v = PRED_NONE;
+        out[i] = v;
+    }
+}
+
+// Jacobi round of the left fold over the tight DAG, entries variant.
+template <class K>
+__global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,
+                                    size_t npad, const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                    const uint32_t* __restrict__ ent_u, const K* __restrict__ ent_w,
+                                    const float* __restrict__ ent_b, const uint32_t* __restrict__ csc_off,
+                                    const uint32_t* __restrict__ csc_ent, const float* __restrict__ Lin,
+                                    float* __restrict__ Lout, uint32_t* __restrict__ changed_flag) {
+    const size_t total = (size_t)n * V;
+    uint32_t changed = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / V, t = i - r * V;
+        const uint32_t s = nodes[r];
+        const uint32_t p = PRED[r * ldp + t];
+        const float* Lrow = Lin + r * ldp;
+        float v;
+        if (t == s) {
+            v = 0.0f;
+        } else if (p == PRED_NONE) {
+            v = 1.0f;
+        } else if (p != PRED_MULTI) {
+            v = fold_loss(Lrow[ent_u[p]], ent_b[p]);
+        } else {
+            const K dst = DST[t * npad + r];
+            v = 1.0f;
+            for (uint32_t k = csc_off[t]; k < csc_off[t + 1]; ++k) {
+                const uint32_t e = csc_ent[k];
+                const uint32_t u = ent_u[e];
+                if (KeyOps<K>::add(DST[(size_t)u * npad + r], ent_w[e]) != dst) continue;
+                const float cnd = fold_loss(Lrow[u], ent_b[e]);
+                v = cnd < v ? cnd : v;
+            }
+        }
+        Lout[r * ldp + t] = v;
+        changed |= (v != Lrow[t]);
+    }
+    if (changed) atomicOr(changed_flag, 1u);
+}
+
+}  // namespace srg

@@ -51,7 +51,7 @@ def compute_shortest_paths_device(router, dgraph, nodes_t, out_lat_t, out_loss_t
 
 
 def set_profiling(router, enable):
-    N.lib().srg_set_profiling(router._h, 1 if enable else 0)
+    router.set_option(N.SRG_OPT_PROFILING, 1 if enable else 0)
 
 
 __all__ = ["DeviceGraph", "Router", "compute_shortest_paths_device", "set_profiling"]

@@ -153,6 +153,11 @@ class Router:
                 r = cls._default[device] = Router(device)
             return r
 
+    def set_option(self, option, value):
+        rc = N.lib().srg_set_option(self._h, int(option), float(value))
+        if rc != N.SRG_OK:
+            _raise(rc, f"srg_set_option({option}, {value}) failed")
+
     def close(self):
         if getattr(self, "_h", None):
             N.lib().srg_destroy(self._h)

@@ -23,7 +23,8 @@ def assert_parity(table, lat, loss):
 
 
 @pytest.mark.parametrize("fx", load_vectors(), ids=lambda f: f["name"])
-def test_golden_vectors(router, fx):
+def test_golden_vectors(scan_router, fx):
+    router = scan_router
     e = fixture_edges(fx)
     if fx["expect_code"]:
         with pytest.raises(NetGraphError) as ei:
@@ -61,8 +62,19 @@ CASES = [
 ]
 
 
+@pytest.fixture(params=["sparse", "dense"])
+def scan_router(request):
+    """Both tight-scan variants: essential-edge (sparse) and all-triples (dense)."""
+    r = Router(0)
+    r.set_option(N.SRG_OPT_SPARSE_THRESHOLD, 1.0 if request.param == "sparse" else 0.0)
+    r.expect_scan = N.SRG_SCAN_SPARSE if request.param == "sparse" else N.SRG_SCAN_DENSE
+    yield r
+    r.close()
+
+
 @pytest.mark.parametrize("kw", CASES, ids=lambda k: f"V{k['V']}_s{k['seed']}")
-def test_random_vs_oracle(router, kw):
+def test_random_vs_oracle(scan_router, kw):
+    router = scan_router
     kw = dict(kw)
     V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
     g = synth.random_graph(V, dens, seed, **kw)
@@ -74,10 +86,13 @@ def test_random_vs_oracle(router, kw):
             router.compute_shortest_paths(g, nodes)
         assert ei.value.code == e.code
         return
-    assert_parity(router.compute_shortest_paths(g, nodes), lat, loss)
+    tab = router.compute_shortest_paths(g, nodes)
+    assert tab.stats["scan_kind"] == router.expect_scan
+    assert_parity(tab, lat, loss)
 
 
-def test_subset_nodes_scrambled(router):
+def test_subset_nodes_scrambled(scan_router):
+    router = scan_router
     g = synth.random_graph(180, 0.1, 7, lat_hi=100)
     rng = np.random.default_rng(1)
     nodes = rng.permutation(180)[:77].tolist()
