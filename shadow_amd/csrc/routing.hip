@@ -258,6 +258,7 @@ __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, 
                           const uint32_t* __restrict__ nodes, uint32_t n, const uint64_t* __restrict__ self_lat,
                           const float* __restrict__ self_loss, uint64_t* __restrict__ out_lat,
                           float* __restrict__ out_loss, Flags* flags) {
+    // L == nullptr: out_loss was already written by k_loss_rows
     const size_t total = (size_t)n * n;
     uint32_t unreach = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -265,12 +266,12 @@ __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, 
         const uint32_t s = nodes[a], t = nodes[b];
         if (a == b) {
             out_lat[i] = self_lat[s];  // raw self-loop weight, no 1-(1-p) rounding
-            out_loss[i] = self_loss[s];
+            if (L) out_loss[i] = self_loss[s];
         } else {
             const K d = D[(size_t)s * ld + t];
             unreach |= d == KeyOps<K>::INF;
             out_lat[i] = (uint64_t)d;
-            out_loss[i] = L[a * ld + t];
+            if (L) out_loss[i] = L[a * ld + t];
         }
     }
     if (unreach) atomicOr(&flags->unreachable_used_pair, 1u);
@@ -524,6 +525,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
     unsigned long long nmulti = 0;
     uint64_t n_ess = 0;
     int scan_kind = SRG_SCAN_NONE;
+    bool loss_written = false;  // out_loss already filled by the per-row kernel
     float* Lfin = L0;
     double ms_scan = 0;
     if (n) {
@@ -588,26 +590,41 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
             k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
-            k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
             HIP_CHECK(hipGetLastError());
             ms_scan = tm.lap();
-            float* Lin = L0;
-            float* Lout = L1;
-            for (;;) {
+            const size_t lds_rows = (size_t)V * 12;
+            if (lds_rows <= 150 * 1024) {
+                // per-row Gauss-Seidel in LDS, writes out_loss directly
+                set_lds(k_loss_rows<K>, lds_rows);
                 HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
-                k_loss_round_sparse<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(
-                    PRED, Vp, DST, npad, nodes, n, V, ent_u, ent_w, ent_b, cscoff, cscent, Lin, Lout,
-                    &P.flags->changed);
+                k_loss_rows<K><<<n, 1024, lds_rows, st>>>(PRED, Vp, V, nodes, n, ent_u, ent_b, ent_w, DST, npad, cscoff,
+                                                          cscent, P.selfloss, out_loss, &P.flags->changed);
                 HIP_CHECK(hipGetLastError());
-                ++rounds;
-                uint32_t ch = 0;
-                HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                uint32_t sw = 0;
+                HIP_CHECK(hipMemcpyAsync(&sw, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipStreamSynchronize(st));
-                std::swap(Lin, Lout);
-                if (!ch) break;
-                if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
+                rounds = (int)sw;
+                loss_written = true;
+            } else {
+                k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+                float* Lin = L0;
+                float* Lout = L1;
+                for (;;) {
+                    HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
+                    k_loss_round_sparse<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(
+                        PRED, Vp, DST, npad, nodes, n, V, ent_u, ent_w, ent_b, cscoff, cscent, Lin, Lout,
+                        &P.flags->changed);
+                    HIP_CHECK(hipGetLastError());
+                    ++rounds;
+                    uint32_t ch = 0;
+                    HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                    HIP_CHECK(hipStreamSynchronize(st));
+                    std::swap(Lin, Lout);
+                    if (!ch) break;
+                    if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
+                }
+                Lfin = Lin;
             }
-            Lfin = Lin;
         } else {
             scan_kind = SRG_SCAN_DENSE;
             const size_t lds3 = (size_t)2 * KC * (TS + VE) * sizeof(K);
@@ -642,8 +659,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
 
     if (n) {
         HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
-        k_extract<K><<<grid_for((size_t)n * n), kThreads, 0, st>>>(D, Lfin, Vp, nodes, n, P.selflat, P.selfloss,
-                                                                   out_lat, out_loss, P.flags);
+        k_extract<K><<<grid_for((size_t)n * n), kThreads, 0, st>>>(D, loss_written ? nullptr : Lfin, Vp, nodes, n,
+                                                                   P.selflat, P.selfloss, out_lat, out_loss, P.flags);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
     }

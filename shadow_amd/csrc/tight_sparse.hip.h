@@ -332,4 +332,91 @@ __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ld
     if (changed) atomicOr(changed_flag, 1u);
 }
 
+// Per-row left fold in LDS (one workgroup per used source row, Gauss-Seidel sweeps).
+//   U[t] = tight predecessor u (or a marker), B[t] = 1 - loss(u,t), L[t] = path loss.
+// Sweeps update L in place until a full sweep changes nothing: that state satisfies every
+// L[t] = fold(L[U[t]], B[t]) at once, whose solution on the tight DAG is unique (induction on
+// depth), so it equals Dijkstra's lexicographic scores (mod.rs:305-331).  Writes the used
+// columns of the row straight into out_loss (diagonal = raw self-loop loss, mod.rs:216).
+constexpr uint32_t U_SELF = 0xFFFFFFFFu, U_NONE = 0xFFFFFFFEu, U_MULTI = 0xFFFFFFFDu;
+
+template <class K>
+__global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__ PRED, size_t ldp, uint32_t V,
+                                                     const uint32_t* __restrict__ nodes, uint32_t n,
+                                                     const uint32_t* __restrict__ ent_u,
+                                                     const float* __restrict__ ent_b, const K* __restrict__ ent_w,
+                                                     const K* __restrict__ DST, size_t npad,
+                                                     const uint32_t* __restrict__ csc_off,
+                                                     const uint32_t* __restrict__ csc_ent,
+                                                     const float* __restrict__ self_loss, float* __restrict__ out_loss,
+                                                     uint32_t* __restrict__ max_sweeps) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    uint32_t* U = reinterpret_cast<uint32_t*>(smem_raw);
+    float* Bf = reinterpret_cast<float*>(U + V);
+    float* L = Bf + V;
+    __shared__ uint32_t changed;
+    const uint32_t r = blockIdx.x;
+    const uint32_t s = nodes[r];
+    const uint32_t* prow = PRED + (size_t)r * ldp;
+    for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) {
+        const uint32_t p = prow[t];
+        uint32_t u;
+        float bb = 1.0f, l = 1.0f;
+        if (t == s) {
+            u = U_SELF;
+            l = 0.0f;  // Dijkstra start score PathProperties::default()
+        } else if (p == PRED_NONE) {
+            u = U_NONE;
+        } else if (p == PRED_MULTI) {
+            u = U_MULTI;
+        } else {
+            u = ent_u[p];
+            bb = ent_b[p];
+        }
+        U[t] = u;
+        Bf[t] = bb;
+        L[t] = l;
+    }
+    uint32_t sweeps = 0;
+    for (;;) {
+        if (threadIdx.x == 0) changed = 0;
+        __syncthreads();
+        uint32_t ch = 0;
+        for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) {
+            const uint32_t u = U[t];
+            if (u >= U_MULTI) {
+                if (u != U_MULTI) continue;
+                // several latency-tight predecessors: min over them (in-edges of t)
+                const K dst = DST[(size_t)t * npad + r];
+                float v = 1.0f;
+                for (uint32_t k = csc_off[t]; k < csc_off[t + 1]; ++k) {
+                    const uint32_t e = csc_ent[k];
+                    const uint32_t uu = ent_u[e];
+                    if (KeyOps<K>::add(DST[(size_t)uu * npad + r], ent_w[e]) != dst) continue;
+                    const float cnd = fold_loss(L[uu], ent_b[e]);
+                    v = cnd < v ? cnd : v;
+                }
+                if (v != L[t]) {
+                    L[t] = v;
+                    ch = 1;
+                }
+                continue;
+            }
+            const float v = fold_loss(L[u], Bf[t]);
+            if (v != L[t]) {
+                L[t] = v;
+                ch = 1;
+            }
+        }
+        if (ch) changed = 1;  // benign race: every writer stores 1
+        __syncthreads();
+        ++sweeps;
+        if (!changed) break;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(max_sweeps, sweeps);
+    float* orow = out_loss + (size_t)r * n;
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) orow[j] = (j == r) ? self_loss[s] : L[nodes[j]];
+}
+
 }  // namespace srg
