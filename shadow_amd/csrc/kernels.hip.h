@@ -31,7 +31,11 @@ struct KeyOps<uint32_t> {
     }
     __device__ __forceinline__ static uint32_t min2(uint32_t a, uint32_t b) { return a < b ? a : b; }
     __device__ __forceinline__ static uint32_t min3(uint32_t a, uint32_t b, uint32_t c) {
-        return min2(a, min2(b, c));  // v_min3_u32
+        // one v_min3_u32 (hipcc otherwise re-associates a min chain into a v_min tree:
+        // 1.75 instead of 1.5 VALU ops per relaxation)
+        uint32_t r;
+        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+        return r;
     }
 };
 
@@ -90,13 +94,16 @@ __device__ __forceinline__ void st16(K* p, const Vec16<K>& v) { stv<K, 16 / size
 
 // ---------------------------------------------------------------------------------------
 // Phase 1: close the pivot block D[kb][kb] (sequential k inside one workgroup).
+// The T x T block lives in registers (M x M per thread).  Step k needs only row k and
+// column k, so after updating, the owners of row k+1 / column k+1 publish them into a
+// parity double-buffered LDS strip (step k reads buffer k&1, writes buffer (k+1)&1):
+// one barrier per step and 2*T LDS words written instead of the whole block.
 template <class K, int T>
 __global__ void __launch_bounds__(256) fw_phase1(K* __restrict__ D, size_t ld, int kb) {
     using G = Geo<K, T>;
     constexpr int M = G::M;
-    constexpr int LDP = T + 16 / (int)sizeof(K);  // padded LDS row
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    K* P = reinterpret_cast<K*>(smem_raw);
+    __shared__ __attribute__((aligned(16))) K prow[2][T];
+    __shared__ __attribute__((aligned(16))) K pcol[2][T];
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
     K* base = D + (size_t)kb * T * ld + (size_t)kb * T;
     K c[M][M];
@@ -108,35 +115,52 @@ __global__ void __launch_bounds__(256) fw_phase1(K* __restrict__ D, size_t ld, i
             VecN<K, G::H> v = ldv<K, G::H>(base + (size_t)r * ld + G::rc(tx, h * G::H));
 #pragma unroll
             for (int e = 0; e < G::H; ++e) c[a][h * G::H + e] = v.v[e];
-            stv<K, G::H>(P + r * LDP + G::rc(tx, h * G::H), v);
+        }
+    }
+    // publish row 0 / column 0
+#pragma unroll
+    for (int a = 0; a < M; ++a) {
+        if (G::rc(ty, a) == 0) {
+#pragma unroll
+            for (int b = 0; b < M; ++b) prow[0][G::rc(tx, b)] = c[a][b];
+        }
+        if (G::rc(tx, a) == 0) {
+#pragma unroll
+            for (int b = 0; b < M; ++b) pcol[0][G::rc(ty, b)] = c[b][a];
         }
     }
     __syncthreads();
     for (int k = 0; k < T; ++k) {
+        const int p = k & 1;
         K colk[M], rowk[M];
 #pragma unroll
-        for (int a = 0; a < M; ++a) colk[a] = P[G::rc(ty, a) * LDP + k];
-#pragma unroll
         for (int h = 0; h < 2; ++h) {
-            VecN<K, G::H> v = ldv<K, G::H>(P + k * LDP + G::rc(tx, h * G::H));
+            VecN<K, G::H> vc = ldv<K, G::H>(&pcol[p][G::rc(ty, h * G::H)]);
+            VecN<K, G::H> vr = ldv<K, G::H>(&prow[p][G::rc(tx, h * G::H)]);
 #pragma unroll
-            for (int e = 0; e < G::H; ++e) rowk[h * G::H + e] = v.v[e];
+            for (int e = 0; e < G::H; ++e) {
+                colk[h * G::H + e] = vc.v[e];
+                rowk[h * G::H + e] = vr.v[e];
+            }
         }
 #pragma unroll
         for (int a = 0; a < M; ++a)
 #pragma unroll
             for (int b = 0; b < M; ++b) c[a][b] = KeyOps<K>::min2(c[a][b], KeyOps<K>::add(colk[a], rowk[b]));
-        // row k / column k are unchanged by iteration k (D[k][k] == 0), so writing every
-        // element here cannot race with this iteration's reads.
+        if (k + 1 < T) {
+            const int q = (k + 1) & 1;
 #pragma unroll
-        for (int a = 0; a < M; ++a)
+            for (int a = 0; a < M; ++a) {
+                if (G::rc(ty, a) == k + 1) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                VecN<K, G::H> v;
+                    for (int b = 0; b < M; ++b) prow[q][G::rc(tx, b)] = c[a][b];
+                }
+                if (G::rc(tx, a) == k + 1) {
 #pragma unroll
-                for (int e = 0; e < G::H; ++e) v.v[e] = c[a][h * G::H + e];
-                stv<K, G::H>(P + G::rc(ty, a) * LDP + G::rc(tx, h * G::H), v);
+                    for (int b = 0; b < M; ++b) pcol[q][G::rc(ty, b)] = c[b][a];
+                }
             }
+        }
         __syncthreads();
     }
 #pragma unroll
@@ -186,16 +210,67 @@ __device__ __forceinline__ void stage_chunk(K* __restrict__ At, K* __restrict__ 
 //   mode 3: blockIdx.(x,y) -> (I,J) skipping kb:  C = D[I][J], A = D[I][kb], B = D[kb][J]
 // With D[kb][kb] closed (phase 1) one product is exact for the panels; every product reads
 // all of A and B before the tile is stored, so the in-place row/col panel is race-free.
+//
+// Staging: the k range is cut into KC-wide chunks held in a double-buffered LDS image
+// (A transposed, B as is, rows padded by one 16-B vector).  Chunk i+1's global loads are
+// issued into registers before chunk i is computed and written to the other LDS buffer
+// after it (issue early / write late), so one barrier per chunk separates the phases.
 template <class K, int T, int KC>
-__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, int nb,
-                                                   int mode) {
+struct Stage {
+    static constexpr int VE = 16 / (int)sizeof(K);  // elements per 16-B vector
+    static constexpr int AV = T * KC / VE / 256;    // A vectors per thread per chunk
+    static constexpr int BV = KC * T / VE / 256;    // B vectors per thread per chunk
+    Vec16<K> a[AV], b[BV];
+};
+
+template <class K, int T, int KC>
+__device__ __forceinline__ void stage_load(Stage<K, T, KC>& sg, const K* __restrict__ A, const K* __restrict__ B,
+                                           size_t ld, const uint32_t* arow_idx, int k0) {
+    using S = Stage<K, T, KC>;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < S::AV; ++q) {
+        const int v = tid + 256 * q;
+        const int i = v / (KC / S::VE), kq = v % (KC / S::VE);
+        sg.a[q] = ld16(A + (size_t)arow_idx[i] * ld + k0 + kq * S::VE);
+    }
+#pragma unroll
+    for (int q = 0; q < S::BV; ++q) {
+        const int v = tid + 256 * q;
+        const int kk = v / (T / S::VE), jq = v % (T / S::VE);
+        sg.b[q] = ld16(B + (size_t)(k0 + kk) * ld + jq * S::VE);
+    }
+}
+
+template <class K, int T, int KC>
+__device__ __forceinline__ void stage_store(const Stage<K, T, KC>& sg, K* __restrict__ At, K* __restrict__ Bs) {
+    using S = Stage<K, T, KC>;
+    constexpr int LDP = T + S::VE;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < S::AV; ++q) {
+        const int v = tid + 256 * q;
+        const int i = v / (KC / S::VE), kq = v % (KC / S::VE);
+#pragma unroll
+        for (int e = 0; e < S::VE; ++e) At[(kq * S::VE + e) * LDP + i] = sg.a[q].v[e];
+    }
+#pragma unroll
+    for (int q = 0; q < S::BV; ++q) {
+        const int v = tid + 256 * q;
+        const int kk = v / (T / S::VE), jq = v % (T / S::VE);
+        st16(Bs + kk * LDP + jq * S::VE, sg.b[q]);
+    }
+}
+
+template <class K, int T, int KC>
+__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, int nb, int mode) {
     using G = Geo<K, T>;
     constexpr int M = G::M;
     constexpr int VE = 16 / (int)sizeof(K);
     constexpr int LDP = T + VE;
+    constexpr int BUF = 2 * KC * LDP;  // elements per LDS buffer (A^T + B)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    K* At = reinterpret_cast<K*>(smem_raw);
-    K* Bs = At + KC * LDP;
+    K* lds = reinterpret_cast<K*>(smem_raw);
     __shared__ uint32_t arow[T];
 
     int I, J;
@@ -214,11 +289,14 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
         J = blockIdx.x + (blockIdx.x >= (unsigned)kb);
     }
     K* C = D + (size_t)I * T * ld + (size_t)J * T;
-    const K* A = D + (size_t)kb * T;                     // column block kb, rows via arow
+    const K* A = D + (size_t)kb * T;                       // column block kb, rows via arow
     const K* B = D + (size_t)kb * T * ld + (size_t)J * T;  // row block kb, cols J
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
     if (tid < T) arow[tid] = I * T + tid;
+    __syncthreads();
 
+    Stage<K, T, KC> sg;
+    stage_load<K, T, KC>(sg, A, B, ld, arow, 0);
     K c[M][M];
 #pragma unroll
     for (int a = 0; a < M; ++a)
@@ -228,12 +306,15 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
 #pragma unroll
             for (int e = 0; e < G::H; ++e) c[a][h * G::H + e] = v.v[e];
         }
-    for (int k0 = 0; k0 < T; k0 += KC) {
-        __syncthreads();
-        stage_chunk<K, T, KC>(At, Bs, A, B - (size_t)0, ld, arow, k0);
-        // B chunk rows are (kb*T + k0 + kk): stage_chunk indexes B + (k0+kk)*ld
-        __syncthreads();
-#pragma unroll 2
+    stage_store<K, T, KC>(sg, lds, lds + KC * LDP);
+    __syncthreads();
+    constexpr int NCH = T / KC;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const K* At = lds + (ch & 1) * BUF;
+        const K* Bs = At + KC * LDP;
+        if (ch + 1 < NCH) stage_load<K, T, KC>(sg, A, B, ld, arow, (ch + 1) * KC);  // issue early
+#pragma unroll 4
         for (int kk = 0; kk < KC; kk += 2) {
             K a0[M], a1[M], b0[M], b1[M];
 #pragma unroll
@@ -257,6 +338,11 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
                     c[a][b] = KeyOps<K>::min3(c[a][b], KeyOps<K>::add(a0[a], b0[b]),
                                               KeyOps<K>::add(a1[a], b1[b]));
         }
+        if (ch + 1 < NCH) {  // write late into the other buffer
+            K* Ant = lds + ((ch + 1) & 1) * BUF;
+            stage_store<K, T, KC>(sg, Ant, Ant + KC * LDP);
+        }
+        __syncthreads();
     }
 #pragma unroll
     for (int a = 0; a < M; ++a)

@@ -471,9 +471,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
 
     // ---- blocked Floyd-Warshall ----
     constexpr int VE = 16 / (int)sizeof(K);
-    const size_t lds1 = (size_t)T * (T + VE) * sizeof(K);
-    const size_t lds2 = (size_t)2 * KC * (T + VE) * sizeof(K);
-    set_lds(fw_phase1<K, T>, lds1);
+    const size_t lds1 = 0;  // phase 1 uses static LDS only
+    const size_t lds2 = (size_t)4 * KC * (T + VE) * sizeof(K);  // double-buffered A^T + B chunks
     set_lds(fw_product<K, T, KC>, lds2);
     const bool prof = c.profiling && nb > 1;
     if (prof) {
