@@ -139,7 +139,7 @@ def main():
         relax = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = relax * OPS_PER_RELAX.get(kind, 1.5) / (avg_ms * 1e-3) / 1e12
         traffic, tsrc = load_traffic("fw_product")
-        roofline = {"bound": "valu", "kernel": "fw_product (FW phase 3)", "achieved": round(achieved, 3),
+        roofline = {"bound": "valu", "kernel": "fw_product<u32,128,32,5> (FW phase 3, non-lookahead tiles)", "achieved": round(achieved, 3),
                     "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),

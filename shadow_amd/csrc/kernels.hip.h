@@ -262,8 +262,12 @@ __device__ __forceinline__ void stage_store(const Stage<K, T, KC>& sg, K* __rest
     }
 }
 
-template <class K, int T, int KC>
-__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, int nb, int mode) {
+//   mode 4 (lookahead, kb+1 < nb): the tiles of the NEXT pivot's row (kb+1, J) and column
+//           (I, kb+1), skipping kb — they must be final before phase 1/2 of kb+1 start.
+//   mode 5 (kb+1 < nb): every other tile (I, J), I, J not in {kb, kb+1}.
+// MODE is a template parameter so each phase is its own kernel symbol in rocprof.
+template <class K, int T, int KC, int MODE>
+__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, int nb) {
     using G = Geo<K, T>;
     constexpr int M = G::M;
     constexpr int VE = 16 / (int)sizeof(K);
@@ -274,7 +278,7 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
     __shared__ uint32_t arow[T];
 
     int I, J;
-    if (mode == 2) {
+    if constexpr (MODE == 2) {
         const int b = blockIdx.x;
         if (b < nb - 1) {
             I = kb;
@@ -284,9 +288,22 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
             I += (I >= kb);
             J = kb;
         }
-    } else {
+    } else if constexpr (MODE == 3) {
         I = blockIdx.y + (blockIdx.y >= (unsigned)kb);
         J = blockIdx.x + (blockIdx.x >= (unsigned)kb);
+    } else if constexpr (MODE == 4) {
+        const int b = blockIdx.x;
+        if (b < nb - 1) {  // row kb+1, all J != kb
+            I = kb + 1;
+            J = b + (b >= kb);
+        } else {           // column kb+1, I not in {kb, kb+1}
+            I = b - (nb - 1);
+            I += (I >= kb) ? 2 : 0;
+            J = kb + 1;
+        }
+    } else {
+        I = blockIdx.y + ((blockIdx.y >= (unsigned)kb) ? 2 : 0);
+        J = blockIdx.x + ((blockIdx.x >= (unsigned)kb) ? 2 : 0);
     }
     K* C = D + (size_t)I * T * ld + (size_t)J * T;
     const K* A = D + (size_t)kb * T;                       // column block kb, rows via arow

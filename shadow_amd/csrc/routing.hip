@@ -325,6 +325,8 @@ struct srg_ctx {
     bool profiling = false;
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
+    hipStream_t aux_stream = nullptr;  // FW lookahead: phase 1/2 of the next pivot block
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;
     std::mutex mu;
     DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
     DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
@@ -340,6 +342,9 @@ struct srg_ctx {
                           &b_cscent, &b_gblk, &b_DST, &b_scantmp, &b_small, &b_entkw})
             b->release();
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
+        if (ev_a) (void)hipEventDestroy(ev_a);
+        if (ev_b) (void)hipEventDestroy(ev_b);
+        if (aux_stream) (void)hipStreamDestroy(aux_stream);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -473,8 +478,14 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
     constexpr int VE = 16 / (int)sizeof(K);
     const size_t lds1 = 0;  // phase 1 uses static LDS only
     const size_t lds2 = (size_t)4 * KC * (T + VE) * sizeof(K);  // double-buffered A^T + B chunks
-    set_lds(fw_product<K, T, KC>, lds2);
-    const bool prof = c.profiling && nb > 1;
+    set_lds(fw_product<K, T, KC, 2>, lds2);
+    set_lds(fw_product<K, T, KC, 3>, lds2);
+    set_lds(fw_product<K, T, KC, 4>, lds2);
+    set_lds(fw_product<K, T, KC, 5>, lds2);
+    // Lookahead schedule: for pivot block kb, phase 3 first updates the tiles of pivot kb+1's
+    // row and column (mode 4); phase 1 + phase 2 of kb+1 then run on the auxiliary stream
+    // while the remaining phase-3 tiles of kb (mode 5, the dominant kernel) run on `st`.
+    const bool prof = c.profiling && nb > 2;
     if (prof) {
         while (c.prof_events.size() < (size_t)2 * nb) {
             hipEvent_t e;
@@ -482,27 +493,47 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
             c.prof_events.push_back(e);
         }
     }
+    hipStream_t aux = c.aux_stream;
+    hipEvent_t ev_panels = c.ev_a, ev_pivot = c.ev_b;
+    uint64_t prof_relax = 0;
+    int prof_n = 0;
+    fw_phase1<K, T><<<1, 256, lds1, st>>>(D, Vp, 0);
+    if (nb > 1) fw_product<K, T, KC, 2><<<2 * (nb - 1), 256, lds2, st>>>(D, Vp, 0, nb);
     for (int kb = 0; kb < nb; ++kb) {
-        fw_phase1<K, T><<<1, 256, lds1, st>>>(D, Vp, kb);
-        if (nb > 1) {
-            fw_product<K, T, KC><<<2 * (nb - 1), 256, lds2, st>>>(D, Vp, kb, nb, 2);
-            if (prof) HIP_CHECK(hipEventRecord(c.prof_events[2 * kb], st));
-            fw_product<K, T, KC><<<dim3(nb - 1, nb - 1), 256, lds2, st>>>(D, Vp, kb, nb, 3);
-            if (prof) HIP_CHECK(hipEventRecord(c.prof_events[2 * kb + 1], st));
+        if (nb == 1) break;
+        if (kb + 1 < nb) {
+            fw_product<K, T, KC, 4><<<2 * nb - 3, 256, lds2, st>>>(D, Vp, kb, nb);
+            HIP_CHECK(hipEventRecord(ev_panels, st));
+            HIP_CHECK(hipStreamWaitEvent(aux, ev_panels, 0));
+            fw_phase1<K, T><<<1, 256, lds1, aux>>>(D, Vp, kb + 1);
+            fw_product<K, T, KC, 2><<<2 * (nb - 1), 256, lds2, aux>>>(D, Vp, kb + 1, nb);
+            HIP_CHECK(hipEventRecord(ev_pivot, aux));
+            if (nb > 2) {
+                if (prof) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
+                fw_product<K, T, KC, 5><<<dim3(nb - 2, nb - 2), 256, lds2, st>>>(D, Vp, kb, nb);
+                if (prof) {
+                    HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
+                    prof_relax += (uint64_t)(nb - 2) * (nb - 2) * T * T * T;
+                    ++prof_n;
+                }
+            }
+            HIP_CHECK(hipStreamWaitEvent(st, ev_pivot, 0));
+        } else {
+            fw_product<K, T, KC, 3><<<dim3(nb - 1, nb - 1), 256, lds2, st>>>(D, Vp, kb, nb);
         }
     }
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
     if (prof && stats) {
         double sum = 0;
-        for (int kb = 0; kb < nb; ++kb) {
+        for (int i = 0; i < prof_n; ++i) {
             float ms = 0;
-            HIP_CHECK(hipEventElapsedTime(&ms, c.prof_events[2 * kb], c.prof_events[2 * kb + 1]));
+            HIP_CHECK(hipEventElapsedTime(&ms, c.prof_events[2 * i], c.prof_events[2 * i + 1]));
             sum += ms;
         }
-        stats->prof_launches += nb;
+        stats->prof_launches += prof_n;
         stats->prof_kernel_ms += sum;
-        stats->prof_relaxations += (uint64_t)nb * (nb - 1) * (nb - 1) * T * T * T;
+        stats->prof_relaxations += prof_relax;
     }
 
     Flags fl{};
@@ -832,6 +863,9 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c->device = device;
         HIP_CHECK(hipSetDevice(device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&c->ev_a, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&c->ev_b, hipEventDisableTiming));
     });
     if (rc != SRG_OK) {
         delete c;
