@@ -7,8 +7,12 @@ edge list already resident in HBM -> every (latency_ns, packet_loss) of the 10^8
 written to HBM (dense W build, blocked FW, tight-DAG loss pass, extraction).
 
 value = source-SSSPs/s over the whole job (sources routed per second, all ranks).
-N > 1 (round 1): independent replicas, one full 10k-vertex APSP per rank per step
-("scaling": "weak"); the RCCL pivot-broadcast FW is the planned strong-scaling path.
+N > 1: ONE 10k-vertex RoutingInfo per step built by all N GPUs together ("scaling":
+"strong"): FW row blocks split across ranks with a per-pivot-block RCCL broadcast of the
+pivot row panel, each rank routes the sources whose rows it owns, and the output rows are
+exchanged point to point so that every rank ends with the whole table.
+--graph ba selects config C4 (50,000-vertex Barabasi-Albert, m=4; sparse batched
+Bellman-Ford with sources sharded across ranks + output row exchange).
 """
 import argparse
 import json
@@ -73,7 +77,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--graph", choices=["atlas", "ba"], default="atlas")
+    ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
+    ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     args = ap.parse_args()
+    if args.graph == "ba" and args.vertices == 10000 and "--vertices" not in sys.argv:
+        args.vertices = 50000
 
     import torch
     import torch.distributed as dist
@@ -87,27 +97,44 @@ def main():
     dev = torch.device("cuda", local)
 
     from shadow_amd import Router, synth
+    from shadow_amd import _native as N
     from shadow_amd.device import DeviceGraph, compute_shortest_paths_device, set_profiling
 
     V = args.vertices
     seed = args.seed if args.seed is not None else V
     t0 = time.time()
-    edges = synth.atlas_like(V, seed=seed)
-    log(f"[rank {rank}] generated atlas_like({V}, seed={seed}): {edges.num_edges} edges in {time.time()-t0:.1f}s")
+    if args.graph == "atlas":
+        edges = synth.atlas_like(V, seed=seed)
+        gdesc = f"C3 atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph"
+    else:
+        edges = synth.barabasi_albert(V, 4, seed=seed)
+        gdesc = f"C4 barabasi_albert({V}, m=4, seed={seed}): sparse undirected graph"
+    log(f"[rank {rank}] generated {gdesc}: {edges.num_edges} edges in {time.time()-t0:.1f}s")
     dg = DeviceGraph(edges, dev)
     nodes = torch.arange(V, dtype=torch.int32, device=dev)
     out_lat = torch.empty((V, V), dtype=torch.int64, device=dev)
     out_loss = torch.empty((V, V), dtype=torch.float32, device=dev)
-    router = Router(local)
+    strong = world > 1 and not args.replicas
+    if strong:
+        from shadow_amd import dist as sd
+        router = sd.init_router(local)
+        if args.no_gather:
+            router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
+    else:
+        router = Router(local)
+    if args.no_locality:
+        router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
 
     def step():
         return compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
 
     for i in range(args.warmup):
         s = step()
-        log(f"[rank {rank}] warmup {i}: {s['ms_total']:.2f} ms (fw {s['ms_fw']:.2f}, loss {s['ms_loss']:.2f}, "
-            f"scan {s['ms_scan']:.2f}, rounds {s['loss_rounds']}, multi {s['multi_pred_pairs']}, kind {s['path_kind']}, "
-            f"ess {s['essential_edges']} ({s['essential_edges'] / V / V:.3f} of V^2), scan_kind {s['scan_kind']})")
+        log(f"[rank {rank}] warmup {i}: {s['ms_total']:.2f} ms (build {s['ms_build']:.2f}, fw/bf {s['ms_fw']:.2f}, "
+            f"scan {s['ms_scan']:.2f}, loss {s['ms_loss']:.2f}, extract {s['ms_extract']:.2f}, "
+            f"exchange {s['ms_exchange']:.2f}; rounds {s['loss_rounds']}, multi {s['multi_pred_pairs']}, "
+            f"kind {s['path_kind']}, ess {s['essential_edges']} ({s['essential_edges'] / V / V:.3f} of V^2), "
+            f"scan_kind {s['scan_kind']}, relax {s['relaxations']}, local {s['local_sources']})")
     set_profiling(router, not args.no_profile)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -130,16 +157,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * V * args.steps / elapsed
+    value = (1 if strong else world) * V * args.steps / elapsed
 
     kind = s["path_kind"]
     roofline = None
-    if agg.get("prof_launches"):
+    if agg.get("prof_launches") and kind == 3:
+        # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
+        # (SURVEY §8d): arcs*16 + (V+1)*4 + V*12
+        arcs = int(((edges.src != edges.dst).sum()) * (1 if edges.directed else 2))
+        per_src = arcs * 16 + (V + 1) * 4 + V * 12
+        avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
+        srcs = agg["prof_relaxations"] / agg["prof_launches"]
+        achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford)",
+                    "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                    "frac": round(achieved / 8000.0, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 3),
+                    "bytes_per_source": per_src, "sources_per_launch": int(srcs)}
+    elif agg.get("prof_launches"):
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         relax = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = relax * OPS_PER_RELAX.get(kind, 1.5) / (avg_ms * 1e-3) / 1e12
         traffic, tsrc = load_traffic("fw_product")
-        roofline = {"bound": "valu", "kernel": "fw_product<u32,128,32,5> (FW phase 3, non-lookahead tiles)", "achieved": round(achieved, 3),
+        roofline = {"bound": "valu", "kernel": "fw_product<u32,128,32> (FW phase 3, non-lookahead tiles)", "achieved": round(achieved, 3),
                     "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
@@ -163,14 +202,15 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "source-SSSPs/s", "n_gpus": world, "steps": n,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32+f32" if kind == 0 else "u64+f32",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None,
+            "dtype": "u64+f32" if kind == 1 else "u32+f32",
             "data": "synthetic",
-            "config": {"workload": f"C3 atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph, "
-                                   f"all {V} nodes used, edge list resident in HBM",
+            "config": {"workload": f"{gdesc}, all {V} nodes used, edge list resident in HBM",
                        "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
-                       "parallelism": "replicas" if world > 1 else "single"},
+                       "parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single",
+                       "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
             "apsp_wall_ms": round(ms_per_step, 3),
-            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract")},
+            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange")},
             "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
             "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
             "roofline": roofline, "cpu_baseline": cpu,

@@ -65,7 +65,7 @@ typedef struct srg_stats {
     double ms_total;            /* entry -> return wall time */
     double ms_h2d;              /* host -> device copies (host entry points only) */
     double ms_build;            /* dense weight-matrix build + validation kernels */
-    double ms_fw;               /* blocked Floyd-Warshall on latency */
+    double ms_fw;               /* blocked Floyd-Warshall (dense) / batched Bellman-Ford (sparse) */
     double ms_scan;             /* essential-edge extraction + tight-predecessor scan */
     double ms_loss;             /* left-fold loss rounds over the tight DAG */
     double ms_extract;          /* used x used sub-matrix + diagonal self-loop overwrite */
@@ -82,11 +82,17 @@ typedef struct srg_stats {
     uint64_t prof_launches;     /* profiled launches */
     double prof_kernel_ms;      /* sum of their event-measured durations */
     uint64_t prof_relaxations;  /* relaxations those launches performed */
+    /* multi-rank (srg_comm_init*): this rank's view */
+    double ms_exchange;         /* output row exchange (all ranks end with every row) */
+    int32_t nranks;             /* ranks in the communicator (1 = single GPU) */
+    int32_t rank;               /* this rank */
+    uint64_t local_sources;     /* used sources routed by this rank */
 } srg_stats;
 
 #define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */
 #define SRG_PATH_DENSE_U64 1    /* dense FW, u64 latency keys */
 #define SRG_PATH_DIRECT 2       /* get_direct_paths */
+#define SRG_PATH_SPARSE_U32 3   /* sparse: batched lexicographic Bellman-Ford, u32 latency keys */
 
 #define SRG_SCAN_NONE 0         /* no used sources */
 #define SRG_SCAN_SPARSE 1       /* tight scan over the essential edges (default) */
@@ -104,6 +110,13 @@ void srg_destroy(srg_ctx* ctx);
  *                             tight scan is used (default 0.35; 0 forces the dense scan)      */
 #define SRG_OPT_PROFILING 1
 #define SRG_OPT_SPARSE_THRESHOLD 2
+#define SRG_OPT_GATHER_OUTPUT 3   /* multi-rank: 1 (default) = every rank ends with all rows;
+                                     0 = each rank fills only the rows of the sources it owns */
+#define SRG_OPT_ALGORITHM 4       /* SRG_ALGO_*: how compute_shortest_paths routes */
+#define SRG_ALGO_AUTO 0           /* sparse when V >= 2048 and arcs * 32 < V^2, else dense */
+#define SRG_ALGO_DENSE 1          /* blocked FW + tight-DAG loss pass */
+#define SRG_ALGO_SPARSE 2         /* batched lexicographic Bellman-Ford over CSR */
+#define SRG_OPT_SPARSE_LOCALITY 5 /* sparse: 1 (default) = batch sources in BFS order, 0 = in `nodes` order */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).
@@ -150,6 +163,24 @@ uint32_t srg_graph_node_id(const srg_graph* g, uint32_t index);
 void srg_graph_node_bandwidth(const srg_graph* g, uint32_t index,
                               uint64_t* down_bits, int* has_down,
                               uint64_t* up_bits, int* has_up);
+
+/* ---- multi-GPU: one process (or thread) per GPU, SPMD -------------------------------
+ * After srg_comm_init*, every rank calls srg_compute_shortest_paths[_device] with the SAME
+ * graph and nodes.  FW row blocks are split across ranks with a per-pivot-block broadcast of
+ * the pivot row panel; each rank routes the used sources whose rows it owns; output rows are
+ * exchanged point to point (SRG_OPT_GATHER_OUTPUT).  The reference has no multi-process path
+ * (rayon threads only, mod.rs:190-208): this is new, MI355X-side design.    */
+#define SRG_UNIQUE_ID_BYTES 128
+/* RCCL (over xGMI): rank 0 creates the id, the caller shares it (e.g. torch.distributed). */
+int srg_comm_unique_id(unsigned char id[SRG_UNIQUE_ID_BYTES], char* errbuf, size_t errlen);
+int srg_comm_init(srg_ctx* ctx, int nranks, int rank, const unsigned char id[SRG_UNIQUE_ID_BYTES],
+                  char* errbuf, size_t errlen);
+/* In-process group: several contexts of ONE process (threads; may share one GPU). */
+typedef struct srg_local_group srg_local_group;
+int srg_local_group_create(int nranks, srg_local_group** out);
+void srg_local_group_release(srg_local_group* g);
+int srg_comm_init_local(srg_ctx* ctx, srg_local_group* g, int rank, char* errbuf, size_t errlen);
+int srg_comm_size(srg_ctx* ctx, int* nranks, int* rank);
 
 /* Library build/version string. */
 const char* srg_version(void);

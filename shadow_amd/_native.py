@@ -25,9 +25,17 @@ SRG_ERR_INTERNAL = 10
 SRG_PATH_DENSE_U32 = 0
 SRG_PATH_DENSE_U64 = 1
 SRG_PATH_DIRECT = 2
+SRG_PATH_SPARSE_U32 = 3
 
 SRG_OPT_PROFILING = 1
 SRG_OPT_SPARSE_THRESHOLD = 2
+SRG_OPT_GATHER_OUTPUT = 3
+SRG_OPT_ALGORITHM = 4
+SRG_OPT_SPARSE_LOCALITY = 5
+SRG_ALGO_AUTO = 0
+SRG_ALGO_DENSE = 1
+SRG_ALGO_SPARSE = 2
+SRG_UNIQUE_ID_BYTES = 128
 
 SRG_SCAN_NONE = 0
 SRG_SCAN_SPARSE = 1
@@ -71,6 +79,10 @@ class Stats(ctypes.Structure):
         ("prof_launches", ctypes.c_uint64),
         ("prof_kernel_ms", ctypes.c_double),
         ("prof_relaxations", ctypes.c_uint64),
+        ("ms_exchange", ctypes.c_double),
+        ("nranks", ctypes.c_int32),
+        ("rank", ctypes.c_int32),
+        ("local_sources", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -82,7 +94,8 @@ EXPORTS = [
     "srg_create", "srg_destroy", "srg_set_option", "srg_compute_shortest_paths", "srg_compute_shortest_paths_device",
     "srg_get_direct_paths", "srg_graph_parse_gml", "srg_graph_free", "srg_graph_edge_list",
     "srg_graph_num_vertices", "srg_graph_num_edges", "srg_graph_directed", "srg_graph_node_index",
-    "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version",
+    "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version", "srg_comm_unique_id", "srg_comm_init",
+    "srg_local_group_create", "srg_local_group_release", "srg_comm_init_local", "srg_comm_size",
 ]
 
 _lib = None
@@ -143,5 +156,17 @@ def lib():
                                            c.POINTER(c.c_int)]
     L.srg_version.restype = c.c_char_p
     L.srg_version.argtypes = []
+    L.srg_comm_unique_id.restype = c.c_int
+    L.srg_comm_unique_id.argtypes = [c.c_char_p, c.c_char_p, c.c_size_t]
+    L.srg_comm_init.restype = c.c_int
+    L.srg_comm_init.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_char_p, c.c_char_p, c.c_size_t]
+    L.srg_local_group_create.restype = c.c_int
+    L.srg_local_group_create.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
+    L.srg_local_group_release.restype = None
+    L.srg_local_group_release.argtypes = [c.c_void_p]
+    L.srg_comm_init_local.restype = c.c_int
+    L.srg_comm_init_local.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_char_p, c.c_size_t]
+    L.srg_comm_size.restype = c.c_int
+    L.srg_comm_size.argtypes = [c.c_void_p, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     _lib = L
     return L

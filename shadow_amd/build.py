@@ -12,8 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libshadow_routing.so")
-SOURCES = [os.path.join(CSRC, "routing.hip"), os.path.join(CSRC, "gml.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "kernels.hip.h"), os.path.join(CSRC, "tight_sparse.hip.h"), os.path.join(ROOT, "include", "shadow_routing.h")]
+SOURCES = [os.path.join(CSRC, "routing.hip"), os.path.join(CSRC, "gml.cpp"), os.path.join(CSRC, "comm.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "kernels.hip.h"), os.path.join(CSRC, "tight_sparse.hip.h"), os.path.join(CSRC, "comm.h"), os.path.join(CSRC, "sparse.hip.h"), os.path.join(ROOT, "include", "shadow_routing.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SRG_OFFLOAD_ARCH", "gfx950")
 
@@ -40,7 +40,7 @@ def build(force=False, verbose=True):
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs
+    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-ldl", "-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

@@ -1,0 +1,44 @@
+// comm.h — collectives used by the multi-GPU routing build.
+//
+// The reference has no communication at all (rayon threads in one process, mod.rs:190-208);
+// these are the exchange steps of the MI355X design:
+//   bcast      FW pivot row panel, in place, root = owner of the pivot block
+//   allgatherv row-block segments (essential-edge bitmask, output rows): every rank holds the
+//              same layout and contributes [offs[rank], offs[rank] + lens[rank]) bytes
+//   allreduce_max_u32  small flags (u32 certification, unreachable pairs)
+// All calls are stream-ordered: they start when `s` reaches them and later work on `s` sees
+// the result, like RCCL.  Every rank issues the same sequence of calls.
+//
+// Backends: RCCL over xGMI (one process per GPU, librccl loaded with dlopen on first use), and
+// an in-process group (several contexts in one process, e.g. several ranks on one GPU) used to
+// test the distributed schedule bit-exactly where only one GPU is available.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace srg {
+
+struct Comm {
+    int rank = 0, nranks = 1;
+    virtual ~Comm() = default;
+    virtual const char* kind() const = 0;
+    virtual void bcast(void* buf, size_t bytes, int root, hipStream_t s) = 0;
+    virtual void allgatherv(void* buf, const size_t* offs, const size_t* lens, hipStream_t s) = 0;
+    virtual void allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t s) = 0;
+};
+
+// RCCL: unique id (128 bytes) from rank 0, shared by the caller, then init on every rank.
+// Return "" on success, else an error message.
+std::string rccl_unique_id(unsigned char out[128]);
+std::string rccl_create(int nranks, int rank, const unsigned char id[128], int device, Comm** out);
+
+// In-process group of `nranks` ranks (threads of one process); each rank attaches one context.
+struct LocalGroup;
+LocalGroup* local_group_create(int nranks);
+void local_group_release(LocalGroup* g);  // refcounted: the group and each attached comm
+std::string local_create(LocalGroup* g, int rank, int device, Comm** out);
+
+}  // namespace srg

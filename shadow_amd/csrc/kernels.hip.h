@@ -204,10 +204,11 @@ __device__ __forceinline__ void stage_chunk(K* __restrict__ At, K* __restrict__ 
     }
 }
 
-// Phase 2 / 3: C = min(C, A (x) B) over the kb pivot block (min-plus product).
-//   mode 2: blockIdx.x <  nb-1 : row panel  C = D[kb][J],  A = D[kb][kb], B = C
-//           blockIdx.x >= nb-1 : col panel  C = D[I][kb],  A = C,         B = D[kb][kb]
-//   mode 3: blockIdx.(x,y) -> (I,J) skipping kb:  C = D[I][J], A = D[I][kb], B = D[kb][J]
+// Phase 2 / 3: C = min(C, A (x) B) over the kb pivot block (min-plus product), for the
+// tiles (I, J) of a TileSet:  C = D[I][J],  A = D[I][kb],  B = D[kb][J].
+//   row panel (I = kb):  A = D[kb][kb] (the closed pivot tile), B = C
+//   col panel (J = kb):  A = C,  B = D[kb][kb]
+//   phase 3:             I, J != kb
 // With D[kb][kb] closed (phase 1) one product is exact for the panels; every product reads
 // all of A and B before the tile is stored, so the in-place row/col panel is race-free.
 //
@@ -262,12 +263,23 @@ __device__ __forceinline__ void stage_store(const Stage<K, T, KC>& sg, K* __rest
     }
 }
 
-//   mode 4 (lookahead, kb+1 < nb): the tiles of the NEXT pivot's row (kb+1, J) and column
-//           (I, kb+1), skipping kb — they must be final before phase 1/2 of kb+1 start.
-//   mode 5 (kb+1 < nb): every other tile (I, J), I, J not in {kb, kb+1}.
-// MODE is a template parameter so each phase is its own kernel symbol in rocprof.
-template <class K, int T, int KC, int MODE>
-__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, int nb) {
+// A TileSet is a rectangle of tiles minus at most two whole rows and two whole columns
+// (pivot rows/columns handled elsewhere):  kept row y -> r0 + y, stepping over rx0 < rx1
+// (-1 = none); kept column x likewise.  grid = (kept columns, kept rows).
+struct TileSet {
+    int r0, rx0, rx1;
+    int c0, cx0, cx1;
+};
+
+__device__ __forceinline__ int tile_kept(int base, int idx, int x0, int x1) {
+    int v = base + idx;
+    if (x0 >= 0 && v >= x0) ++v;
+    if (x1 >= 0 && v >= x1) ++v;
+    return v;
+}
+
+template <class K, int T, int KC>
+__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
     using G = Geo<K, T>;
     constexpr int M = G::M;
     constexpr int VE = 16 / (int)sizeof(K);
@@ -277,34 +289,8 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
     K* lds = reinterpret_cast<K*>(smem_raw);
     __shared__ uint32_t arow[T];
 
-    int I, J;
-    if constexpr (MODE == 2) {
-        const int b = blockIdx.x;
-        if (b < nb - 1) {
-            I = kb;
-            J = b + (b >= kb);
-        } else {
-            I = (b - (nb - 1));
-            I += (I >= kb);
-            J = kb;
-        }
-    } else if constexpr (MODE == 3) {
-        I = blockIdx.y + (blockIdx.y >= (unsigned)kb);
-        J = blockIdx.x + (blockIdx.x >= (unsigned)kb);
-    } else if constexpr (MODE == 4) {
-        const int b = blockIdx.x;
-        if (b < nb - 1) {  // row kb+1, all J != kb
-            I = kb + 1;
-            J = b + (b >= kb);
-        } else {           // column kb+1, I not in {kb, kb+1}
-            I = b - (nb - 1);
-            I += (I >= kb) ? 2 : 0;
-            J = kb + 1;
-        }
-    } else {
-        I = blockIdx.y + ((blockIdx.y >= (unsigned)kb) ? 2 : 0);
-        J = blockIdx.x + ((blockIdx.x >= (unsigned)kb) ? 2 : 0);
-    }
+    const int I = tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1);
+    const int J = tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1);
     K* C = D + (size_t)I * T * ld + (size_t)J * T;
     const K* A = D + (size_t)kb * T;                       // column block kb, rows via arow
     const K* B = D + (size_t)kb * T * ld + (size_t)J * T;  // row block kb, cols J

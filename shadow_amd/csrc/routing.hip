@@ -27,6 +27,8 @@
 #include "../../include/shadow_routing.h"
 #include "kernels.hip.h"
 #include "tight_sparse.hip.h"
+#include "comm.h"
+#include "sparse.hip.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -253,28 +255,45 @@ __global__ void k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uin
     if (c) atomicAdd(out, c);
 }
 
+// Used x used outputs for the local source rows: row a (source snodes[a]) goes to output row
+// rowpos[a]; columns are the full `cols` (= nodes) list.  L == nullptr: out_loss was already
+// written by k_loss_rows.
 template <class K>
 __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, size_t ld,
-                          const uint32_t* __restrict__ nodes, uint32_t n, const uint64_t* __restrict__ self_lat,
-                          const float* __restrict__ self_loss, uint64_t* __restrict__ out_lat,
-                          float* __restrict__ out_loss, Flags* flags) {
-    // L == nullptr: out_loss was already written by k_loss_rows
-    const size_t total = (size_t)n * n;
+                          const uint32_t* __restrict__ snodes, uint32_t nloc, const uint32_t* __restrict__ cols,
+                          uint32_t ncols, const uint32_t* __restrict__ rowpos,
+                          const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
+                          uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags) {
+    const size_t total = (size_t)nloc * ncols;
     uint32_t unreach = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t a = i / n, b = i - a * n;
-        const uint32_t s = nodes[a], t = nodes[b];
-        if (a == b) {
-            out_lat[i] = self_lat[s];  // raw self-loop weight, no 1-(1-p) rounding
-            if (L) out_loss[i] = self_loss[s];
+        const size_t a = i / ncols, b = i - a * ncols;
+        const uint32_t s = snodes[a], t = cols[b], p = rowpos[a];
+        const size_t o = (size_t)p * ncols + b;
+        if (p == b) {
+            out_lat[o] = self_lat[s];  // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
+            if (L) out_loss[o] = self_loss[s];
         } else {
             const K d = D[(size_t)s * ld + t];
             unreach |= d == KeyOps<K>::INF;
-            out_lat[i] = (uint64_t)d;
-            if (L) out_loss[i] = L[a * ld + t];
+            out_lat[o] = (uint64_t)d;
+            if (L) out_loss[o] = L[a * ld + t];
         }
     }
     if (unreach) atomicOr(&flags->unreachable_used_pair, 1u);
+}
+
+// Row packing for the output exchange when a rank's rows are not one contiguous range:
+// pack: stage[q] = out[pos[q]]  /  unpack: out[pos[q]] = stage[q]   (rows of `row_bytes`)
+__global__ void k_rows_copy(const unsigned char* __restrict__ src, unsigned char* __restrict__ dst,
+                            const uint32_t* __restrict__ pos, uint32_t nrows, size_t row_bytes, int unpack) {
+    const size_t words = row_bytes / 4;
+    for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
+        const size_t sr = unpack ? q : pos[q], dr = unpack ? pos[q] : q;
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(src + sr * row_bytes);
+        uint32_t* b = reinterpret_cast<uint32_t*>(dst + dr * row_bytes);
+        for (size_t w = threadIdx.x; w < words; w += blockDim.x) b[w] = a[w];
+    }
 }
 
 __global__ void k_positions(const uint32_t* __restrict__ nodes, uint32_t n, int32_t* __restrict__ pos) {
@@ -323,29 +342,37 @@ struct srg_ctx {
     int device = 0;
     double sparse_threshold = 0.35;  // essential-edge density above which the dense scan is used
     bool profiling = false;
+    bool gather_output = true;       // multi-rank: every rank ends with all n x n outputs
+    int algorithm = SRG_ALGO_AUTO;   // dense FW / sparse batched Bellman-Ford
+    bool sparse_locality = true;     // sparse: batch sources in BFS order
+    srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
-    hipStream_t aux_stream = nullptr;  // FW lookahead: phase 1/2 of the next pivot block
-    hipEvent_t ev_a = nullptr, ev_b = nullptr;
+    hipStream_t aux_stream = nullptr;   // FW lookahead: phase 1/2 of the next pivot block
+    hipStream_t comm_stream = nullptr;  // pivot-panel broadcasts (multi-rank)
+    hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
     std::mutex mu;
     DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
     DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
     DevBuf b_stats, b_flags, b_multi, b_pos, b_cnt;
     // sparse tight scan
-    DevBuf b_ecnt, b_gflag, b_eoff, b_goff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu,
-        b_grpe, b_cscent, b_gblk, b_DST, b_scantmp, b_small, b_entkw;
+    DevBuf b_ecnt, b_eoff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu, b_grpe, b_cscent,
+        b_gblk, b_DST, b_scantmp, b_ess;
+    // multi-rank: local sources, their output rows, exchange staging
+    DevBuf b_lnodes, b_lpos, b_allpos, b_stage, b_red, b_outoff, b_outdst;
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
-                          &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_gflag, &b_eoff, &b_goff,
-                          &b_indeg, &b_cscoff, &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe,
-                          &b_cscent, &b_gblk, &b_DST, &b_scantmp, &b_small, &b_entkw})
+                          &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
+                          &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
+                          &b_scantmp, &b_ess, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst})
             b->release();
+        delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
-        if (ev_a) (void)hipEventDestroy(ev_a);
-        if (ev_b) (void)hipEventDestroy(ev_b);
-        if (aux_stream) (void)hipStreamDestroy(aux_stream);
-        if (stream) (void)hipStreamDestroy(stream);
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d})
+            if (e) (void)hipEventDestroy(e);
+        for (hipStream_t s : {aux_stream, comm_stream, stream})
+            if (s) (void)hipStreamDestroy(s);
     }
 };
 
@@ -387,6 +414,7 @@ struct Prelude {
     uint64_t* selflat;
     float* selfloss;
     Flags* flags;
+    std::vector<uint32_t> nodes_h;  // host copy of `nodes` (partitioning, error text)
 };
 
 Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, hipStream_t st,
@@ -409,8 +437,10 @@ Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                                                        P.selflat, P.selfloss, es);
     HIP_CHECK(hipGetLastError());
     Flags fl;
+    P.nodes_h.resize(n);
     HIP_CHECK(hipMemcpyAsync(&P.es, es, sizeof(EdgeStats), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
+    if (n) HIP_CHECK(hipMemcpyAsync(P.nodes_h.data(), nodes, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     if (P.es.bad_endpoint) fail(SRG_ERR_ARG, "edge endpoint out of range (>= num_vertices)");
     if (fl.bad_node & 1) fail(SRG_ERR_ARG, "node index out of range (>= num_vertices)");
@@ -419,12 +449,11 @@ Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         if (P.es.lat_overflow)
             fail(SRG_ERR_LATENCY_RANGE, "The resulting value is outside of the bounds [0, 18446744073709551615]");
         // there must be a single self-loop for each node (mod.rs:215-216), in `nodes` order
-        std::vector<uint32_t> cnt(V), nd(n);
+        std::vector<uint32_t> cnt(V);
         HIP_CHECK(hipMemcpyAsync(cnt.data(), P.selfcnt, (size_t)V * 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(nd.data(), nodes, (size_t)n * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t v = nd[i];
+            const uint32_t v = P.nodes_h[i];
             if (cnt[v] == 1) continue;
             const uint32_t id = node_gml_id(g, v, st);
             if (cnt[v] == 0)
@@ -448,16 +477,158 @@ struct Timer {
     }
 };
 
+// ---- distribution plan --------------------------------------------------
+// G ranks, 1-D row blocks: rank r owns FW row blocks [r*nb/G, (r+1)*nb/G) (rows of D, and so
+// the D rows of the used sources in them).  Each rank routes the used sources whose vertex it
+// owns; outputs are exchanged row-wise at the end.  G = 1 is the single-GPU case.
+struct Plan {
+    int G = 1, g = 0, nb = 0, rb0 = 0, rb1 = 0;
+    uint32_t u0 = 0, u1 = 0;               // own vertex rows, clipped to [0, V)
+    std::vector<int> blk_lo;               // [G+1] first row block per rank
+    std::vector<uint32_t> lnodes, lpos;    // own used sources (vertex) and their positions in `nodes`
+    std::vector<uint32_t> cnt, first;      // per rank: source count and first row in rank order
+    std::vector<uint32_t> allpos;          // positions of every rank's sources, in rank order
+    bool contiguous = true;                // allpos == 0..n-1 (rows already in rank order)
+    int owner(int b) const { return (int)(std::upper_bound(blk_lo.begin(), blk_lo.end(), b) - blk_lo.begin()) - 1; }
+    bool own(int b) const { return b >= rb0 && b < rb1; }
+};
+
+Plan make_plan(int G, int g, uint32_t V, int T, const std::vector<uint32_t>& nodes_h) {
+    Plan p;
+    p.G = G;
+    p.g = g;
+    p.nb = (int)(((size_t)V + T - 1) / T);
+    p.blk_lo.resize(G + 1);
+    for (int r = 0; r <= G; ++r) p.blk_lo[r] = (int)((int64_t)r * p.nb / G);
+    p.rb0 = p.blk_lo[g];
+    p.rb1 = p.blk_lo[g + 1];
+    p.u0 = std::min<uint32_t>(V, (uint32_t)p.rb0 * T);
+    p.u1 = std::min<uint32_t>(V, (uint32_t)p.rb1 * T);
+    std::vector<std::vector<uint32_t>> per(G);
+    for (uint32_t r = 0; r < nodes_h.size(); ++r) per[p.owner((int)(nodes_h[r] / T))].push_back(r);
+    p.cnt.resize(G);
+    p.first.resize(G);
+    uint32_t acc = 0;
+    for (int r = 0; r < G; ++r) {
+        p.cnt[r] = (uint32_t)per[r].size();
+        p.first[r] = acc;
+        for (uint32_t q : per[r]) {
+            p.contiguous &= (q == acc);
+            p.allpos.push_back(q);
+            ++acc;
+        }
+    }
+    p.lpos = per[g];
+    for (uint32_t q : p.lpos) p.lnodes.push_back(nodes_h[q]);
+    return p;
+}
+
 constexpr int KC = 32;
+
+// tiles of one min-plus product launch: rows [ra, rb) minus {rx...}, cols [ca, cb) minus {cx...}
+template <class K, int T>
+void fw_tiles(K* D, size_t ld, int kb, int ra, int rb, std::initializer_list<int> rx, int ca, int cb,
+              std::initializer_list<int> cx, size_t lds, hipStream_t s) {
+    auto norm = [](int a, int b, std::initializer_list<int> x, int& x0, int& x1) {
+        std::vector<int> v;
+        for (int e : x)
+            if (e >= a && e < b && std::find(v.begin(), v.end(), e) == v.end()) v.push_back(e);
+        std::sort(v.begin(), v.end());
+        x0 = v.size() > 0 ? v[0] : -1;
+        x1 = v.size() > 1 ? v[1] : -1;
+        return std::max(0, b - a - (int)v.size());
+    };
+    TileSet ts;
+    const int nr = norm(ra, rb, rx, ts.rx0, ts.rx1);
+    const int nc = norm(ca, cb, cx, ts.cx0, ts.cx1);
+    if (nr <= 0 || nc <= 0) return;
+    ts.r0 = ra;
+    ts.c0 = ca;
+    fw_product<K, T, KC><<<dim3(nc, nr), 256, lds, s>>>(D, ld, kb, ts);
+}
+
+// Blocked Floyd-Warshall over the rank's row blocks with a one-block lookahead:
+//   pivot kb+1's owner updates row kb+1 (w.r.t. kb) first, closes pivot kb+1 and its row
+//   panel on the auxiliary stream, and broadcasts the panel (T x Vp keys, in place) while
+//   every rank finishes the remaining tiles of kb; then each rank updates its own column
+//   panel of kb+1.  Single GPU: the same schedule with the broadcast elided.
+template <class K, int T>
+void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax, int& prof_n) {
+    const int nb = pl.nb;
+    const size_t lds = (size_t)4 * KC * (T + 16 / (int)sizeof(K)) * sizeof(K);  // double-buffered A^T + B
+    set_lds(fw_product<K, T, KC>, lds);
+    const bool multi = c.comm && c.comm->nranks > 1;
+    const bool prof = c.profiling && nb > 2;
+    if (prof) {
+        while (c.prof_events.size() < (size_t)2 * nb) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            c.prof_events.push_back(e);
+        }
+    }
+    hipStream_t aux = c.aux_stream, cs = c.comm_stream;
+    const size_t panel_bytes = (size_t)T * Vp * sizeof(K);
+    auto panel = [&](int b) { return (void*)(D + (size_t)b * T * Vp); };
+    const int r0 = pl.rb0, r1 = pl.rb1;
+    // pivot 0
+    if (pl.own(0)) {
+        fw_phase1<K, T><<<1, 256, 0, st>>>(D, Vp, 0);
+        fw_tiles<K, T>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st);
+    }
+    if (multi) {
+        HIP_CHECK(hipEventRecord(c.ev_c, st));
+        HIP_CHECK(hipStreamWaitEvent(cs, c.ev_c, 0));
+        c.comm->bcast(panel(0), panel_bytes, pl.owner(0), cs);
+        HIP_CHECK(hipEventRecord(c.ev_c, cs));
+        HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
+    }
+    fw_tiles<K, T>(D, Vp, 0, r0, r1, {0}, 0, 1, {}, lds, st);
+    for (int kb = 0; kb < nb; ++kb) {
+        if (kb + 1 >= nb) {
+            fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb}, 0, nb, {kb}, lds, st);
+            break;
+        }
+        const int k1 = kb + 1;
+        if (pl.own(k1)) fw_tiles<K, T>(D, Vp, kb, k1, k1 + 1, {}, 0, nb, {kb}, lds, st);  // row k1
+        fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb, k1}, k1, k1 + 1, {}, lds, st);             // own col k1
+        HIP_CHECK(hipEventRecord(c.ev_a, st));
+        HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
+        if (pl.own(k1)) {
+            fw_phase1<K, T><<<1, 256, 0, aux>>>(D, Vp, k1);
+            fw_tiles<K, T>(D, Vp, k1, k1, k1 + 1, {}, 0, nb, {k1}, lds, aux);  // row panel k1
+        }
+        if (multi) {
+            HIP_CHECK(hipEventRecord(c.ev_b, aux));
+            HIP_CHECK(hipStreamWaitEvent(cs, c.ev_b, 0));
+            c.comm->bcast(panel(k1), panel_bytes, pl.owner(k1), cs);
+            HIP_CHECK(hipEventRecord(c.ev_c, cs));
+            if (!pl.own(k1)) HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));  // pivot tile arrives in the panel
+        }
+        fw_tiles<K, T>(D, Vp, k1, r0, r1, {k1}, k1, k1 + 1, {}, lds, aux);  // own col panel k1
+        HIP_CHECK(hipEventRecord(c.ev_d, aux));
+        // the remaining tiles of kb (the dominant kernel), overlapped with the above
+        const int nr = (r1 - r0) - (pl.own(kb) ? 1 : 0) - (pl.own(k1) ? 1 : 0);
+        const bool timed = prof && nr > 0 && nb > 2;
+        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
+        fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb, k1}, 0, nb, {kb, k1}, lds, st);
+        if (timed) {
+            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
+            prof_relax += (uint64_t)nr * (nb - 2) * T * T * T;
+            ++prof_n;
+        }
+        HIP_CHECK(hipStreamWaitEvent(st, c.ev_d, 0));
+        if (multi) HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));  // panel k1 sent/received before it is reused
+    }
+}
 
 // Dense path for key type K. Returns false (u32 only) when certification fails.
 template <class K, int T>
-bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
+bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
                float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats) {
     const uint32_t V = g.V;
     const size_t Vp = ((size_t)V + T - 1) / T * T;
-    const int nb = (int)(Vp / T);
     const size_t VV = Vp * Vp;
+    const bool multi = c.comm && c.comm->nranks > 1;
     Timer tm(st);
 
     K* W = (K*)c.b_W.get(VV * sizeof(K));
@@ -471,60 +642,24 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
         k_w_loss<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, W, WL, Vp);
     }
     k_init_d<K><<<grid_for(VV), kThreads, 0, st>>>(W, D, Vp);
+    // local sources and their output rows
+    const uint32_t nloc = (uint32_t)pl.lnodes.size();
+    uint32_t* lnodes = (uint32_t*)c.b_lnodes.get(std::max<size_t>(nloc, 1) * 4);
+    uint32_t* lpos = (uint32_t*)c.b_lpos.get(std::max<size_t>(nloc, 1) * 4);
+    if (nloc) {
+        HIP_CHECK(hipMemcpyAsync(lnodes, pl.lnodes.data(), (size_t)nloc * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(lpos, pl.lpos.data(), (size_t)nloc * 4, hipMemcpyHostToDevice, st));
+    }
     HIP_CHECK(hipGetLastError());
     const double ms_build = tm.lap();
 
     // ---- blocked Floyd-Warshall ----
-    constexpr int VE = 16 / (int)sizeof(K);
-    const size_t lds1 = 0;  // phase 1 uses static LDS only
-    const size_t lds2 = (size_t)4 * KC * (T + VE) * sizeof(K);  // double-buffered A^T + B chunks
-    set_lds(fw_product<K, T, KC, 2>, lds2);
-    set_lds(fw_product<K, T, KC, 3>, lds2);
-    set_lds(fw_product<K, T, KC, 4>, lds2);
-    set_lds(fw_product<K, T, KC, 5>, lds2);
-    // Lookahead schedule: for pivot block kb, phase 3 first updates the tiles of pivot kb+1's
-    // row and column (mode 4); phase 1 + phase 2 of kb+1 then run on the auxiliary stream
-    // while the remaining phase-3 tiles of kb (mode 5, the dominant kernel) run on `st`.
-    const bool prof = c.profiling && nb > 2;
-    if (prof) {
-        while (c.prof_events.size() < (size_t)2 * nb) {
-            hipEvent_t e;
-            HIP_CHECK(hipEventCreate(&e));
-            c.prof_events.push_back(e);
-        }
-    }
-    hipStream_t aux = c.aux_stream;
-    hipEvent_t ev_panels = c.ev_a, ev_pivot = c.ev_b;
     uint64_t prof_relax = 0;
     int prof_n = 0;
-    fw_phase1<K, T><<<1, 256, lds1, st>>>(D, Vp, 0);
-    if (nb > 1) fw_product<K, T, KC, 2><<<2 * (nb - 1), 256, lds2, st>>>(D, Vp, 0, nb);
-    for (int kb = 0; kb < nb; ++kb) {
-        if (nb == 1) break;
-        if (kb + 1 < nb) {
-            fw_product<K, T, KC, 4><<<2 * nb - 3, 256, lds2, st>>>(D, Vp, kb, nb);
-            HIP_CHECK(hipEventRecord(ev_panels, st));
-            HIP_CHECK(hipStreamWaitEvent(aux, ev_panels, 0));
-            fw_phase1<K, T><<<1, 256, lds1, aux>>>(D, Vp, kb + 1);
-            fw_product<K, T, KC, 2><<<2 * (nb - 1), 256, lds2, aux>>>(D, Vp, kb + 1, nb);
-            HIP_CHECK(hipEventRecord(ev_pivot, aux));
-            if (nb > 2) {
-                if (prof) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-                fw_product<K, T, KC, 5><<<dim3(nb - 2, nb - 2), 256, lds2, st>>>(D, Vp, kb, nb);
-                if (prof) {
-                    HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
-                    prof_relax += (uint64_t)(nb - 2) * (nb - 2) * T * T * T;
-                    ++prof_n;
-                }
-            }
-            HIP_CHECK(hipStreamWaitEvent(st, ev_pivot, 0));
-        } else {
-            fw_product<K, T, KC, 3><<<dim3(nb - 1, nb - 1), 256, lds2, st>>>(D, Vp, kb, nb);
-        }
-    }
+    fw_blocked<K, T>(c, pl, D, Vp, st, prof_relax, prof_n);
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
-    if (prof && stats) {
+    if (prof_n && stats) {
         double sum = 0;
         for (int i = 0; i < prof_n; ++i) {
             float ms = 0;
@@ -536,90 +671,107 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
         stats->prof_relaxations += prof_relax;
     }
 
-    Flags fl{};
-    if (n) {
-        k_certify<K><<<grid_for((size_t)n * V), kThreads, 0, st>>>(D, Vp, nodes, n, V, P.flags);
-        HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-    }
-    if (sizeof(K) == 4 && fl.inf_in_used_row) return false;  // saturated or unreachable: redo in u64
+    // u32 certification: no saturated key in any used row (every rank must agree)
+    uint32_t* red = (uint32_t*)c.b_red.get(16);
+    HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
+    if (nloc) k_certify<K><<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(D, Vp, lnodes, nloc, V, P.flags);
+    HIP_CHECK(hipMemcpyAsync(red, &P.flags->inf_in_used_row, 4, hipMemcpyDeviceToDevice, st));
+    if (multi) c.comm->allreduce_max_u32(red, 1, st);
+    uint32_t inf_any = 0;
+    HIP_CHECK(hipMemcpyAsync(&inf_any, red, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (sizeof(K) == 4 && inf_any) return false;  // saturated or unreachable: redo in u64
 
-    // ---- tight-predecessor scan + loss rounds ----
+    // ---- essential edges, tight-predecessor scan, loss ----
     constexpr int TS = 64;
-    const size_t nmax = std::max<uint32_t>(n, 1);
+    constexpr int VE = 16 / (int)sizeof(K);
+    const size_t nmax = std::max<uint32_t>(nloc, 1);
     uint32_t* PRED = (uint32_t*)c.b_PRED.get(nmax * Vp * 4);
-    float* L0 = (float*)c.b_L0.get(nmax * Vp * 4);
-    float* L1 = (float*)c.b_L1.get(nmax * Vp * 4);
-    unsigned long long* multi = (unsigned long long*)c.b_multi.get(8);
+    unsigned long long* multi_cnt = (unsigned long long*)c.b_multi.get(8);
     int rounds = 0;
     unsigned long long nmulti = 0;
     uint64_t n_ess = 0;
     int scan_kind = SRG_SCAN_NONE;
     bool loss_written = false;  // out_loss already filled by the per-row kernel
-    float* Lfin = L0;
+    float* Lfin = nullptr;
     double ms_scan = 0;
-    if (n) {
-        // essential edges: W[u][t] == D[u][t], grouped in 32-target blocks
-        const uint32_t nw64 = (V + 63) / 64;
-        const uint32_t nbT = 2 * nw64;
-        const size_t NQ = (size_t)nbT * V;
-        uint32_t* ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
-        uint32_t* eoff = (uint32_t*)c.b_eoff.get(NQ * 4);
-        uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
-        uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
-        uint32_t* eblk = (uint32_t*)c.b_gblk.get(((size_t)nbT + 1) * 4);
-        HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-        k_ess_count<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, nw64, ecnt, indeg);
+    HIP_CHECK(hipMemsetAsync(multi_cnt, 0, 8, st));
+    // essential bitmask of the own rows, then all-gathered (V^2/8 bytes)
+    const uint32_t nw64 = (V + 63) / 64;
+    const uint32_t nbT = 2 * nw64;
+    unsigned long long* ess = (unsigned long long*)c.b_ess.get((size_t)V * nw64 * 8);
+    if (pl.u1 > pl.u0)
+        k_ess_mask<K><<<grid_for((size_t)(pl.u1 - pl.u0) * nw64 * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, pl.u0,
+                                                                                               pl.u1, nw64, ess);
+    if (multi) {
+        std::vector<size_t> offs(pl.G), lens(pl.G);
+        for (int r = 0; r < pl.G; ++r) {
+            const size_t a = std::min<size_t>(V, (size_t)pl.blk_lo[r] * T), b = std::min<size_t>(V, (size_t)pl.blk_lo[r + 1] * T);
+            offs[r] = a * nw64 * 8;
+            lens[r] = (b - a) * nw64 * 8;
+        }
+        c.comm->allgatherv(ess, offs.data(), lens.data(), st);
+    }
+    const size_t NQ = (size_t)nbT * V;
+    uint32_t* ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
+    uint32_t* eoff = (uint32_t*)c.b_eoff.get(NQ * 4);
+    uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
+    uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
+    uint32_t* eblk = (uint32_t*)c.b_gblk.get(((size_t)nbT + 1) * 4);
+    HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
+    k_ess_count<<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(ess, V, nw64, ecnt, indeg);
+    HIP_CHECK(hipGetLastError());
+    size_t tb0 = 0, tb2 = 0;
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ecnt, eoff, (int)NQ, st));
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, indeg, cscoff, (int)(nw64 * 64 + 1), st));
+    size_t tbytes = std::max(tb0, tb2);
+    void* tmp = c.b_scantmp.get(tbytes);
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ecnt, eoff, (int)NQ, st));
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(nw64 * 64 + 1), st));
+    k_ess_blocks<<<1, 1, 0, st>>>(eoff, ecnt, V, nbT, eblk);
+    uint32_t tail[3];
+    HIP_CHECK(hipMemcpyAsync(&tail[0], eoff + NQ - 1, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&tail[1], ecnt + NQ - 1, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&tail[2], eblk + nbT, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const uint64_t E_ess = (uint64_t)tail[0] + tail[1];
+    const uint64_t E_pad = tail[2];  // padded entry count (blocks rounded up to 64)
+    n_ess = E_ess;
+    const size_t npad = ((size_t)nloc + 63) / 64 * 64;
+    const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
+    const bool sparse = (double)E_ess <= c.sparse_threshold * (double)V * (double)V &&
+                        E_pad + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
+    if (sparse) {
+        scan_kind = SRG_SCAN_SPARSE;
+        const size_t Eb = E_pad + 256;
+        uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
+        uint32_t* ent_ro = (uint32_t*)c.b_entkey.get(Eb * 4);
+        K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
+        uint32_t* ent_tl = (uint32_t*)c.b_grpu.get(Eb * 4);
+        uint32_t* ent_u = (uint32_t*)c.b_grpe.get(Eb * 4);
+        float* ent_b = (float*)c.b_entb.get(Eb * 4);
+        uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
+        HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+        k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
+            ess, W, WL, Vp, V, nw64, std::max<size_t>(npad, 64), eoff, eblk, cscoff, cscfill, ent_ro, ent_w, ent_tl,
+            ent_u, ent_b, cscent);
+        k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
         HIP_CHECK(hipGetLastError());
-        size_t tb0 = 0, tb2 = 0;
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ecnt, eoff, (int)NQ, st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, indeg, cscoff, (int)(nw64 * 64 + 1), st));
-        size_t tbytes = std::max(tb0, tb2);
-        void* tmp = c.b_scantmp.get(tbytes);
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ecnt, eoff, (int)NQ, st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(nw64 * 64 + 1), st));
-        k_ess_blocks<<<1, 1, 0, st>>>(eoff, ecnt, V, nbT, eblk);
-        uint32_t tail[3];
-        HIP_CHECK(hipMemcpyAsync(&tail[0], eoff + NQ - 1, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(&tail[1], ecnt + NQ - 1, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(&tail[2], eblk + nbT, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        const uint64_t E_ess = (uint64_t)tail[0] + tail[1];
-        const uint64_t E_pad = tail[2];  // padded entry count (blocks rounded up to 64)
-        n_ess = E_ess;
-        const size_t npad = ((size_t)n + 63) / 64 * 64;
-        const size_t dst_bytes = (size_t)nw64 * 64 * npad * sizeof(K);
-        const bool sparse = (double)E_ess <= c.sparse_threshold * (double)V * (double)V &&
-                            E_pad + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
-        if (sparse) {
-            scan_kind = SRG_SCAN_SPARSE;
-            const size_t Eb = E_pad + 256;
-            uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
-            uint32_t* ent_ro = (uint32_t*)c.b_entkey.get(Eb * 4);
-            K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
-            uint32_t* ent_tl = (uint32_t*)c.b_grpu.get(Eb * 4);
-            uint32_t* ent_u = (uint32_t*)c.b_grpe.get(Eb * 4);
-            float* ent_b = (float*)c.b_entb.get(Eb * 4);
-            uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
-            HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
-            k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
-                W, D, WL, Vp, V, nw64, npad, eoff, eblk, cscoff, cscfill, ent_ro, ent_w, ent_tl, ent_u, ent_b, cscent);
-            k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
+        if (nloc) {
             const uint32_t nbS = (uint32_t)(npad / 64);
             K* DST = (K*)c.b_DST.get(dst_bytes);
-            k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, nodes, n, DST, npad);
+            k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
-                tight_sparse_u32<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, nodes, n, V,
-                                                      nbT, nbS, eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED,
+                tight_sparse_u32<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc,
+                                                      V, nbT, nbS, eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED,
                                                       Vp);
             } else {
-                tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, nodes, n, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
+                tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, lnodes, nloc, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
                                                       PRED, Vp);
             }
             HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
-            k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
+            k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
             HIP_CHECK(hipGetLastError());
             ms_scan = tm.lap();
             const size_t lds_rows = (size_t)V * 12;
@@ -627,8 +779,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
                 // per-row Gauss-Seidel in LDS, writes out_loss directly
                 set_lds(k_loss_rows<K>, lds_rows);
                 HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
-                k_loss_rows<K><<<n, 1024, lds_rows, st>>>(PRED, Vp, V, nodes, n, ent_u, ent_b, ent_w, DST, npad, cscoff,
-                                                          cscent, P.selfloss, out_loss, &P.flags->changed);
+                k_loss_rows<K><<<nloc, 1024, lds_rows, st>>>(PRED, Vp, V, lnodes, nloc, ent_u, ent_b, ent_w, DST,
+                                                             npad, cscoff, cscent, P.selfloss, nodes, n, lpos,
+                                                             out_loss, &P.flags->changed);
                 HIP_CHECK(hipGetLastError());
                 uint32_t sw = 0;
                 HIP_CHECK(hipMemcpyAsync(&sw, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
@@ -636,13 +789,15 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
                 rounds = (int)sw;
                 loss_written = true;
             } else {
-                k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+                float* L0 = (float*)c.b_L0.get(nmax * Vp * 4);
+                float* L1 = (float*)c.b_L1.get(nmax * Vp * 4);
+                k_fill<float><<<grid_for((size_t)nloc * Vp), kThreads, 0, st>>>(L0, (size_t)nloc * Vp, 1.0f);
                 float* Lin = L0;
                 float* Lout = L1;
                 for (;;) {
                     HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
-                    k_loss_round_sparse<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(
-                        PRED, Vp, DST, npad, nodes, n, V, ent_u, ent_w, ent_b, cscoff, cscent, Lin, Lout,
+                    k_loss_round_sparse<K><<<grid_for((size_t)nloc * V, 256 * 64), kThreads, 0, st>>>(
+                        PRED, Vp, DST, npad, lnodes, nloc, V, ent_u, ent_w, ent_b, cscoff, cscent, Lin, Lout,
                         &P.flags->changed);
                     HIP_CHECK(hipGetLastError());
                     ++rounds;
@@ -655,23 +810,26 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
                 }
                 Lfin = Lin;
             }
-        } else {
-            scan_kind = SRG_SCAN_DENSE;
+        }
+    } else {
+        scan_kind = SRG_SCAN_DENSE;
+        if (nloc) {
             const size_t lds3 = (size_t)2 * KC * (TS + VE) * sizeof(K);
             set_lds(tight_scan<K, TS, KC>, lds3);
-            tight_scan<K, TS, KC><<<dim3((unsigned)(Vp / TS), (n + TS - 1) / TS), 256, lds3, st>>>(D, W, Vp, nodes,
-                                                                                                 n, PRED);
-            HIP_CHECK(hipMemsetAsync(multi, 0, 8, st));
-            k_count_multi<<<grid_for((size_t)n * V), kThreads, 0, st>>>(PRED, n, V, Vp, multi);
-            k_fill<float><<<grid_for((size_t)n * Vp), kThreads, 0, st>>>(L0, (size_t)n * Vp, 1.0f);
+            tight_scan<K, TS, KC><<<dim3((unsigned)(Vp / TS), (nloc + TS - 1) / TS), 256, lds3, st>>>(D, W, Vp, lnodes,
+                                                                                                    nloc, PRED);
+            k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
+            float* L0 = (float*)c.b_L0.get(nmax * Vp * 4);
+            float* L1 = (float*)c.b_L1.get(nmax * Vp * 4);
+            k_fill<float><<<grid_for((size_t)nloc * Vp), kThreads, 0, st>>>(L0, (size_t)nloc * Vp, 1.0f);
             HIP_CHECK(hipGetLastError());
             ms_scan = tm.lap();
             float* Lin = L0;
             float* Lout = L1;
             for (;;) {
                 HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
-                k_loss_round<K><<<grid_for((size_t)n * V, 256 * 64), kThreads, 0, st>>>(PRED, D, W, WL, nodes, n, V,
-                                                                                       Vp, Lin, Lout, P.flags);
+                k_loss_round<K><<<grid_for((size_t)nloc * V, 256 * 64), kThreads, 0, st>>>(
+                    PRED, D, W, WL, lnodes, nloc, V, Vp, Lin, Lout, P.flags);
                 HIP_CHECK(hipGetLastError());
                 ++rounds;
                 uint32_t ch = 0;
@@ -683,36 +841,248 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n,
             }
             Lfin = Lin;
         }
-        HIP_CHECK(hipMemcpyAsync(&nmulti, multi, 8, hipMemcpyDeviceToHost, st));
     }
+    HIP_CHECK(hipMemcpyAsync(&nmulti, multi_cnt, 8, hipMemcpyDeviceToHost, st));
     const double ms_loss = tm.lap();
 
-    if (n) {
-        HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
-        k_extract<K><<<grid_for((size_t)n * n), kThreads, 0, st>>>(D, loss_written ? nullptr : Lfin, Vp, nodes, n,
-                                                                   P.selflat, P.selfloss, out_lat, out_loss, P.flags);
-        HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
-    }
+    HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
+    if (nloc)
+        k_extract<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, loss_written ? nullptr : Lfin, Vp, lnodes,
+                                                                      nloc, nodes, n, lpos, P.selflat, P.selfloss,
+                                                                      out_lat, out_loss, P.flags);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(red, &P.flags->unreachable_used_pair, 4, hipMemcpyDeviceToDevice, st));
+    if (multi) c.comm->allreduce_max_u32(red, 1, st);
+    uint32_t unreach = 0;
+    HIP_CHECK(hipMemcpyAsync(&unreach, red, 4, hipMemcpyDeviceToHost, st));
     const double ms_extract = tm.lap();
-    if (n && fl.unreachable_used_pair)
+    if (unreach)
         fail(SRG_ERR_UNREACHABLE,
              "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
              "from another used node)");
+
+    // ---- output exchange: every rank ends with all n x n rows ----
+    double ms_exchange = 0;
+    if (multi && c.gather_output) {
+        std::vector<size_t> offs(pl.G), lens(pl.G);
+        auto exchange = [&](void* out, size_t elem) {
+            const size_t row = (size_t)n * elem;
+            for (int r = 0; r < pl.G; ++r) {
+                offs[r] = (size_t)pl.first[r] * row;
+                lens[r] = (size_t)pl.cnt[r] * row;
+            }
+            if (pl.contiguous) {
+                c.comm->allgatherv(out, offs.data(), lens.data(), st);
+                return;
+            }
+            unsigned char* stage = (unsigned char*)c.b_stage.get((size_t)n * row);
+            uint32_t* allpos = (uint32_t*)c.b_allpos.get((size_t)n * 4);
+            HIP_CHECK(hipMemcpyAsync(allpos, pl.allpos.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+            if (nloc)
+                k_rows_copy<<<std::min<uint32_t>(nloc, 4096), 256, 0, st>>>(
+                    (const unsigned char*)out, stage + offs[pl.g], lpos, nloc, row, 0);
+            c.comm->allgatherv(stage, offs.data(), lens.data(), st);
+            k_rows_copy<<<std::min<uint32_t>(n, 4096), 256, 0, st>>>(stage, (unsigned char*)out, allpos, n, row, 1);
+            HIP_CHECK(hipGetLastError());
+        };
+        exchange(out_lat, 8);
+        exchange(out_loss, 4);
+        ms_exchange = tm.lap();
+    }
     if (stats) {
         stats->ms_build += ms_build;
         stats->ms_fw += ms_fw;
         stats->ms_scan += ms_scan;
         stats->ms_loss += ms_loss;
         stats->ms_extract += ms_extract;
+        stats->ms_exchange += ms_exchange;
         stats->path_kind = sizeof(K) == 4 ? SRG_PATH_DENSE_U32 : SRG_PATH_DENSE_U64;
         stats->loss_rounds = rounds;
         stats->multi_pred_pairs = nmulti;
-        stats->relaxations = (uint64_t)Vp * Vp * Vp;
+        stats->relaxations = (uint64_t)(pl.rb1 - pl.rb0) * T * Vp * Vp;
         stats->essential_edges = n_ess;
         stats->scan_kind = scan_kind;
+        stats->nranks = pl.G;
+        stats->rank = pl.g;
+        stats->local_sources = nloc;
     }
     return true;
+}
+
+// ---- sparse path: batched lexicographic Bellman-Ford (sparse.hip.h) ----------------------
+// Rank r routes the used sources at positions [r*n/G, (r+1)*n/G) (contiguous output rows).
+// Returns false when a used pair came out saturated/unreachable and the graph's latencies
+// could exceed the u32 keys: the caller then decides on the dense u64 path.
+bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
+                float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats) {
+    const uint32_t V = g.V;
+    const bool multi = c.comm && c.comm->nranks > 1;
+    const int G = multi ? c.comm->nranks : 1, rk = multi ? c.comm->rank : 0;
+    Timer tm(st);
+    // CSR of in-arcs
+    uint32_t* off = (uint32_t*)c.b_indeg.get(((size_t)V + 1) * 4);
+    uint32_t* cur = (uint32_t*)c.b_cscfill.get(((size_t)V + 1) * 4);
+    HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
+    if (g.E) k_csr_count<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.directed, cur);
+    size_t tb = 0;
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cur, off, (int)(V + 1), st));
+    void* tmp = c.b_scantmp.get(tb);
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cur, off, (int)(V + 1), st));
+    uint32_t arcs = 0;
+    HIP_CHECK(hipMemcpyAsync(&arcs, off + V, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    uint32_t* in_src = (uint32_t*)c.b_entkey.get(std::max<size_t>(arcs, 1) * 4);
+    uint32_t* in_w = (uint32_t*)c.b_entw.get(std::max<size_t>(arcs, 1) * 4);
+    float* in_b = (float*)c.b_entb.get(std::max<size_t>(arcs, 1) * 4);
+    HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
+    if (g.E)
+        k_csr_fill<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, off, cur, in_src,
+                                                       in_w, in_b);
+    // out-arcs for the work marks: the in-CSR itself when undirected
+    const uint32_t* out_off = off;
+    const uint32_t* out_dst = in_src;
+    if (g.directed) {
+        uint32_t* ooff = (uint32_t*)c.b_outoff.get(((size_t)V + 1) * 4);
+        uint32_t* odst = (uint32_t*)c.b_outdst.get(std::max<size_t>(arcs, 1) * 4);
+        HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
+        k_csr_count_out<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, cur);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cur, ooff, (int)(V + 1), st));
+        HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
+        k_csr_fill_out<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, ooff, cur, odst);
+        out_off = ooff;
+        out_dst = odst;
+    }
+    // this rank's sources, in graph-locality (BFS) order, in batches of 64 lanes: sources of
+    // one batch are close to each other, so their Bellman-Ford frontiers move together
+    const uint32_t p0 = (uint32_t)((uint64_t)rk * n / G), p1 = (uint32_t)((uint64_t)(rk + 1) * n / G);
+    const uint32_t nloc = p1 - p0;
+    const uint32_t nbatch = (nloc + 63) / 64;
+    std::vector<uint32_t> h_off(V + 1), h_src(arcs);
+    HIP_CHECK(hipMemcpyAsync(h_off.data(), off, ((size_t)V + 1) * 4, hipMemcpyDeviceToHost, st));
+    if (arcs) HIP_CHECK(hipMemcpyAsync(h_src.data(), in_src, (size_t)arcs * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<uint32_t> order(V, 0xFFFFFFFFu), queue;
+    queue.reserve(V);
+    uint32_t next = 0;
+    for (uint32_t root_pass = 0; root_pass < 2 && next < V; ++root_pass) {
+        for (uint32_t r = 0; r < V; ++r) {
+            // first pass: start at the highest-degree vertex; then any unvisited vertex
+            uint32_t start = r;
+            if (root_pass == 0) {
+                uint32_t best = 0;
+                for (uint32_t v = 0; v < V; ++v)
+                    if (h_off[v + 1] - h_off[v] > h_off[best + 1] - h_off[best]) best = v;
+                start = best;
+            }
+            if (order[start] != 0xFFFFFFFFu) continue;
+            order[start] = next++;
+            queue.assign(1, start);
+            for (size_t qi = 0; qi < queue.size(); ++qi) {
+                const uint32_t v = queue[qi];
+                for (uint32_t k = h_off[v]; k < h_off[v + 1]; ++k) {
+                    const uint32_t u = h_src[k];
+                    if (order[u] == 0xFFFFFFFFu) {
+                        order[u] = next++;
+                        queue.push_back(u);
+                    }
+                }
+            }
+            if (root_pass == 0) break;
+        }
+    }
+    std::vector<uint32_t> loc(nloc);
+    for (uint32_t i = 0; i < nloc; ++i) loc[i] = p0 + i;
+    if (c.sparse_locality)
+        std::stable_sort(loc.begin(), loc.end(),
+                         [&](uint32_t x, uint32_t y) { return order[P.nodes_h[x]] < order[P.nodes_h[y]]; });
+    std::vector<uint32_t> bsrc((size_t)std::max<uint32_t>(nbatch, 1) * 64), brow(bsrc.size());
+    for (uint32_t i = 0; i < (uint32_t)bsrc.size(); ++i) {
+        const bool real = i < nloc;
+        bsrc[i] = P.nodes_h[real ? loc[i] : (nloc ? loc[0] : 0)];
+        brow[i] = real ? loc[i] : 0xFFFFFFFFu;
+    }
+    uint32_t* d_bsrc = (uint32_t*)c.b_lnodes.get(bsrc.size() * 4);
+    uint32_t* d_brow = (uint32_t*)c.b_lpos.get(brow.size() * 4);
+    HIP_CHECK(hipMemcpyAsync(d_bsrc, bsrc.data(), bsrc.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_brow, brow.data(), brow.size() * 4, hipMemcpyHostToDevice, st));
+    uint32_t* fl = (uint32_t*)c.b_red.get(64);
+    HIP_CHECK(hipMemsetAsync(fl, 0, 64, st));
+    HIP_CHECK(hipGetLastError());
+    const double ms_build = tm.lap();
+
+    int dev_cus = 256;
+    HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * 2));
+    const size_t lds = ((size_t)(V + 63) / 64) * 4 * 8 + 64 * 65 * 8;
+    if (nbatch) {
+        if (lds > 160 * 1024) fail(SRG_ERR_INTERNAL, "sparse path: flag bitmaps exceed LDS (V too large)");
+        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
+        set_lds(k_sparse_bf, lds);
+        SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
+                     P.selflat, P.selfloss, out_lat, out_loss, fl};
+        if (c.profiling) {
+            while (c.prof_events.size() < 2) {
+                hipEvent_t e;
+                HIP_CHECK(hipEventCreate(&e));
+                c.prof_events.push_back(e);
+            }
+            HIP_CHECK(hipEventRecord(c.prof_events[0], st));
+        }
+        k_sparse_bf<<<grid, SP_THREADS, lds, st>>>(a);
+        HIP_CHECK(hipGetLastError());
+        if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
+    }
+    // every rank agrees on the outcome before any exchange
+    if (multi) c.comm->allreduce_max_u32(fl, 2, st);
+    uint32_t hfl[4] = {0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(hfl, fl, 16, hipMemcpyDeviceToHost, st));
+    const double ms_sssp = tm.lap();
+    if (hfl[0]) {
+        const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (V > 1 ? V - 1 : 1);
+        if (bound >= 0xFFFFFFFFull) return false;  // maybe saturated: decide on the u64 path
+        fail(SRG_ERR_UNREACHABLE,
+             "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
+             "from another used node)");
+    }
+    double ms_exchange = 0;
+    if (multi && c.gather_output) {
+        std::vector<size_t> offs(G), lens(G);
+        for (int elem : {8, 4}) {
+            for (int r = 0; r < G; ++r) {
+                const size_t a0 = (uint64_t)r * n / G, a1 = (uint64_t)(r + 1) * n / G;
+                offs[r] = a0 * n * elem;
+                lens[r] = (a1 - a0) * n * elem;
+            }
+            c.comm->allgatherv(elem == 8 ? (void*)out_lat : (void*)out_loss, offs.data(), lens.data(), st);
+        }
+        ms_exchange = tm.lap();
+    }
+    if (stats && c.profiling && nbatch) {
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, c.prof_events[0], c.prof_events[1]));
+        stats->prof_launches += 1;
+        stats->prof_kernel_ms += ms;
+        stats->prof_relaxations += nloc;  // sparse: sources routed by the profiled launch
+    }
+    if (stats) {
+        stats->ms_build += ms_build;
+        stats->ms_fw += ms_sssp;
+        stats->ms_exchange += ms_exchange;
+        stats->path_kind = SRG_PATH_SPARSE_U32;
+        stats->loss_rounds = (int)hfl[1];
+        stats->relaxations = (((uint64_t)hfl[3] << 32) | hfl[2]) * 64;
+        stats->nranks = G;
+        stats->rank = rk;
+        stats->local_sources = nloc;
+    }
+    return true;
+}
+
+bool choose_sparse(const srg_ctx& c, const DevGraph& g) {
+    if (c.algorithm == SRG_ALGO_DENSE) return false;
+    if (c.algorithm == SRG_ALGO_SPARSE) return true;
+    const double arcs = (double)g.E * (g.directed ? 1.0 : 2.0);
+    return g.V >= 2048 && arcs * 32.0 < (double)g.V * g.V;
 }
 
 void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
@@ -728,10 +1098,16 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     if (bound >= ((unsigned __int128)1 << 62))
         fail(SRG_ERR_LATENCY_RANGE, "path latency sum could exceed 2^62 ns (max edge latency " +
                                         std::to_string(P.es.max_lat) + " ns)");
-    if (P.es.max_lat < 0xFFFFFFFFull) {
-        if (run_dense<uint32_t, 128>(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
+    const int G = c.comm ? c.comm->nranks : 1, rk = c.comm ? c.comm->rank : 0;
+    if (choose_sparse(c, g) && P.es.max_lat < 0xFFFFFFFFull) {
+        if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
     }
-    run_dense<uint64_t, 64>(c, g, nodes, n, out_lat, out_loss, st, P, stats);
+    if (P.es.max_lat < 0xFFFFFFFFull) {
+        Plan pl = make_plan(G, rk, g.V, 128, P.nodes_h);
+        if (run_dense<uint32_t, 128>(c, g, pl, nodes, n, out_lat, out_loss, st, P, stats)) return;
+    }
+    Plan pl = make_plan(G, rk, g.V, 64, P.nodes_h);
+    run_dense<uint64_t, 64>(c, g, pl, nodes, n, out_lat, out_loss, st, P, stats);
 }
 
 void direct_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
@@ -864,8 +1240,9 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipSetDevice(device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&c->ev_a, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&c->ev_b, hipEventDisableTiming));
+        HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d})
+            HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     });
     if (rc != SRG_OK) {
         delete c;
@@ -885,6 +1262,16 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SPARSE_THRESHOLD:
             if (!(value >= 0.0)) return SRG_ERR_ARG;
             ctx->sparse_threshold = value;
+            return SRG_OK;
+        case SRG_OPT_GATHER_OUTPUT:
+            ctx->gather_output = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_LOCALITY:
+            ctx->sparse_locality = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_ALGORITHM:
+            if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
+            ctx->algorithm = (int)value;
             return SRG_OK;
         default:
             return SRG_ERR_ARG;
@@ -930,6 +1317,63 @@ int srg_compute_shortest_paths_device(srg_ctx* ctx, const srg_edge_list* g, cons
     });
 }
 
-const char* srg_version(void) { return "shadow_amd routing 0.1 (gfx950, dense FW u32/u64 + tight-DAG loss)"; }
+int srg_comm_unique_id(unsigned char id[SRG_UNIQUE_ID_BYTES], char* errbuf, size_t errlen) {
+    if (!id) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    return guard(errbuf, errlen, [&]() {
+        const std::string e = srg::rccl_unique_id(id);
+        if (!e.empty()) fail(SRG_ERR_RCCL, e);
+    });
+}
+
+int srg_comm_init(srg_ctx* ctx, int nranks, int rank, const unsigned char id[SRG_UNIQUE_ID_BYTES], char* errbuf,
+                  size_t errlen) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) {
+        set_err(errbuf, errlen, "bad argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return guard(errbuf, errlen, [&]() {
+        srg::Comm* cm = nullptr;
+        const std::string e = srg::rccl_create(nranks, rank, id, ctx->device, &cm);
+        if (!e.empty()) fail(SRG_ERR_RCCL, e);
+        delete ctx->comm;
+        ctx->comm = cm;
+    });
+}
+
+int srg_local_group_create(int nranks, srg_local_group** out) {
+    if (!out || nranks < 1) return SRG_ERR_ARG;
+    *out = reinterpret_cast<srg_local_group*>(srg::local_group_create(nranks));
+    return SRG_OK;
+}
+
+void srg_local_group_release(srg_local_group* g) { srg::local_group_release(reinterpret_cast<srg::LocalGroup*>(g)); }
+
+int srg_comm_init_local(srg_ctx* ctx, srg_local_group* g, int rank, char* errbuf, size_t errlen) {
+    if (!ctx || !g) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return guard(errbuf, errlen, [&]() {
+        srg::Comm* cm = nullptr;
+        const std::string e = srg::local_create(reinterpret_cast<srg::LocalGroup*>(g), rank, ctx->device, &cm);
+        if (!e.empty()) fail(SRG_ERR_ARG, e);
+        delete ctx->comm;
+        ctx->comm = cm;
+    });
+}
+
+int srg_comm_size(srg_ctx* ctx, int* nranks, int* rank) {
+    if (!ctx || !nranks || !rank) return SRG_ERR_ARG;
+    *nranks = ctx->comm ? ctx->comm->nranks : 1;
+    *rank = ctx->comm ? ctx->comm->rank : 0;
+    return SRG_OK;
+}
+
+const char* srg_version(void) { return "shadow_amd routing 0.2 (gfx950, dense FW u32/u64 + tight-DAG loss, RCCL row-block FW)"; }
 
 }  // extern "C"

@@ -1,0 +1,312 @@
+// sparse.hip.h — batched lexicographic Bellman-Ford over CSR for sparse graphs (gfx950).
+//
+// Per used source the reference runs petgraph's Dijkstra with PathProperties scores
+// (mod.rs:190-208, 305-331).  Its result is the unique solution of
+//     label(s) = (0, 0.0),   label(t) = lexmin over in-arcs (u,t) of label(u) (+) arc
+// where (+) is PathProperties::add (u64 latency sum, left-fold f32 loss) and lexmin compares
+// latency then loss (positive latencies make the tight graph a DAG, so the fixpoint is unique
+// and equals Dijkstra's scores bit for bit).  Any relaxation order that reaches the fixpoint
+// therefore reproduces the reference; this file reaches it with pull-style Bellman-Ford sweeps.
+//
+// Batching: one 64-lane wave relaxes ONE vertex for 64 sources at once (lane = source), so
+// every label access is one coalesced 512-byte row.  A label is the lexicographic key
+//     (latency_u32 << 32) | float_bits(loss)        (loss >= +0: bit order == numeric order)
+// so lexmin is a single u64 min.  Latency keys saturate at 2^32-1 (= "unreachable or too
+// long"); the host re-runs such graphs on the dense u64 path.
+//
+// Layout (HBM):
+//   in_off [V+1], in_src/in_w/in_b [arcs]  CSR of IN-arcs (self-loops dropped; undirected
+//                                          edges give both arcs; parallel arcs kept)
+//   slot labels [V][64] u64 per resident workgroup (one batch of 64 sources at a time)
+// One workgroup owns one batch for all of its sweeps (no inter-workgroup synchronisation):
+// per sweep every wave pulls the vertices it owns, skipping arcs whose source vertex did not
+// change in the previous sweep (bit flags in LDS), and the batch ends when a sweep changes
+// nothing.  Workgroups take batches from an atomic queue until none are left.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hip.h"
+
+namespace srg {
+
+constexpr unsigned long long LBL_INF = ~0ull;
+constexpr int SP_WAVES = 16;           // waves per workgroup (1024 threads)
+constexpr int SP_THREADS = SP_WAVES * 64;
+
+__device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, uint32_t w, float b) {
+    const uint32_t lat = (uint32_t)(lu >> 32);
+    const uint32_t nl = __builtin_elementwise_add_sat(lat, w);
+    const float loss = fold_loss(__uint_as_float((uint32_t)lu), b);
+    const unsigned long long c = ((unsigned long long)nl << 32) | __float_as_uint(loss);
+    return nl == 0xFFFFFFFFu ? LBL_INF : c;
+}
+
+// ---- CSR of in-arcs -------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lat_key32(uint64_t l) { return l >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)l; }
+
+__global__ void k_csr_count(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                            int directed, uint32_t* __restrict__ indeg) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s == t) continue;
+        atomicAdd(&indeg[t], 1u);
+        if (!directed) atomicAdd(&indeg[s], 1u);
+    }
+}
+
+// out-arcs (directed graphs only): targets per source vertex
+__global__ void k_csr_count_out(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                uint32_t* __restrict__ outdeg) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x)
+        if (src[e] != dst[e]) atomicAdd(&outdeg[src[e]], 1u);
+}
+
+__global__ void k_csr_fill_out(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                               const uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                               uint32_t* __restrict__ out_dst) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s != t) out_dst[off[s] + atomicAdd(&cur[s], 1u)] = t;
+    }
+}
+
+__global__ void k_csr_fill(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                           const uint64_t* __restrict__ lat, const float* __restrict__ loss, int directed,
+                           const uint32_t* __restrict__ off, uint32_t* __restrict__ cur, uint32_t* __restrict__ in_src,
+                           uint32_t* __restrict__ in_w, float* __restrict__ in_b) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s == t) continue;
+        const uint32_t w = lat_key32(lat[e]);
+        const float b = __fsub_rn(1.0f, loss[e] + 0.0f);
+        uint32_t k = off[t] + atomicAdd(&cur[t], 1u);
+        in_src[k] = s;
+        in_w[k] = w;
+        in_b[k] = b;
+        if (!directed) {
+            k = off[s] + atomicAdd(&cur[s], 1u);
+            in_src[k] = t;
+            in_w[k] = w;
+            in_b[k] = b;
+        }
+    }
+}
+
+// ---- the batched sweep kernel ------------------------------------------------------------
+struct SparseArgs {
+    const uint32_t* in_off;
+    const uint32_t* in_src;
+    const uint32_t* in_w;
+    const float* in_b;
+    const uint32_t* out_off;     // CSR of OUT-arcs (== the in-CSR for undirected graphs)
+    const uint32_t* out_dst;
+    uint32_t V;
+    const uint32_t* batch_src;   // [nbatch*64] source vertex per lane
+    const uint32_t* batch_row;   // [nbatch*64] output row per lane (0xFFFFFFFF = padding lane)
+    uint32_t nbatch;
+    unsigned long long* slots;   // [gridDim.x][V][64]
+    uint32_t* queue;             // next batch
+    const uint32_t* cols;        // [ncols] used target vertices (output columns)
+    uint32_t ncols;
+    const uint64_t* self_lat;    // raw self-loop weight (diagonal, mod.rs:211-217)
+    const float* self_loss;
+    uint64_t* out_lat;           // [rows][ncols]
+    float* out_loss;
+    uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2] total evaluations (lo)
+};
+
+__device__ __forceinline__ unsigned long long ld_label(const unsigned long long* p) {
+    // L1-bypassing load: rows written by other waves of this workgroup in the previous sweep
+    return __builtin_nontemporal_load(p);
+}
+
+// LDS bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
+// pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
+// sweep (the out-neighbours of changed vertices, pushed when a vertex changes).  A sweep
+// only visits marked vertices, 64 per wave step (one bitmap word pair).
+__global__ void __launch_bounds__(SP_THREADS) k_sparse_bf(SparseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const uint32_t V = a.V;
+    const uint32_t nw = (V + 63) / 64;  // 64-vertex windows
+    unsigned long long* fprev = reinterpret_cast<unsigned long long*>(smem_raw);
+    unsigned long long* fcur = fprev + nw;
+    unsigned long long* mark = fcur + nw;
+    unsigned long long* mnext = mark + nw;
+    unsigned long long* tile = mnext + nw;  // [64][65] output transpose
+    __shared__ uint32_t s_batch, s_changed;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
+    uint32_t max_sweeps = 0;
+    unsigned long long evals = 0;
+
+    auto push_out = [&](uint32_t v) {  // mark the out-neighbours of v for the next sweep
+        const uint32_t o0 = a.out_off[v], o1 = a.out_off[v + 1];
+        for (uint32_t k = o0 + lane; k < o1; k += 64) {
+            const uint32_t t = a.out_dst[k];
+            atomicOr(&mnext[t >> 6], 1ull << (t & 63));
+        }
+    };
+
+    for (;;) {
+        if (threadIdx.x == 0) s_batch = atomicAdd(a.queue, 1u);
+        __syncthreads();
+        const uint32_t bt = s_batch;
+        __syncthreads();
+        if (bt >= a.nbatch) break;
+        const uint32_t my_src = a.batch_src[bt * 64 + lane];
+        // init: labels INF except the sources; changed = the sources; marks = their out-neighbours
+        for (uint32_t v = wave; v < V; v += SP_WAVES)
+            L[(size_t)v * 64 + lane] = (v == my_src) ? 0ull : LBL_INF;
+        for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+            fprev[w] = 0;
+            fcur[w] = 0;
+            mark[w] = 0;
+            mnext[w] = 0;
+        }
+        __syncthreads();
+        if (wave == 0) atomicOr(&fprev[my_src >> 6], 1ull << (my_src & 63));
+        for (uint32_t q = wave; q < 64; q += SP_WAVES) {
+            const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)my_src, q);
+            push_out(sv);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+            mark[w] = mnext[w];
+            mnext[w] = 0;
+        }
+        __syncthreads();
+        uint32_t sweeps = 0;
+        for (;;) {
+            if (threadIdx.x == 0) s_changed = 0;
+            __syncthreads();
+            uint32_t chg = 0;
+            for (uint32_t w = wave; w < nw; w += SP_WAVES) {
+                unsigned long long mk = mark[w];
+                if (!mk) continue;
+                const uint32_t vl = w * 64 + lane;
+                const uint32_t off_lo = vl < V ? a.in_off[vl] : 0u;
+                const uint32_t off_hi = vl < V ? a.in_off[vl + 1] : 0u;
+                while (mk) {
+                    const int i = __builtin_ctzll(mk);
+                    mk &= mk - 1;
+                    const uint32_t v = w * 64 + (uint32_t)i;
+                    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)off_lo, i);
+                    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)off_hi, i);
+                    unsigned long long best = 0, old = 0;
+                    bool have = false;
+                    for (uint32_t base = a0; base < a1; base += 64) {
+                        const uint32_t k = base + lane;
+                        uint32_t u = 0;
+                        bool act = false;
+                        if (k < a1) {
+                            u = a.in_src[k];
+                            act = (fprev[u >> 6] >> (u & 63)) & 1ull;
+                        }
+                        unsigned long long m = __ballot(act);
+                        if (!m) continue;
+                        if (!have) {
+                            old = best = ld_label(&L[(size_t)v * 64 + lane]);
+                            have = true;
+                        }
+                        const uint32_t w_l = act ? a.in_w[k] : 0u;
+                        const float b_l = act ? a.in_b[k] : 0.0f;
+                        while (m) {
+                            // up to 4 active arcs per step: issue their row loads together
+                            int j[4];
+                            int cnt = 0;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                j[q] = m ? __builtin_ctzll(m) : -1;
+                                if (m) {
+                                    m &= m - 1;
+                                    ++cnt;
+                                }
+                            }
+                            unsigned long long row[4];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                if (j[q] >= 0) {
+                                    const uint32_t uu = (uint32_t)__builtin_amdgcn_readlane((int)u, j[q]);
+                                    row[q] = ld_label(&L[(size_t)uu * 64 + lane]);
+                                }
+                            }
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                if (j[q] >= 0) {
+                                    const uint32_t ww = (uint32_t)__builtin_amdgcn_readlane((int)w_l, j[q]);
+                                    const float bb =
+                                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b_l), j[q]));
+                                    const unsigned long long c = row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], ww, bb);
+                                    best = c < best ? c : best;
+                                }
+                            }
+                            evals += (unsigned long long)cnt;
+                        }
+                    }
+                    if (!have) continue;
+                    const bool lower = best < old;
+                    if (__ballot(lower)) {
+                        if (lower) L[(size_t)v * 64 + lane] = best;
+                        if (lane == 0) atomicOr(&fcur[v >> 6], 1ull << (v & 63));
+                        push_out(v);
+                        chg = 1;
+                    }
+                }
+            }
+            if (chg && lane == 0) s_changed = 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // label stores reached L2
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            ++sweeps;
+            const bool more = s_changed != 0;
+            for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+                fprev[w] = fcur[w];
+                fcur[w] = 0;
+                mark[w] = mnext[w];
+                mnext[w] = 0;
+            }
+            __syncthreads();
+            if (!more) break;
+        }
+        max_sweeps = sweeps > max_sweeps ? sweeps : max_sweeps;
+        // ---- output rows: 64 targets x 64 sources tiles transposed through LDS ----
+        uint32_t bad = 0;
+        for (uint32_t j0 = 0; j0 < a.ncols; j0 += 64) {
+            for (uint32_t i = wave; i < 64; i += SP_WAVES) {
+                const uint32_t j = j0 + i;
+                tile[i * 65 + lane] = j < a.ncols ? ld_label(&L[(size_t)a.cols[j] * 64 + lane]) : 0ull;
+            }
+            __syncthreads();
+            for (uint32_t sl = wave; sl < 64; sl += SP_WAVES) {
+                const uint32_t row = a.batch_row[bt * 64 + sl];
+                const uint32_t j = j0 + lane;
+                if (row == 0xFFFFFFFFu || j >= a.ncols) continue;
+                const unsigned long long l = tile[lane * 65 + sl];
+                uint64_t ol;
+                float os;
+                if (j == row) {  // diagonal: the raw self-loop weight
+                    const uint32_t s = a.batch_src[bt * 64 + sl];
+                    ol = a.self_lat[s];
+                    os = a.self_loss[s];
+                } else {
+                    const uint32_t lat = (uint32_t)(l >> 32);
+                    bad |= lat == 0xFFFFFFFFu;
+                    ol = lat;
+                    os = __uint_as_float((uint32_t)l);
+                }
+                a.out_lat[(size_t)row * a.ncols + j] = ol;
+                a.out_loss[(size_t)row * a.ncols + j] = os;
+            }
+            __syncthreads();
+        }
+        if (bad) atomicOr(&a.flags[0], 1u);
+    }
+    if (threadIdx.x == 0) atomicMax(&a.flags[1], max_sweeps);
+    if (lane == 0 && evals) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[2]), evals);
+}
+
+}  // namespace srg

@@ -33,24 +33,38 @@ namespace srg {
 constexpr uint32_t TB = 32;  // targets per block of the sparse scan
 
 // ---- essential-edge extraction ---------------------------------------------------------
-// One wave per (u, 64-target window w64): lanes = targets; window w64 = blocks 2*w64, 2*w64+1.
+// ESS[u][w64] (u64): bit `lane` set <=> edge u -> t = 64*w64 + lane is essential.  Computed by
+// the owner of row u (its rows of D are the only ones it has in the multi-GPU layout) and
+// then all-gathered: V^2/8 bytes instead of the V^2 keys of D.
 template <class K>
-__device__ __forceinline__ unsigned long long ess_mask(const K* __restrict__ W, const K* __restrict__ D,
-                                                      size_t ld, uint32_t V, uint32_t u, uint32_t w64,
-                                                      uint32_t lane) {
-    const uint32_t t = w64 * 64 + lane;
-    bool ess = false;
-    if (t < V && t != u) {
-        const K w = W[(size_t)u * ld + t];
-        ess = (w != KeyOps<K>::INF) && (w == D[(size_t)u * ld + t]);
+__global__ void __launch_bounds__(256) k_ess_mask(const K* __restrict__ W, const K* __restrict__ D, size_t ld,
+                                                   uint32_t V, uint32_t u0, uint32_t u1, uint32_t nw64,
+                                                   unsigned long long* __restrict__ ess) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    const size_t total = (size_t)nw64 * (u1 - u0);
+    for (size_t q = wave; q < total; q += nwaves) {
+        const uint32_t u = u0 + (uint32_t)(q / nw64), w64 = (uint32_t)(q % nw64);
+        const uint32_t t = w64 * 64 + lane;
+        bool e = false;
+        if (t < V && t != u) {
+            const K w = W[(size_t)u * ld + t];
+            e = (w != KeyOps<K>::INF) && (w == D[(size_t)u * ld + t]);
+        }
+        const unsigned long long m = __ballot(e);
+        if (lane == 0) ess[(size_t)u * nw64 + w64] = m;
     }
-    return __ballot(ess);
+}
+
+__device__ __forceinline__ unsigned long long ess_mask(const unsigned long long* __restrict__ ess, uint32_t nw64,
+                                                      uint32_t u, uint32_t w64) {
+    return ess[(size_t)u * nw64 + w64];  // wave-uniform load
 }
 
 // cnt[b*V + u] = essential edges u -> block b;  indeg[t] for the CSC lists.
-template <class K>
-__global__ void __launch_bounds__(256) k_ess_count(const K* __restrict__ W, const K* __restrict__ D, size_t ld,
-                                                    uint32_t V, uint32_t nw64, uint32_t* __restrict__ cnt,
+__global__ void __launch_bounds__(256) k_ess_count(const unsigned long long* __restrict__ ess, uint32_t V,
+                                                    uint32_t nw64, uint32_t* __restrict__ cnt,
                                                     uint32_t* __restrict__ indeg) {
     const uint32_t lane = threadIdx.x & 63;
     const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
@@ -58,7 +72,7 @@ __global__ void __launch_bounds__(256) k_ess_count(const K* __restrict__ W, cons
     const size_t total = (size_t)nw64 * V;
     for (size_t q = wave; q < total; q += nwaves) {
         const uint32_t w64 = (uint32_t)(q / V), u = (uint32_t)(q - (size_t)w64 * V);
-        const unsigned long long m = ess_mask<K>(W, D, ld, V, u, w64, lane);
+        const unsigned long long m = ess_mask(ess, nw64, u, w64);
         if ((m >> lane) & 1ull) atomicAdd(&indeg[w64 * 64 + lane], 1u);
         if (lane == 0) {
             cnt[(size_t)(2 * w64) * V + u] = (uint32_t)__popcll(m & 0xFFFFFFFFull);
@@ -82,8 +96,9 @@ __global__ void k_ess_blocks(const uint32_t* __restrict__ eoff, const uint32_t* 
 }
 
 template <class K>
-__global__ void __launch_bounds__(256) k_ess_fill(const K* __restrict__ W, const K* __restrict__ D,
-                                                   const uint32_t* __restrict__ WL, size_t ld, uint32_t V,
+__global__ void __launch_bounds__(256) k_ess_fill(const unsigned long long* __restrict__ ess,
+                                                   const K* __restrict__ W, const uint32_t* __restrict__ WL,
+                                                   size_t ld, uint32_t V,
                                                    uint32_t nw64, size_t npad, const uint32_t* __restrict__ eoff,
                                                    const uint32_t* __restrict__ eblk,
                                                    const uint32_t* __restrict__ csc_off,
@@ -97,7 +112,7 @@ __global__ void __launch_bounds__(256) k_ess_fill(const K* __restrict__ W, const
     const size_t total = (size_t)nw64 * V;
     for (size_t q = wave; q < total; q += nwaves) {
         const uint32_t w64 = (uint32_t)(q / V), u = (uint32_t)(q - (size_t)w64 * V);
-        const unsigned long long m = ess_mask<K>(W, D, ld, V, u, w64, lane);
+        const unsigned long long m = ess_mask(ess, nw64, u, w64);
         if (!((m >> lane) & 1ull)) continue;
         const uint32_t t = w64 * 64 + lane;
         const uint32_t hb = lane >> 5;  // which 32-target block of the window
@@ -348,7 +363,9 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
                                                      const K* __restrict__ DST, size_t npad,
                                                      const uint32_t* __restrict__ csc_off,
                                                      const uint32_t* __restrict__ csc_ent,
-                                                     const float* __restrict__ self_loss, float* __restrict__ out_loss,
+                                                     const float* __restrict__ self_loss,
+                                                     const uint32_t* __restrict__ cols, uint32_t ncols,
+                                                     const uint32_t* __restrict__ rowpos, float* __restrict__ out_loss,
                                                      uint32_t* __restrict__ max_sweeps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     uint32_t* U = reinterpret_cast<uint32_t*>(smem_raw);
@@ -415,8 +432,9 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
         __syncthreads();
     }
     if (threadIdx.x == 0) atomicMax(max_sweeps, sweeps);
-    float* orow = out_loss + (size_t)r * n;
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) orow[j] = (j == r) ? self_loss[s] : L[nodes[j]];
+    const uint32_t p = rowpos[r];  // output row = position of s in the full `nodes` list
+    float* orow = out_loss + (size_t)p * ncols;
+    for (uint32_t j = threadIdx.x; j < ncols; j += blockDim.x) orow[j] = (j == p) ? self_loss[s] : L[cols[j]];
 }
 
 }  // namespace srg

@@ -186,8 +186,62 @@ class Router:
     def compute_shortest_paths(self, edges, nodes):
         return self._run(N.lib().srg_compute_shortest_paths, edges, nodes)
 
+    # ---- multi-GPU (include/shadow_routing.h srg_comm_*) ----------------------------------
+    @staticmethod
+    def comm_unique_id():
+        """128-byte RCCL unique id (rank 0 creates it; share it with every rank)."""
+        buf = ctypes.create_string_buffer(N.SRG_UNIQUE_ID_BYTES)
+        err = ctypes.create_string_buffer(1024)
+        rc = N.lib().srg_comm_unique_id(buf, err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+        return buf.raw
+
+    def init_comm(self, nranks, rank, unique_id):
+        """Attach an RCCL communicator: later calls run SPMD across `nranks` GPUs."""
+        assert len(unique_id) == N.SRG_UNIQUE_ID_BYTES
+        err = ctypes.create_string_buffer(1024)
+        rc = N.lib().srg_comm_init(self._h, int(nranks), int(rank), bytes(unique_id), err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+
+    def init_comm_local(self, group, rank):
+        """Attach rank `rank` of an in-process LocalGroup (ranks are threads of this process)."""
+        err = ctypes.create_string_buffer(1024)
+        rc = N.lib().srg_comm_init_local(self._h, group._h, int(rank), err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+
+    def comm_size(self):
+        nr, rk = ctypes.c_int(), ctypes.c_int()
+        N.lib().srg_comm_size(self._h, ctypes.byref(nr), ctypes.byref(rk))
+        return nr.value, rk.value
+
     def get_direct_paths(self, edges, nodes):
         return self._run(N.lib().srg_get_direct_paths, edges, nodes)
+
+
+class LocalGroup:
+    """srg_local_group: N ranks inside one process (threads), e.g. several ranks on one GPU."""
+
+    def __init__(self, nranks):
+        h = ctypes.c_void_p()
+        rc = N.lib().srg_local_group_create(int(nranks), ctypes.byref(h))
+        if rc != N.SRG_OK:
+            _raise(rc, "srg_local_group_create failed")
+        self._h = h
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().srg_local_group_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Edges:

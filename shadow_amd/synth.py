@@ -77,25 +77,27 @@ def barabasi_albert(V=50000, m=4, seed=50000, lat_lo=1_000_000, lat_hi=50_000_00
     chosen proportionally to degree, networkx-style repeated-nodes list), undirected."""
     rng = np.random.default_rng(seed)
     s0, d0, l0, p0 = _selfloops(V, rng, fixed=1_000_000)
-    src, dst = [], []
-    repeated = []
+    E = (V - m) * m
+    src = np.empty(E, dtype=np.uint32)
+    dst = np.empty(E, dtype=np.uint32)
+    repeated = np.empty(2 * E, dtype=np.int64)  # endpoint multiset (degree-proportional)
+    nrep = 0
     targets = list(range(m))
+    k = 0
     for v in range(m, V):
-        for t in targets:
-            src.append(v)
-            dst.append(t)
-        repeated.extend(targets)
-        repeated.extend([v] * m)
+        src[k:k + m] = v
+        dst[k:k + m] = targets
+        k += m
+        repeated[nrep:nrep + m] = targets
+        repeated[nrep + m:nrep + 2 * m] = v
+        nrep += 2 * m
         chosen = set()
-        rep = np.asarray(repeated)
         while len(chosen) < m:
-            chosen.add(int(rep[rng.integers(0, len(rep))]))
+            chosen.add(int(repeated[rng.integers(0, nrep)]))
         targets = sorted(chosen)
-    E = len(src)
     lat = rng.integers(lat_lo, lat_hi + 1, size=E, dtype=np.uint64)
     loss = _loss(rng, E, 0.5, loss_hi)
-    return Edges(V, np.concatenate([s0, np.asarray(src, dtype=np.uint32)]),
-                 np.concatenate([d0, np.asarray(dst, dtype=np.uint32)]), np.concatenate([l0, lat]),
+    return Edges(V, np.concatenate([s0, src]), np.concatenate([d0, dst]), np.concatenate([l0, lat]),
                  np.concatenate([p0, loss]), directed=False)
 
 

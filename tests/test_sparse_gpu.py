@@ -1,0 +1,126 @@
+"""GPU parity of the sparse path (batched lexicographic Bellman-Ford, sparse.hip.h) against the
+oracle: latency bit-exact, packet_loss bit-exact (the north star allows 1e-6 relative; the
+lexicographic fixpoint is unique, so bits must match).  Forced on small random graphs (ties,
+parallel edges, directed, tiny losses) and auto-selected on Barabasi-Albert graphs (C4 shape)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from shadow_amd import LocalGroup, NetGraphError, Router, RoutingPanic, synth
+from shadow_amd import _native as N
+from shadow_amd.graph import Edges
+from helpers import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def bf_router():
+    r = Router(0)
+    r.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_SPARSE)
+    yield r
+    r.close()
+
+
+CASES = [
+    dict(V=50, density=0.2, seed=201, lat_hi=8),
+    dict(V=129, density=0.1, seed=202, directed=True, lat_hi=1000),
+    dict(V=130, density=0.3, seed=203, lat_hi=3, parallel=0.3),
+    dict(V=200, density=0.05, seed=204, directed=True, lat_hi=20, loss_hi=1e-6),
+    dict(V=300, density=0.02, seed=206, lat_hi=50),
+    dict(V=1000, density=0.004, seed=207, lat_hi=100),
+]
+
+
+@pytest.mark.parametrize("kw", CASES, ids=lambda k: f"V{k['V']}_s{k['seed']}")
+def test_bf_random_vs_oracle(bf_router, kw):
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    nodes = list(range(V))
+    try:
+        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    except oracle.OracleError as e:
+        with pytest.raises(NetGraphError) as ei:
+            bf_router.compute_shortest_paths(g, nodes)
+        assert ei.value.code == e.code
+        return
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    assert np.array_equal(t.latency_ns, lat)
+    assert bits_equal(t.packet_loss, loss)
+
+
+def test_bf_subset_scrambled(bf_router):
+    g = synth.random_graph(400, 0.02, 208, lat_hi=60)
+    nodes = np.random.default_rng(3).permutation(400)[:130].tolist()
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
+def test_bf_unreachable_panics(bf_router):
+    iso = Edges(4, [0, 1, 2, 3, 0], [0, 1, 2, 3, 1], [1, 1, 1, 1, 3], [0.0] * 5, False)
+    with pytest.raises(RoutingPanic):
+        bf_router.compute_shortest_paths(iso, [0, 1, 2, 3])
+    t = bf_router.compute_shortest_paths(iso, [0, 1])
+    assert t[(0, 1)].latency_ns == 3
+
+
+def test_bf_large_latency_falls_back_exactly(bf_router):
+    """Latencies whose sums may pass 2^32: saturated u32 keys hand over to the u64 dense path."""
+    g = synth.random_graph(120, 0.05, 209, lat_lo=2**30, lat_hi=2**31)
+    nodes = list(range(120))
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
+@pytest.mark.parametrize("V", [3000, 12000])
+def test_ba_auto_sparse_sampled(V):
+    """C4 shape (Barabasi-Albert m=4): auto-dispatch picks the sparse path; full matrix vs
+    seeded oracle rows, plus symmetric latency and the self-loop diagonal."""
+    e = synth.barabasi_albert(V, 4, seed=V)
+    r = Router(0)
+    nodes = list(range(V))
+    t = r.compute_shortest_paths(e, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    rows = np.random.default_rng(V).choice(V, 16, replace=False).tolist()
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, nthreads=16)
+    assert np.array_equal(t.latency_ns[rows], lat)
+    assert bits_equal(t.packet_loss[rows], loss)
+    assert np.array_equal(np.diag(t.latency_ns), np.full(V, 1_000_000, dtype=np.uint64))
+    off = ~np.eye(V, dtype=bool)
+    assert np.array_equal(t.latency_ns[off], t.latency_ns.T[off])
+    r.close()
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_bf_multi_rank(G):
+    e = synth.barabasi_albert(2500, 3, seed=77)
+    nodes = np.random.default_rng(5).permutation(2500)[:900].tolist()
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, nthreads=16)
+    group = LocalGroup(G)
+    routers = [Router(0) for _ in range(G)]
+    out = [None] * G
+    for i, rt in enumerate(routers):
+        rt.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_SPARSE)
+        rt.init_comm_local(group, i)
+
+    def work(i):
+        out[i] = routers[i].compute_shortest_paths(e, nodes)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(G)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    for i, t in enumerate(out):
+        assert t is not None, f"rank {i} failed"
+        assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+    for rt in routers:
+        rt.close()
+    group.close()
