@@ -81,6 +81,9 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
+    ap.add_argument("--simulate-rank", type=str, default=None,
+                    help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
+                         "(outputs invalid; prints a diagnostic line, never the bench result)")
     args = ap.parse_args()
     if args.graph == "ba" and args.vertices == 10000 and "--vertices" not in sys.argv:
         args.vertices = 50000
@@ -124,6 +127,9 @@ def main():
         router = Router(local)
     if args.no_locality:
         router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
+    if args.simulate_rank:
+        sg, sr = (int(x) for x in args.simulate_rank.split(":"))
+        router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)
 
     def step():
         return compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
@@ -197,6 +203,14 @@ def main():
                "sample": f"{k} random sources of the same 10k-vertex graph, reference-equivalent pipeline "
                          f"(HashMap-score Dijkstra + linear nodes.contains + HashMap merge), {sec:.1f}s"}
 
+    if args.simulate_rank:
+        n = args.steps
+        print(json.dumps({"diagnostic": "simulated rank (collectives elided, outputs invalid)",
+                          "simulate_rank": args.simulate_rank, "ms_per_step": round(ms_per_step, 3),
+                          "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in
+                                           ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange")},
+                          "roofline": roofline}), flush=True)
+        return
     if rank == 0:
         n = args.steps
         line = {

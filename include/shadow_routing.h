@@ -117,6 +117,8 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_ALGO_DENSE 1          /* blocked FW + tight-DAG loss pass */
 #define SRG_ALGO_SPARSE 2         /* batched lexicographic Bellman-Ford over CSR */
 #define SRG_OPT_SPARSE_LOCALITY 5 /* sparse: 1 (default) = batch sources in BFS order, 0 = in `nodes` order */
+#define SRG_OPT_SIMULATE_RANK 6   /* TIMING AID ONLY: value = nranks*1000 + rank runs this rank's share
+                                     with every collective elided -- outputs are NOT valid; 0 detaches */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

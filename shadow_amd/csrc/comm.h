@@ -35,6 +35,9 @@ struct Comm {
 std::string rccl_unique_id(unsigned char out[128]);
 std::string rccl_create(int nranks, int rank, const unsigned char id[128], int device, Comm** out);
 
+// Timing aid: collectives are no-ops (results invalid), see SRG_OPT_SIMULATE_RANK.
+Comm* null_create(int nranks, int rank);
+
 // In-process group of `nranks` ranks (threads of one process); each rank attaches one context.
 struct LocalGroup;
 LocalGroup* local_group_create(int nranks);

@@ -93,84 +93,114 @@ template <class K>
 __device__ __forceinline__ void st16(K* p, const Vec16<K>& v) { stv<K, 16 / sizeof(K)>(p, v); }
 
 // ---------------------------------------------------------------------------------------
-// Phase 1: close the pivot block D[kb][kb] (sequential k inside one workgroup).
-// The T x T block lives in registers (M x M per thread).  Step k needs only row k and
-// column k, so after updating, the owners of row k+1 / column k+1 publish them into a
-// parity double-buffered LDS strip (step k reads buffer k&1, writes buffer (k+1)&1):
-// one barrier per step and 2*T LDS words written instead of the whole block.
+// Phase 1: close the pivot block D[kb][kb] (the sequential k chain of FW; on the critical
+// path of the multi-GPU schedule, so it is latency-optimised).
+// 512 threads (2 waves per SIMD), thread (ty < 32, tx < 16) holds MR = T/32 rows x MC = T/16
+// columns in registers.  The k steps run in groups of R = 4 per barrier: at the start of a
+// group every thread reads the group's R pivot rows (its MC columns), R pivot columns (its
+// MR rows) and the R x R pivot sub-block from LDS, replays the group's R steps on those
+// cross values (tiny), and then folds all R steps into its own elements at once:
+//   c = min(c, C_0 + R_0, ..., C_{R-1} + R_{R-1})   (C_i, R_i = step-i values; v_min3 pairs)
+// which equals R sequential FW steps.  The owners then publish the next group's rows and
+// columns into the other half of a double-buffered LDS strip.
 template <class K, int T>
-__global__ void __launch_bounds__(256) fw_phase1(K* __restrict__ D, size_t ld, int kb) {
-    using G = Geo<K, T>;
-    constexpr int M = G::M;
-    __shared__ __attribute__((aligned(16))) K prow[2][T];
-    __shared__ __attribute__((aligned(16))) K pcol[2][T];
+struct P1Geo {
+    static constexpr int MR = T / 32, MC = T / 16;
+    static constexpr int HR = MR / 2, HC = MC / 2;
+    __device__ __forceinline__ static int row(int ty, int a) { return a < HR ? ty * HR + a : T / 2 + ty * HR + (a - HR); }
+    __device__ __forceinline__ static int col(int tx, int b) { return b < HC ? tx * HC + b : T / 2 + tx * HC + (b - HC); }
+};
+
+template <class K, int T>
+__global__ void __launch_bounds__(512) fw_phase1(K* __restrict__ D, size_t ld, int kb) {
+    using G = P1Geo<K, T>;
+    constexpr int MR = G::MR, MC = G::MC, HR = G::HR, HC = G::HC;
+    constexpr int R = 4;
+    __shared__ __attribute__((aligned(16))) K prow[2][R][T];  // prow[.][j][col] = D[k0+j][col]
+    __shared__ __attribute__((aligned(16))) K pcol[2][R][T];  // pcol[.][j][row] = D[row][k0+j]
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
     K* base = D + (size_t)kb * T * ld + (size_t)kb * T;
-    K c[M][M];
+    K c[MR][MC];
 #pragma unroll
-    for (int a = 0; a < M; ++a) {
-        const int r = G::rc(ty, a);
+    for (int a = 0; a < MR; ++a)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            VecN<K, G::H> v = ldv<K, G::H>(base + (size_t)r * ld + G::rc(tx, h * G::H));
+            VecN<K, HC> v = ldv<K, HC>(base + (size_t)G::row(ty, a) * ld + G::col(tx, h * HC));
 #pragma unroll
-            for (int e = 0; e < G::H; ++e) c[a][h * G::H + e] = v.v[e];
+            for (int e = 0; e < HC; ++e) c[a][h * HC + e] = v.v[e];
         }
-    }
-    // publish row 0 / column 0
+    auto publish = [&](int q, int k0) {
 #pragma unroll
-    for (int a = 0; a < M; ++a) {
-        if (G::rc(ty, a) == 0) {
+        for (int a = 0; a < MR; ++a) {
+            const int r = G::row(ty, a) - k0;
+            if (r >= 0 && r < R) {
 #pragma unroll
-            for (int b = 0; b < M; ++b) prow[0][G::rc(tx, b)] = c[a][b];
+                for (int b = 0; b < MC; ++b) prow[q][r][G::col(tx, b)] = c[a][b];
+            }
         }
-        if (G::rc(tx, a) == 0) {
 #pragma unroll
-            for (int b = 0; b < M; ++b) pcol[0][G::rc(ty, b)] = c[b][a];
+        for (int b = 0; b < MC; ++b) {
+            const int j = G::col(tx, b) - k0;
+            if (j >= 0 && j < R) {
+#pragma unroll
+                for (int a = 0; a < MR; ++a) pcol[q][j][G::row(ty, a)] = c[a][b];
+            }
         }
-    }
+    };
+    publish(0, 0);
     __syncthreads();
-    for (int k = 0; k < T; ++k) {
-        const int p = k & 1;
-        K colk[M], rowk[M];
+    for (int g = 0; g < T / R; ++g) {
+        const int q = g & 1, k0 = g * R;
+        K Rv[R][MC], Cv[MR][R], Pv[R][R];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            VecN<K, G::H> vc = ldv<K, G::H>(&pcol[p][G::rc(ty, h * G::H)]);
-            VecN<K, G::H> vr = ldv<K, G::H>(&prow[p][G::rc(tx, h * G::H)]);
+        for (int j = 0; j < R; ++j) {
 #pragma unroll
-            for (int e = 0; e < G::H; ++e) {
-                colk[h * G::H + e] = vc.v[e];
-                rowk[h * G::H + e] = vr.v[e];
+            for (int h = 0; h < 2; ++h) {
+                VecN<K, HC> vr = ldv<K, HC>(&prow[q][j][G::col(tx, h * HC)]);
+                VecN<K, HR> vc = ldv<K, HR>(&pcol[q][j][G::row(ty, h * HR)]);
+#pragma unroll
+                for (int e = 0; e < HC; ++e) Rv[j][h * HC + e] = vr.v[e];
+#pragma unroll
+                for (int e = 0; e < HR; ++e) Cv[h * HR + e][j] = vc.v[e];
             }
+#pragma unroll
+            for (int i = 0; i < R; ++i) Pv[j][i] = prow[q][j][k0 + i];
         }
+        // replay the group's steps on the cross values
 #pragma unroll
-        for (int a = 0; a < M; ++a)
+        for (int i = 0; i < R; ++i) {
 #pragma unroll
-            for (int b = 0; b < M; ++b) c[a][b] = KeyOps<K>::min2(c[a][b], KeyOps<K>::add(colk[a], rowk[b]));
-        if (k + 1 < T) {
-            const int q = (k + 1) & 1;
+            for (int x = i + 1; x < R; ++x)
 #pragma unroll
-            for (int a = 0; a < M; ++a) {
-                if (G::rc(ty, a) == k + 1) {
+                for (int b = 0; b < MC; ++b) Rv[x][b] = KeyOps<K>::min2(Rv[x][b], KeyOps<K>::add(Pv[x][i], Rv[i][b]));
 #pragma unroll
-                    for (int b = 0; b < M; ++b) prow[q][G::rc(tx, b)] = c[a][b];
-                }
-                if (G::rc(tx, a) == k + 1) {
+            for (int y = i + 1; y < R; ++y)
 #pragma unroll
-                    for (int b = 0; b < M; ++b) pcol[q][G::rc(ty, b)] = c[b][a];
-                }
+                for (int a = 0; a < MR; ++a) Cv[a][y] = KeyOps<K>::min2(Cv[a][y], KeyOps<K>::add(Cv[a][i], Pv[i][y]));
+#pragma unroll
+            for (int x = i + 1; x < R; ++x)
+#pragma unroll
+                for (int y = i + 1; y < R; ++y) Pv[x][y] = KeyOps<K>::min2(Pv[x][y], KeyOps<K>::add(Pv[x][i], Pv[i][y]));
+        }
+        // fold the R steps into the own elements
+#pragma unroll
+        for (int a = 0; a < MR; ++a)
+#pragma unroll
+            for (int b = 0; b < MC; ++b) {
+                K v = KeyOps<K>::min3(c[a][b], KeyOps<K>::add(Cv[a][0], Rv[0][b]), KeyOps<K>::add(Cv[a][1], Rv[1][b]));
+                c[a][b] = KeyOps<K>::min3(v, KeyOps<K>::add(Cv[a][2], Rv[2][b]), KeyOps<K>::add(Cv[a][3], Rv[3][b]));
             }
-        }
+        if (g + 1 < T / R) publish(q ^ 1, k0 + R);
         __syncthreads();
     }
 #pragma unroll
-    for (int a = 0; a < M; ++a)
+    for (int a = 0; a < MR; ++a)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            VecN<K, G::H> v;
+            VecN<K, HC> v;
 #pragma unroll
-            for (int e = 0; e < G::H; ++e) v.v[e] = c[a][h * G::H + e];
-            stv<K, G::H>(base + (size_t)G::rc(ty, a) * ld + G::rc(tx, h * G::H), v);
+            for (int e = 0; e < HC; ++e) v.v[e] = c[a][h * HC + e];
+            stv<K, HC>(base + (size_t)G::row(ty, a) * ld + G::col(tx, h * HC), v);
         }
 }
 
@@ -278,8 +308,34 @@ __device__ __forceinline__ int tile_kept(int base, int idx, int x0, int x1) {
     return v;
 }
 
+// gridDim.z > 1 splits the pivot block's k range across workgroups (split-K): each split
+// reduces its share and merges with atomicMin, which is exact because min is associative and
+// commutative (used for the short launches on the multi-GPU critical path).
+template <class K, int T, int KC>
+__device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J);
+
 template <class K, int T, int KC>
 __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
+    fw_tile<K, T, KC>(D, ld, kb, tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1),
+                      tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1));
+}
+
+// Two tile sets in one launch (the pivot's row panel and column panel: they are independent
+// once the pivot tile is closed, and each is a single short wave of workgroups, so one launch
+// instead of two takes a tile latency off the FW critical path).  grid.x = na + nb tiles;
+// set s is nc_s columns wide, tiles flattened row-major.
+template <class K, int T, int KC>
+__global__ void __launch_bounds__(256) fw_product_pair(K* __restrict__ D, size_t ld, int kb, TileSet a, int na,
+                                                       int nca, TileSet b, int ncb) {
+    int x = (int)blockIdx.x;
+    const TileSet& t = x < na ? a : b;
+    const int nc = x < na ? nca : ncb;
+    if (x >= na) x -= na;
+    fw_tile<K, T, KC>(D, ld, kb, tile_kept(t.r0, x / nc, t.rx0, t.rx1), tile_kept(t.c0, x % nc, t.cx0, t.cx1));
+}
+
+template <class K, int T, int KC>
+__device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J) {
     using G = Geo<K, T>;
     constexpr int M = G::M;
     constexpr int VE = 16 / (int)sizeof(K);
@@ -288,9 +344,6 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     K* lds = reinterpret_cast<K*>(smem_raw);
     __shared__ uint32_t arow[T];
-
-    const int I = tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1);
-    const int J = tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1);
     K* C = D + (size_t)I * T * ld + (size_t)J * T;
     const K* A = D + (size_t)kb * T;                       // column block kb, rows via arow
     const K* B = D + (size_t)kb * T * ld + (size_t)J * T;  // row block kb, cols J
@@ -298,25 +351,34 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
     if (tid < T) arow[tid] = I * T + tid;
     __syncthreads();
 
+    constexpr int NCH = T / KC;
+    const int nsplit = (int)gridDim.z;
+    const int ch0 = (int)blockIdx.z * NCH / nsplit, ch1 = ((int)blockIdx.z + 1) * NCH / nsplit;
     Stage<K, T, KC> sg;
-    stage_load<K, T, KC>(sg, A, B, ld, arow, 0);
+    stage_load<K, T, KC>(sg, A, B, ld, arow, ch0 * KC);
     K c[M][M];
+    if (nsplit == 1) {
 #pragma unroll
-    for (int a = 0; a < M; ++a)
+        for (int a = 0; a < M; ++a)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            VecN<K, G::H> v = ldv<K, G::H>(C + (size_t)G::rc(ty, a) * ld + G::rc(tx, h * G::H));
+            for (int h = 0; h < 2; ++h) {
+                VecN<K, G::H> v = ldv<K, G::H>(C + (size_t)G::rc(ty, a) * ld + G::rc(tx, h * G::H));
 #pragma unroll
-            for (int e = 0; e < G::H; ++e) c[a][h * G::H + e] = v.v[e];
-        }
+                for (int e = 0; e < G::H; ++e) c[a][h * G::H + e] = v.v[e];
+            }
+    } else {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int b = 0; b < M; ++b) c[a][b] = KeyOps<K>::INF;
+    }
     stage_store<K, T, KC>(sg, lds, lds + KC * LDP);
     __syncthreads();
-    constexpr int NCH = T / KC;
 #pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
-        const K* At = lds + (ch & 1) * BUF;
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const K* At = lds + ((ch - ch0) & 1) * BUF;
         const K* Bs = At + KC * LDP;
-        if (ch + 1 < NCH) stage_load<K, T, KC>(sg, A, B, ld, arow, (ch + 1) * KC);  // issue early
+        if (ch + 1 < ch1) stage_load<K, T, KC>(sg, A, B, ld, arow, (ch + 1) * KC);  // issue early
 #pragma unroll 4
         for (int kk = 0; kk < KC; kk += 2) {
             K a0[M], a1[M], b0[M], b1[M];
@@ -341,21 +403,28 @@ __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, 
                     c[a][b] = KeyOps<K>::min3(c[a][b], KeyOps<K>::add(a0[a], b0[b]),
                                               KeyOps<K>::add(a1[a], b1[b]));
         }
-        if (ch + 1 < NCH) {  // write late into the other buffer
-            K* Ant = lds + ((ch + 1) & 1) * BUF;
+        if (ch + 1 < ch1) {  // write late into the other buffer
+            K* Ant = lds + ((ch + 1 - ch0) & 1) * BUF;
             stage_store<K, T, KC>(sg, Ant, Ant + KC * LDP);
         }
         __syncthreads();
     }
+    if (nsplit == 1) {
 #pragma unroll
-    for (int a = 0; a < M; ++a)
+        for (int a = 0; a < M; ++a)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            VecN<K, G::H> v;
+            for (int h = 0; h < 2; ++h) {
+                VecN<K, G::H> v;
 #pragma unroll
-            for (int e = 0; e < G::H; ++e) v.v[e] = c[a][h * G::H + e];
-            stv<K, G::H>(C + (size_t)G::rc(ty, a) * ld + G::rc(tx, h * G::H), v);
-        }
+                for (int e = 0; e < G::H; ++e) v.v[e] = c[a][h * G::H + e];
+                stv<K, G::H>(C + (size_t)G::rc(ty, a) * ld + G::rc(tx, h * G::H), v);
+            }
+    } else {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int b = 0; b < M; ++b) atomicMin(C + (size_t)G::rc(ty, a) * ld + G::rc(tx, b), c[a][b]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------

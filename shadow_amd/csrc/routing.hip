@@ -184,6 +184,57 @@ __global__ void k_w_loss(uint64_t E, const uint32_t* __restrict__ src, const uin
     }
 }
 
+// u32 keys: one pass over the edges with a packed lexicographic key
+//   KW[s][t] = min over parallel edges of (latency << 32 | loss bits)    (mod.rs:305-313)
+// (loss in [0,1] is non-negative, so its f32 bit order is its numeric order).
+__global__ void k_w_key(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                        const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                        unsigned long long* __restrict__ KW, size_t ld) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s == t) continue;  // self-loops never shorten a path; kept for the diagonal only
+        const unsigned long long k = ((unsigned long long)lat[e] << 32) | __float_as_uint(loss[e] + 0.0f);
+        atomicMin(&KW[(size_t)s * ld + t], k);
+    }
+}
+
+// 64x64 tiles: (undirected) KW = min(KW, KW^T), then split into W (latency), WL (loss bits)
+// and D (= W with a zero diagonal).  grid = (nb64, nb64) over the upper triangle incl. diagonal
+// blocks when undirected (each block pair handled once), all blocks when directed.
+__global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __restrict__ KW, size_t ld, int directed,
+                                                 uint32_t* __restrict__ W, uint32_t* __restrict__ WL,
+                                                 uint32_t* __restrict__ D) {
+    __shared__ unsigned long long tb[64][65];
+    const uint32_t bi = blockIdx.y, bj = blockIdx.x;
+    if (!directed && bj < bi) return;
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    if (!directed) {
+        for (uint32_t r = ty; r < 64; r += 4) tb[r][tx] = KW[(size_t)(bj * 64 + r) * ld + bi * 64 + tx];  // (bj, bi)
+        __syncthreads();
+    }
+    for (uint32_t r = ty; r < 64; r += 4) {
+        const size_t i = bi * 64 + r, j = bj * 64 + tx;
+        unsigned long long k = KW[i * ld + j];
+        if (!directed) k = min(k, tb[tx][r]);
+        const uint32_t w = (uint32_t)(k >> 32);
+        W[i * ld + j] = w;
+        WL[i * ld + j] = (uint32_t)k;
+        D[i * ld + j] = i == j ? 0u : w;
+        if (!directed && bi != bj) tb[tx][r] = k;  // the mirrored element, written below
+    }
+    if (!directed && bi != bj) {
+        __syncthreads();
+        for (uint32_t r = ty; r < 64; r += 4) {
+            const size_t i = bj * 64 + r, j = bi * 64 + tx;
+            const unsigned long long k = tb[r][tx];
+            const uint32_t w = (uint32_t)(k >> 32);
+            W[i * ld + j] = w;
+            WL[i * ld + j] = (uint32_t)k;
+            D[i * ld + j] = w;
+        }
+    }
+}
+
 template <class K>
 __global__ void k_init_d(const K* __restrict__ W, K* __restrict__ D, size_t ld) {
     const size_t total = ld * ld;
@@ -263,7 +314,8 @@ __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, 
                           const uint32_t* __restrict__ snodes, uint32_t nloc, const uint32_t* __restrict__ cols,
                           uint32_t ncols, const uint32_t* __restrict__ rowpos,
                           const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
-                          uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags) {
+                          uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags, int mode) {
+    // mode bit 0: latency (+ unreachable check), bit 1: loss from L
     const size_t total = (size_t)nloc * ncols;
     uint32_t unreach = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -271,13 +323,16 @@ __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, 
         const uint32_t s = snodes[a], t = cols[b], p = rowpos[a];
         const size_t o = (size_t)p * ncols + b;
         if (p == b) {
-            out_lat[o] = self_lat[s];  // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
-            if (L) out_loss[o] = self_loss[s];
+            // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
+            if (mode & 1) out_lat[o] = self_lat[s];
+            if (mode & 2) out_loss[o] = self_loss[s];
         } else {
-            const K d = D[(size_t)s * ld + t];
-            unreach |= d == KeyOps<K>::INF;
-            out_lat[o] = (uint64_t)d;
-            if (L) out_loss[o] = L[a * ld + t];
+            if (mode & 1) {
+                const K d = D[(size_t)s * ld + t];
+                unreach |= d == KeyOps<K>::INF;
+                out_lat[o] = (uint64_t)d;
+            }
+            if (mode & 2) out_loss[o] = L[a * ld + t];
         }
     }
     if (unreach) atomicOr(&flags->unreachable_used_pair, 1u);
@@ -350,7 +405,7 @@ struct srg_ctx {
     hipStream_t stream = nullptr;
     hipStream_t aux_stream = nullptr;   // FW lookahead: phase 1/2 of the next pivot block
     hipStream_t comm_stream = nullptr;  // pivot-panel broadcasts (multi-rank)
-    hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr, ev_e = nullptr;
     std::mutex mu;
     DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
     DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
@@ -369,7 +424,7 @@ struct srg_ctx {
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e})
             if (e) (void)hipEventDestroy(e);
         for (hipStream_t s : {aux_stream, comm_stream, stream})
             if (s) (void)hipStreamDestroy(s);
@@ -526,9 +581,12 @@ Plan make_plan(int G, int g, uint32_t V, int T, const std::vector<uint32_t>& nod
 constexpr int KC = 32;
 
 // tiles of one min-plus product launch: rows [ra, rb) minus {rx...}, cols [ca, cb) minus {cx...}
-template <class K, int T>
-void fw_tiles(K* D, size_t ld, int kb, int ra, int rb, std::initializer_list<int> rx, int ca, int cb,
-              std::initializer_list<int> cx, size_t lds, hipStream_t s) {
+struct Rect {
+    TileSet ts;
+    int nr, nc;
+};
+
+inline Rect make_rect(int ra, int rb, std::initializer_list<int> rx, int ca, int cb, std::initializer_list<int> cx) {
     auto norm = [](int a, int b, std::initializer_list<int> x, int& x0, int& x1) {
         std::vector<int> v;
         for (int e : x)
@@ -538,13 +596,41 @@ void fw_tiles(K* D, size_t ld, int kb, int ra, int rb, std::initializer_list<int
         x1 = v.size() > 1 ? v[1] : -1;
         return std::max(0, b - a - (int)v.size());
     };
-    TileSet ts;
-    const int nr = norm(ra, rb, rx, ts.rx0, ts.rx1);
-    const int nc = norm(ca, cb, cx, ts.cx0, ts.cx1);
-    if (nr <= 0 || nc <= 0) return;
-    ts.r0 = ra;
-    ts.c0 = ca;
-    fw_product<K, T, KC><<<dim3(nc, nr), 256, lds, s>>>(D, ld, kb, ts);
+    Rect r;
+    r.nr = norm(ra, rb, rx, r.ts.rx0, r.ts.rx1);
+    r.nc = norm(ca, cb, cx, r.ts.cx0, r.ts.cx1);
+    r.ts.r0 = ra;
+    r.ts.c0 = ca;
+    return r;
+}
+
+// split-K factor for a short launch of `tiles` workgroups (critical-path launches only)
+template <int T>
+int split_for(int tiles, bool enable) {
+    if (!enable) return 1;
+    constexpr int maxs = T / KC;
+    int sp = 1;
+    while (sp < maxs && tiles * sp * 2 <= 512) sp *= 2;
+    return sp;
+}
+
+template <class K, int T>
+void fw_tiles(K* D, size_t ld, int kb, int ra, int rb, std::initializer_list<int> rx, int ca, int cb,
+              std::initializer_list<int> cx, size_t lds, hipStream_t s, bool split = false) {
+    const Rect r = make_rect(ra, rb, rx, ca, cb, cx);
+    if (r.nr <= 0 || r.nc <= 0) return;
+    const int sp = split_for<T>(r.nr * r.nc, split);
+    fw_product<K, T, KC><<<dim3(r.nc, r.nr, sp), 256, lds, s>>>(D, ld, kb, r.ts);
+}
+
+template <class K, int T>
+void fw_tiles_pair(K* D, size_t ld, int kb, const Rect& a, const Rect& b, size_t lds, hipStream_t s,
+                   bool split = false) {
+    const int na = std::max(0, a.nr) * std::max(0, a.nc), nb = std::max(0, b.nr) * std::max(0, b.nc);
+    if (na + nb == 0) return;
+    const int sp = split_for<T>(na + nb, split);
+    fw_product_pair<K, T, KC><<<dim3(na + nb, 1, sp), 256, lds, s>>>(D, ld, kb, a.ts, na, std::max(1, a.nc), b.ts,
+                                                                    std::max(1, b.nc));
 }
 
 // Blocked Floyd-Warshall over the rank's row blocks with a one-block lookahead:
@@ -557,6 +643,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     const int nb = pl.nb;
     const size_t lds = (size_t)4 * KC * (T + 16 / (int)sizeof(K)) * sizeof(K);  // double-buffered A^T + B
     set_lds(fw_product<K, T, KC>, lds);
+    set_lds(fw_product_pair<K, T, KC>, lds);
     const bool multi = c.comm && c.comm->nranks > 1;
     const bool prof = c.profiling && nb > 2;
     if (prof) {
@@ -572,8 +659,8 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     const int r0 = pl.rb0, r1 = pl.rb1;
     // pivot 0
     if (pl.own(0)) {
-        fw_phase1<K, T><<<1, 256, 0, st>>>(D, Vp, 0);
-        fw_tiles<K, T>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st);
+        fw_phase1<K, T><<<1, 512, 0, st>>>(D, Vp, 0);
+        fw_tiles<K, T>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st, pl.G > 1);
     }
     if (multi) {
         HIP_CHECK(hipEventRecord(c.ev_c, st));
@@ -589,22 +676,30 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
             break;
         }
         const int k1 = kb + 1;
-        if (pl.own(k1)) fw_tiles<K, T>(D, Vp, kb, k1, k1 + 1, {}, 0, nb, {kb}, lds, st);  // row k1
-        fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb, k1}, k1, k1 + 1, {}, lds, st);             // own col k1
+        // critical chain: row k1 (w.r.t. kb) -> close pivot k1 -> its row + column panels
+        const bool sk = pl.G > 1;  // split-K the chain's short launches when the rest is short too
+        if (pl.own(k1)) fw_tiles<K, T>(D, Vp, kb, k1, k1 + 1, {}, 0, nb, {kb}, lds, st, sk);  // row k1
         HIP_CHECK(hipEventRecord(c.ev_a, st));
+        fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb, k1}, k1, k1 + 1, {}, lds, st, sk);             // own col k1
+        HIP_CHECK(hipEventRecord(c.ev_e, st));
         HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
+        const Rect colp = make_rect(r0, r1, {k1}, k1, k1 + 1, {});  // own column panel of k1
         if (pl.own(k1)) {
-            fw_phase1<K, T><<<1, 256, 0, aux>>>(D, Vp, k1);
-            fw_tiles<K, T>(D, Vp, k1, k1, k1 + 1, {}, 0, nb, {k1}, lds, aux);  // row panel k1
+            fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1);
+            HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
+            fw_tiles_pair<K, T>(D, Vp, k1, make_rect(k1, k1 + 1, {}, 0, nb, {k1}), colp, lds, aux, sk);
         }
         if (multi) {
             HIP_CHECK(hipEventRecord(c.ev_b, aux));
             HIP_CHECK(hipStreamWaitEvent(cs, c.ev_b, 0));
             c.comm->bcast(panel(k1), panel_bytes, pl.owner(k1), cs);
             HIP_CHECK(hipEventRecord(c.ev_c, cs));
-            if (!pl.own(k1)) HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));  // pivot tile arrives in the panel
+            if (!pl.own(k1)) {  // the pivot tile arrives in the panel
+                HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
+                HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
+                fw_tiles_pair<K, T>(D, Vp, k1, Rect{TileSet{0, -1, -1, 0, -1, -1}, 0, 0}, colp, lds, aux, sk);
+            }
         }
-        fw_tiles<K, T>(D, Vp, k1, r0, r1, {k1}, k1, k1 + 1, {}, lds, aux);  // own col panel k1
         HIP_CHECK(hipEventRecord(c.ev_d, aux));
         // the remaining tiles of kb (the dominant kernel), overlapped with the above
         const int nr = (r1 - r0) - (pl.own(kb) ? 1 : 0) - (pl.own(k1) ? 1 : 0);
@@ -634,14 +729,24 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     K* W = (K*)c.b_W.get(VV * sizeof(K));
     uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
     K* D = (K*)c.b_D.get(VV * sizeof(K));
-    if (sizeof(K) == 4) HIP_CHECK(hipMemsetAsync(W, 0xFF, VV * 4, st));
-    else k_fill<K><<<grid_for(VV), kThreads, 0, st>>>(W, VV, KeyOps<K>::INF);
-    HIP_CHECK(hipMemsetAsync(WL, 0xFF, VV * 4, st));
-    if (g.E) {
-        k_w_lat<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.directed, W, Vp);
-        k_w_loss<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, W, WL, Vp);
+    if constexpr (sizeof(K) == 4) {
+        // packed (latency, loss) keys: one atomic pass, then a tiled symmetrize + split pass
+        static_assert(T % 64 == 0, "tile");
+        unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
+        HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, st));
+        if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, KW, Vp);
+        const unsigned nb64 = (unsigned)(Vp / 64);
+        k_w_split<<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, (uint32_t*)W, WL, (uint32_t*)D);
+    } else {
+        k_fill<K><<<grid_for(VV), kThreads, 0, st>>>(W, VV, KeyOps<K>::INF);
+        HIP_CHECK(hipMemsetAsync(WL, 0xFF, VV * 4, st));
+        if (g.E) {
+            k_w_lat<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.directed, W, Vp);
+            k_w_loss<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, W, WL,
+                                                             Vp);
+        }
+        k_init_d<K><<<grid_for(VV), kThreads, 0, st>>>(W, D, Vp);
     }
-    k_init_d<K><<<grid_for(VV), kThreads, 0, st>>>(W, D, Vp);
     // local sources and their output rows
     const uint32_t nloc = (uint32_t)pl.lnodes.size();
     uint32_t* lnodes = (uint32_t*)c.b_lnodes.get(std::max<size_t>(nloc, 1) * 4);
@@ -671,16 +776,79 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         stats->prof_relaxations += prof_relax;
     }
 
+    // Every collective after FW runs on the comm stream, in the same order on every rank:
+    // allreduce(certify) -> allreduce(unreachable) -> allgather(latency rows, overlapped with
+    // the scan) -> allgather(essential bitmask) -> allgather(loss rows).
+    hipStream_t cs = c.comm_stream;
+    auto cs_after_st = [&]() {
+        HIP_CHECK(hipEventRecord(c.ev_a, st));
+        HIP_CHECK(hipStreamWaitEvent(cs, c.ev_a, 0));
+    };
+    auto st_after_cs = [&]() {
+        HIP_CHECK(hipEventRecord(c.ev_b, cs));
+        HIP_CHECK(hipStreamWaitEvent(st, c.ev_b, 0));
+    };
+    auto reduce_flag = [&](uint32_t* flag_dev) -> uint32_t {
+        uint32_t* red = (uint32_t*)c.b_red.get(16);
+        HIP_CHECK(hipMemcpyAsync(red, flag_dev, 4, hipMemcpyDeviceToDevice, st));
+        if (multi) {
+            cs_after_st();
+            c.comm->allreduce_max_u32(red, 1, cs);
+            st_after_cs();
+        }
+        uint32_t v = 0;
+        HIP_CHECK(hipMemcpyAsync(&v, red, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        return v;
+    };
+    // output rows of every rank: [first[r], first[r] + cnt[r]) in rank order (staged when the
+    // ranks' rows are not contiguous in `nodes` order)
+    const bool exchange = multi && c.gather_output;
+    if (exchange && !pl.contiguous) {
+        c.b_stage.get((size_t)n * n * 8);
+        uint32_t* allpos = (uint32_t*)c.b_allpos.get((size_t)n * 4);
+        HIP_CHECK(hipMemcpyAsync(allpos, pl.allpos.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    }
+    auto exchange_rows = [&](void* out, size_t elem) {  // on cs, after st
+        const size_t row = (size_t)n * elem;
+        std::vector<size_t> offs(pl.G), lens(pl.G);
+        for (int r = 0; r < pl.G; ++r) {
+            offs[r] = (size_t)pl.first[r] * row;
+            lens[r] = (size_t)pl.cnt[r] * row;
+        }
+        cs_after_st();
+        if (pl.contiguous) {
+            c.comm->allgatherv(out, offs.data(), lens.data(), cs);
+            return;
+        }
+        unsigned char* stage = (unsigned char*)c.b_stage.p;
+        const uint32_t* allpos = (const uint32_t*)c.b_allpos.p;
+        if (nloc)
+            k_rows_copy<<<std::min<uint32_t>(nloc, 4096), 256, 0, cs>>>((const unsigned char*)out, stage + offs[pl.g],
+                                                                      lpos, nloc, row, 0);
+        c.comm->allgatherv(stage, offs.data(), lens.data(), cs);
+        k_rows_copy<<<std::min<uint32_t>(n, 4096), 256, 0, cs>>>(stage, (unsigned char*)out, allpos, n, row, 1);
+        HIP_CHECK(hipGetLastError());
+    };
+
     // u32 certification: no saturated key in any used row (every rank must agree)
-    uint32_t* red = (uint32_t*)c.b_red.get(16);
     HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
     if (nloc) k_certify<K><<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(D, Vp, lnodes, nloc, V, P.flags);
-    HIP_CHECK(hipMemcpyAsync(red, &P.flags->inf_in_used_row, 4, hipMemcpyDeviceToDevice, st));
-    if (multi) c.comm->allreduce_max_u32(red, 1, st);
-    uint32_t inf_any = 0;
-    HIP_CHECK(hipMemcpyAsync(&inf_any, red, 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    const uint32_t inf_any = reduce_flag(&P.flags->inf_in_used_row);
     if (sizeof(K) == 4 && inf_any) return false;  // saturated or unreachable: redo in u64
+
+    // latency outputs (+ diagonal self-loops) of the own rows, right after FW
+    HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
+    if (nloc)
+        k_extract<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, nullptr, Vp, lnodes, nloc, nodes, n, lpos,
+                                                                      P.selflat, P.selfloss, out_lat, out_loss,
+                                                                      P.flags, 1);
+    HIP_CHECK(hipGetLastError());
+    if (reduce_flag(&P.flags->unreachable_used_pair))
+        fail(SRG_ERR_UNREACHABLE,
+             "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
+             "from another used node)");
+    if (exchange) exchange_rows(out_lat, 8);  // overlaps the scan and the loss pass below
 
     // ---- essential edges, tight-predecessor scan, loss ----
     constexpr int TS = 64;
@@ -710,7 +878,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             offs[r] = a * nw64 * 8;
             lens[r] = (b - a) * nw64 * 8;
         }
-        c.comm->allgatherv(ess, offs.data(), lens.data(), st);
+        cs_after_st();
+        c.comm->allgatherv(ess, offs.data(), lens.data(), cs);
+        st_after_cs();
     }
     const size_t NQ = (size_t)nbT * V;
     uint32_t* ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
@@ -845,48 +1015,18 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     HIP_CHECK(hipMemcpyAsync(&nmulti, multi_cnt, 8, hipMemcpyDeviceToHost, st));
     const double ms_loss = tm.lap();
 
-    HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
-    if (nloc)
-        k_extract<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, loss_written ? nullptr : Lfin, Vp, lnodes,
-                                                                      nloc, nodes, n, lpos, P.selflat, P.selfloss,
-                                                                      out_lat, out_loss, P.flags);
+    if (nloc && !loss_written)
+        k_extract<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, Lfin, Vp, lnodes, nloc, nodes, n, lpos,
+                                                                      P.selflat, P.selfloss, out_lat, out_loss,
+                                                                      P.flags, 2);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMemcpyAsync(red, &P.flags->unreachable_used_pair, 4, hipMemcpyDeviceToDevice, st));
-    if (multi) c.comm->allreduce_max_u32(red, 1, st);
-    uint32_t unreach = 0;
-    HIP_CHECK(hipMemcpyAsync(&unreach, red, 4, hipMemcpyDeviceToHost, st));
     const double ms_extract = tm.lap();
-    if (unreach)
-        fail(SRG_ERR_UNREACHABLE,
-             "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
-             "from another used node)");
 
     // ---- output exchange: every rank ends with all n x n rows ----
     double ms_exchange = 0;
-    if (multi && c.gather_output) {
-        std::vector<size_t> offs(pl.G), lens(pl.G);
-        auto exchange = [&](void* out, size_t elem) {
-            const size_t row = (size_t)n * elem;
-            for (int r = 0; r < pl.G; ++r) {
-                offs[r] = (size_t)pl.first[r] * row;
-                lens[r] = (size_t)pl.cnt[r] * row;
-            }
-            if (pl.contiguous) {
-                c.comm->allgatherv(out, offs.data(), lens.data(), st);
-                return;
-            }
-            unsigned char* stage = (unsigned char*)c.b_stage.get((size_t)n * row);
-            uint32_t* allpos = (uint32_t*)c.b_allpos.get((size_t)n * 4);
-            HIP_CHECK(hipMemcpyAsync(allpos, pl.allpos.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-            if (nloc)
-                k_rows_copy<<<std::min<uint32_t>(nloc, 4096), 256, 0, st>>>(
-                    (const unsigned char*)out, stage + offs[pl.g], lpos, nloc, row, 0);
-            c.comm->allgatherv(stage, offs.data(), lens.data(), st);
-            k_rows_copy<<<std::min<uint32_t>(n, 4096), 256, 0, st>>>(stage, (unsigned char*)out, allpos, n, row, 1);
-            HIP_CHECK(hipGetLastError());
-        };
-        exchange(out_lat, 8);
-        exchange(out_loss, 4);
+    if (exchange) {
+        exchange_rows(out_loss, 4);
+        st_after_cs();
         ms_exchange = tm.lap();
     }
     if (stats) {
@@ -1239,9 +1379,13 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c->device = device;
         HIP_CHECK(hipSetDevice(device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+        // the FW lookahead chain (pivot close, row/col panels) is latency-critical: its workgroups
+        // should be dispatched ahead of the bulk phase-3 tiles
+        int prio_lo = 0, prio_hi = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIP_CHECK(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d})
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     });
     if (rc != SRG_OK) {
@@ -1266,6 +1410,18 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_GATHER_OUTPUT:
             ctx->gather_output = value != 0.0;
             return SRG_OK;
+        case SRG_OPT_SIMULATE_RANK: {
+            // value = nranks * 1000 + rank; 0 detaches
+            const int v = (int)value;
+            delete ctx->comm;
+            ctx->comm = nullptr;
+            if (v > 0) {
+                const int nr = v / 1000, rk = v % 1000;
+                if (nr < 1 || rk >= nr) return SRG_ERR_ARG;
+                ctx->comm = srg::null_create(nr, rk);
+            }
+            return SRG_OK;
+        }
         case SRG_OPT_SPARSE_LOCALITY:
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
