@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
+    ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--simulate-rank", type=str, default=None,
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
                          "(outputs invalid; prints a diagnostic line, never the bench result)")
@@ -127,6 +128,8 @@ def main():
         router = Router(local)
     if args.no_locality:
         router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
+    if args.fw_tile:
+        router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
     if args.simulate_rank:
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)

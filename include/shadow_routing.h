@@ -119,6 +119,7 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SPARSE_LOCALITY 5 /* sparse: 1 (default) = batch sources in BFS order, 0 = in `nodes` order */
 #define SRG_OPT_SIMULATE_RANK 6   /* TIMING AID ONLY: value = nranks*1000 + rank runs this rank's share
                                      with every collective elided -- outputs are NOT valid; 0 detaches */
+#define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

@@ -33,6 +33,7 @@ SRG_OPT_GATHER_OUTPUT = 3
 SRG_OPT_ALGORITHM = 4
 SRG_OPT_SPARSE_LOCALITY = 5
 SRG_OPT_SIMULATE_RANK = 6
+SRG_OPT_FW_TILE = 7
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

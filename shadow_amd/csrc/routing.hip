@@ -400,6 +400,7 @@ struct srg_ctx {
     bool gather_output = true;       // multi-rank: every rank ends with all n x n outputs
     int algorithm = SRG_ALGO_AUTO;   // dense FW / sparse batched Bellman-Ford
     bool sparse_locality = true;     // sparse: batch sources in BFS order
+    int fw_tile = 0;                 // 0 = auto, 64 or 128
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -1243,8 +1244,16 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
         if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
     }
     if (P.es.max_lat < 0xFFFFFFFFull) {
-        Plan pl = make_plan(G, rk, g.V, 128, P.nodes_h);
-        if (run_dense<uint32_t, 128>(c, g, pl, nodes, n, out_lat, out_loss, st, P, stats)) return;
+        // FW tile: 128 (more work per launch) on one GPU; the multi-rank schedule is bound by
+        // the per-pivot chain (close pivot -> panels), whose latency scales with T^3
+        const int tile = c.fw_tile ? c.fw_tile : 128;
+        if (tile == 64) {
+            Plan pl = make_plan(G, rk, g.V, 64, P.nodes_h);
+            if (run_dense<uint32_t, 64>(c, g, pl, nodes, n, out_lat, out_loss, st, P, stats)) return;
+        } else {
+            Plan pl = make_plan(G, rk, g.V, 128, P.nodes_h);
+            if (run_dense<uint32_t, 128>(c, g, pl, nodes, n, out_lat, out_loss, st, P, stats)) return;
+        }
     }
     Plan pl = make_plan(G, rk, g.V, 64, P.nodes_h);
     run_dense<uint64_t, 64>(c, g, pl, nodes, n, out_lat, out_loss, st, P, stats);
@@ -1422,6 +1431,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             }
             return SRG_OK;
         }
+        case SRG_OPT_FW_TILE:
+            if (value != 0 && value != 64 && value != 128) return SRG_ERR_ARG;
+            ctx->fw_tile = (int)value;
+            return SRG_OK;
         case SRG_OPT_SPARSE_LOCALITY:
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
