@@ -1154,7 +1154,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * 2));
-    const size_t lds = ((size_t)(V + 63) / 64) * 4 * 8 + 64 * 65 * 8;
+    const size_t lds = ((size_t)(V + 63) / 64) * 4 * 8 + sp_scratch_bytes();
     if (nbatch) {
         if (lds > 160 * 1024) fail(SRG_ERR_INTERNAL, "sparse path: flag bitmaps exceed LDS (V too large)");
         unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);

@@ -33,6 +33,12 @@ namespace srg {
 constexpr unsigned long long LBL_INF = ~0ull;
 constexpr int SP_WAVES = 16;           // waves per workgroup (1024 threads)
 constexpr int SP_THREADS = SP_WAVES * 64;
+constexpr int SP_CAP = 128;            // active-arc list entries per wave
+constexpr int SP_G = 8;                // label rows in flight per wave
+constexpr size_t sp_scratch_bytes() {
+    return (size_t)SP_WAVES * (128 + 4 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 4 * SP_CAP) * 4
+                                                                   : (size_t)64 * 65 * 8;
+}
 
 __device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, uint32_t w, float b) {
     const uint32_t lat = (uint32_t)(lu >> 32);
@@ -125,7 +131,7 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
 // pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
 // sweep (the out-neighbours of changed vertices, pushed when a vertex changes).  A sweep
 // only visits marked vertices, 64 per wave step (one bitmap word pair).
-__global__ void __launch_bounds__(SP_THREADS) k_sparse_bf(SparseArgs a) {
+__global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
     const uint32_t nw = (V + 63) / 64;  // 64-vertex windows
@@ -133,9 +139,18 @@ __global__ void __launch_bounds__(SP_THREADS) k_sparse_bf(SparseArgs a) {
     unsigned long long* fcur = fprev + nw;
     unsigned long long* mark = fcur + nw;
     unsigned long long* mnext = mark + nw;
-    unsigned long long* tile = mnext + nw;  // [64][65] output transpose
     __shared__ uint32_t s_batch, s_changed;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (4 x SP_CAP);
+    // the output transpose tile [64][65] u64 reuses the same region after convergence
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(mnext + nw);
+    uint32_t* w_st = scratch + wave * (128 + 4 * SP_CAP);
+    uint32_t* w_lo = w_st + 64;
+    uint32_t* w_u = w_lo + 64;
+    uint32_t* w_w = w_u + SP_CAP;
+    uint32_t* w_b = w_w + SP_CAP;
+    uint32_t* w_vi = w_b + SP_CAP;
+    unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
     unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
     uint32_t max_sweeps = 0;
     unsigned long long evals = 0;
@@ -184,77 +199,157 @@ __global__ void __launch_bounds__(SP_THREADS) k_sparse_bf(SparseArgs a) {
             __syncthreads();
             uint32_t chg = 0;
             for (uint32_t w = wave; w < nw; w += SP_WAVES) {
-                unsigned long long mk = mark[w];
+                const unsigned long long mk = mark[w];
                 if (!mk) continue;
+                // (1) offsets of the window's 64 vertices: one load for all of them
                 const uint32_t vl = w * 64 + lane;
-                const uint32_t off_lo = vl < V ? a.in_off[vl] : 0u;
-                const uint32_t off_hi = vl < V ? a.in_off[vl + 1] : 0u;
-                while (mk) {
-                    const int i = __builtin_ctzll(mk);
-                    mk &= mk - 1;
-                    const uint32_t v = w * 64 + (uint32_t)i;
-                    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)off_lo, i);
-                    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)off_hi, i);
+                const bool marked = (mk >> lane) & 1ull;
+                const uint32_t lo = vl < V ? a.in_off[vl] : 0u;
+                const uint32_t hi = vl < V ? a.in_off[vl + 1] : 0u;
+                // flattened slots per marked vertex: slot 0 = its own row (the old label), then
+                // one slot per in-arc
+                const uint32_t deg = marked ? hi - lo + 1 : 0u;
+                uint32_t incl = deg;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t t = __shfl_up(incl, o, 64);
+                    if ((int)lane >= o) incl += t;
+                }
+                const uint32_t total = (uint32_t)__shfl(incl, 63, 64);
+                w_st[lane] = incl - deg;
+                w_lo[lane] = lo;
+                __builtin_amdgcn_wave_barrier();
+                // (2) flattened scan of the marked vertices' in-arcs -> LDS list of the active
+                //     ones (source vertex changed last sweep), grouped by target vertex, each
+                //     group led by the vertex's own row (w_vi high bit set)
+                uint32_t n = 0;
+                unsigned long long changed = 0;  // window vertices whose label dropped
+                auto process = [&](uint32_t cnt) {
+                    // (3) consume the list in groups of SP_G rows, all loads of a group in flight
+                    int cur = -1;
                     unsigned long long best = 0, old = 0;
-                    bool have = false;
-                    for (uint32_t base = a0; base < a1; base += 64) {
-                        const uint32_t k = base + lane;
-                        uint32_t u = 0;
-                        bool act = false;
-                        if (k < a1) {
+                    for (uint32_t j0 = 0; j0 < cnt; j0 += SP_G) {
+                        unsigned long long row[SP_G];
+#pragma unroll
+                        for (int q = 0; q < SP_G; ++q)
+                            if (j0 + q < cnt) row[q] = ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]);
+#pragma unroll
+                        for (int q = 0; q < SP_G; ++q) {
+                            const uint32_t e = j0 + q;
+                            if (e >= cnt) break;
+                            const uint32_t tag = w_vi[e];
+                            if (tag & 0x80000000u) {  // a new vertex: its current label
+                                if (cur >= 0 && __ballot(best < old)) {
+                                    if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
+                                    changed |= 1ull << cur;
+                                }
+                                cur = (int)(tag & 63u);
+                                old = best = row[q];
+                            } else {
+                                const unsigned long long c =
+                                    row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(w_b[e]));
+                                best = c < best ? c : best;
+                                ++evals;
+                            }
+                        }
+                    }
+                    if (cur >= 0 && __ballot(best < old)) {
+                        if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
+                        changed |= 1ull << cur;
+                    }
+                };
+                for (uint32_t f0 = 0; f0 < total; f0 += 64) {
+                    const uint32_t f = f0 + lane;
+                    bool act = false;
+                    uint32_t u = 0, k = 0, vi = 0;
+                    if (f < total) {
+                        uint32_t i = 0;
+#pragma unroll
+                        for (uint32_t step = 32; step; step >>= 1)
+                            if (i + step < 64 && w_st[i + step] <= f) i += step;
+                        const uint32_t slot = f - w_st[i];
+                        if (slot == 0) {
+                            u = w * 64 + i;
+                            vi = 0x80000000u | i;
+                            act = true;
+                        } else {
+                            k = w_lo[i] + slot - 1;
                             u = a.in_src[k];
+                            vi = i;
                             act = (fprev[u >> 6] >> (u & 63)) & 1ull;
                         }
-                        unsigned long long m = __ballot(act);
-                        if (!m) continue;
-                        if (!have) {
-                            old = best = ld_label(&L[(size_t)v * 64 + lane]);
-                            have = true;
-                        }
-                        const uint32_t w_l = act ? a.in_w[k] : 0u;
-                        const float b_l = act ? a.in_b[k] : 0.0f;
-                        while (m) {
-                            // up to 4 active arcs per step: issue their row loads together
-                            int j[4];
-                            int cnt = 0;
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                j[q] = m ? __builtin_ctzll(m) : -1;
-                                if (m) {
-                                    m &= m - 1;
-                                    ++cnt;
-                                }
-                            }
-                            unsigned long long row[4];
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                if (j[q] >= 0) {
-                                    const uint32_t uu = (uint32_t)__builtin_amdgcn_readlane((int)u, j[q]);
-                                    row[q] = ld_label(&L[(size_t)uu * 64 + lane]);
-                                }
-                            }
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                if (j[q] >= 0) {
-                                    const uint32_t ww = (uint32_t)__builtin_amdgcn_readlane((int)w_l, j[q]);
-                                    const float bb =
-                                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b_l), j[q]));
-                                    const unsigned long long c = row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], ww, bb);
-                                    best = c < best ? c : best;
-                                }
-                            }
-                            evals += (unsigned long long)cnt;
-                        }
                     }
-                    if (!have) continue;
-                    const bool lower = best < old;
-                    if (__ballot(lower)) {
-                        if (lower) L[(size_t)v * 64 + lane] = best;
-                        if (lane == 0) atomicOr(&fcur[v >> 6], 1ull << (v & 63));
-                        push_out(v);
-                        chg = 1;
+                    const unsigned long long m = __ballot(act);
+                    if (act) {
+                        const uint32_t pos = n + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                                     (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        w_u[pos] = u;
+                        if (!(vi & 0x80000000u)) {
+                            w_w[pos] = a.in_w[k];
+                            w_b[pos] = __float_as_uint(a.in_b[k]);
+                        }
+                        w_vi[pos] = vi;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    n += (uint32_t)__popcll(m);
+                    if (n > SP_CAP - 64) {
+                        process(n);
+                        n = 0;
+                        // a vertex whose arcs continue past this chunk restarts its group with
+                        // its (possibly just lowered) label: our stores must land first
+                        const uint32_t fn = f0 + 64;
+                        if (fn < total) {
+                            uint32_t i = 0;
+                            for (uint32_t step = 32; step; step >>= 1)
+                                if (i + step < 64 && w_st[i + step] <= fn) i += step;
+                            if (fn != w_st[i]) {
+                                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                if (lane == 0) {
+                                    w_u[0] = w * 64 + i;
+                                    w_vi[0] = 0x80000000u | i;
+                                }
+                                __builtin_amdgcn_wave_barrier();
+                                n = 1;
+                            }
+                        }
                     }
                 }
+                if (n) process(n);
+                // (4) mark the out-neighbours of the changed vertices for the next sweep
+                if (changed) {
+                    if (lane == 0) atomicOr(&fcur[w], changed);
+                    chg = 1;
+                    const bool ch = (changed >> lane) & 1ull;
+                    uint32_t olo = lo, ohi = hi;
+                    if (a.out_off != a.in_off) {
+                        olo = ch ? a.out_off[vl] : 0u;
+                        ohi = ch ? a.out_off[vl + 1] : 0u;
+                    }
+                    const uint32_t odeg = ch ? ohi - olo : 0u;
+                    uint32_t oin = odeg;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t t = __shfl_up(oin, o, 64);
+                        if ((int)lane >= o) oin += t;
+                    }
+                    const uint32_t ototal = (uint32_t)__shfl(oin, 63, 64);
+                    __builtin_amdgcn_wave_barrier();
+                    w_st[lane] = oin - odeg;
+                    w_lo[lane] = olo;
+                    __builtin_amdgcn_wave_barrier();
+                    for (uint32_t f0 = 0; f0 < ototal; f0 += 64) {
+                        const uint32_t f = f0 + lane;
+                        if (f < ototal) {
+                            uint32_t i = 0;
+#pragma unroll
+                            for (uint32_t step = 32; step; step >>= 1)
+                                if (w_st[i + step < 64 ? i + step : 63] <= f && i + step < 64) i += step;
+                            const uint32_t t = a.out_dst[w_lo[i] + (f - w_st[i])];
+                            atomicOr(&mnext[t >> 6], 1ull << (t & 63));
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
             }
             if (chg && lane == 0) s_changed = 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // label stores reached L2
