@@ -27,9 +27,10 @@ METRIC = "APSP wall time + source-SSSPs/sec, 10k-vertex GML graph, 1/2/4/8 MI355
 # VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md chip table: wave64
 # issues over 2 cycles on a SIMD-32) = 78.6 T int32 lane-ops/s.
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
-# minimal VALU ops per relaxation on gfx950: u32 = v_add_u32 clamp + 1/2 v_min3_u32;
-# u64 = v_lshl_add_u64 + v_cmp_lt_u64 + 2 v_cndmask
-OPS_PER_RELAX = {0: 1.5, 1: 4.0}
+# algorithmic int32 ops per min-plus relaxation c = min(c, a + b): one add + one min (u32 keys);
+# u64 keys: 64-bit add (2) + 64-bit compare (1) + 2 selects.  Issued on gfx950 as
+# v_lshl_add_u64 (two packed u32 adds) + v_min3_u32 per two relaxations (kernels.hip.h fw_tile_pk).
+OPS_PER_RELAX = {0: 2.0, 1: 5.0}
 
 
 def log(*a):
@@ -82,6 +83,7 @@ def main():
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
+    ap.add_argument("--fw-packed", type=int, default=1, help="u32 FW tiles: 1 = packed-pair adds, 0 = add + min3")
     ap.add_argument("--simulate-rank", type=str, default=None,
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
                          "(outputs invalid; prints a diagnostic line, never the bench result)")
@@ -130,6 +132,7 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
     if args.fw_tile:
         router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
+    router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
     if args.simulate_rank:
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)
@@ -185,13 +188,13 @@ def main():
     elif agg.get("prof_launches"):
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         relax = agg["prof_relaxations"] / agg["prof_launches"]
-        achieved = relax * OPS_PER_RELAX.get(kind, 1.5) / (avg_ms * 1e-3) / 1e12
+        achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
         traffic, tsrc = load_traffic("fw_product")
-        roofline = {"bound": "valu", "kernel": "fw_product<u32,128,32> (FW phase 3, non-lookahead tiles)", "achieved": round(achieved, 3),
+        roofline = {"bound": "valu", "kernel": ("fw_product<u32,128,32,packed> (FW phase 3, non-lookahead tiles)" if args.fw_packed else "fw_product<u32,128,32> (FW phase 3, non-lookahead tiles)") if kind == 0 else "fw_product<u64,64,32> (FW phase 3)", "achieved": round(achieved, 3),
                     "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
-                    "ops_per_relaxation": OPS_PER_RELAX.get(kind, 1.5),
+                    "ops_per_relaxation": OPS_PER_RELAX.get(kind, 2.0), "relax_per_s": round(relax / (avg_ms * 1e-3), 1),
                     "traffic_source": tsrc}
 
     cpu = None

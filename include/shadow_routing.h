@@ -120,6 +120,8 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SIMULATE_RANK 6   /* TIMING AID ONLY: value = nranks*1000 + rank runs this rank's share
                                      with every collective elided -- outputs are NOT valid; 0 detaches */
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
+#define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles: 1 (default) = two relaxations per 64-bit add of
+                                     packed key pairs + v_min3; 0 = one add per relaxation */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).
@@ -184,6 +186,48 @@ int srg_local_group_create(int nranks, srg_local_group** out);
 void srg_local_group_release(srg_local_group* g);
 int srg_comm_init_local(srg_ctx* ctx, srg_local_group* g, int rank, char* errbuf, size_t errlen);
 int srg_comm_size(srg_ctx* ctx, int* nranks, int* rank);
+
+/* ---- stretch: one round's cross-host packet-event batch ---------------
+ * Replaces, for a whole batch at once, the per-packet tail of Worker::send_packet
+ * (src/main/core/worker.rs:391-424: latency lookup in RoutingInfo, deliver time raised to the
+ * round end, lowest used latency for the dynamic runahead runahead.rs:61-116, next event time)
+ * and the per-destination EventQueue ordering (worker.rs:644-654, event_queue.rs:38-49,
+ * Event::partial_cmp event.rs:84-155: time, then src_host_id, then src_host_event_id), plus the
+ * round's minimum next-event time (manager.rs:459-464).  The latency table is the dense
+ * num_nodes x num_nodes output of srg_compute_shortest_paths (rows = sending node position).
+ * Outputs: deliver_ns[i] per event; order = event indices grouped by destination host
+ * (increasing HostId), each host's events in its queue's pop order; host_offsets[h] ..
+ * host_offsets[h+1] = host h's slice.  The packet-drop draw (worker.rs:374-389) consumes each
+ * host's RNG stream in program order and is not part of the batch.                          */
+#define SRG_ERR_EVENT_ORDER 11  /* two events with no relative order: PanickingOrd unwrap panic
+                                   (event.rs:141-147, event_queue.rs:87-90) */
+typedef struct srg_event_batch {
+    uint64_t num_events;
+    const uint32_t* src_node;      /* [n] row of the latency table (sender's node position)   */
+    const uint32_t* dst_node;      /* [n] column of the latency table                          */
+    const uint32_t* src_host;      /* [n] HostId of the sender                                 */
+    const uint32_t* dst_host;      /* [n] HostId of the receiver, < num_hosts                  */
+    const uint64_t* send_time_ns;  /* [n] Worker::current_time at the send (EmulatedTime ns)   */
+    const uint64_t* src_event_id;  /* [n] src_host.get_new_event_id()                          */
+    uint32_t num_hosts;
+    uint32_t reserved;
+    uint64_t round_end_ns;         /* Worker::round_end_time                                   */
+} srg_event_batch;
+
+typedef struct srg_event_result {
+    uint64_t min_next_event_ns;    /* min deliver time (UINT64_MAX when empty)                 */
+    uint64_t min_used_latency_ns;  /* min latency used (UINT64_MAX when empty)                 */
+    uint32_t key_bits;             /* composite sort-key width actually used                   */
+    uint32_t radix_passes;         /* 8-bit LSD passes run                                     */
+    double ms_total;
+} srg_event_result;
+
+/* Device pointers throughout (batch arrays, table, outputs); `hip_stream` as above.          */
+int srg_order_packet_events_device(srg_ctx* ctx, const srg_event_batch* batch_dev,
+                                   const uint64_t* latency_table_dev, uint32_t table_n,
+                                   uint64_t* out_deliver_ns_dev, uint32_t* out_order_dev,
+                                   uint64_t* out_host_offsets_dev, void* hip_stream,
+                                   srg_event_result* result, char* errbuf, size_t errlen);
 
 /* Library build/version string. */
 const char* srg_version(void);

@@ -54,6 +54,10 @@ def lib():
             ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, _u32p, _u32p, _u64p, _f32p, _u32p,
             ctypes.c_uint32, _u32p, ctypes.c_uint32, ctypes.c_int, _u64p]
         L.oracle_hw_threads.restype = ctypes.c_int
+        L.oracle_order_packet_events.restype = ctypes.c_int
+        L.oracle_order_packet_events.argtypes = [
+            ctypes.c_uint64, _u32p, _u32p, _u32p, _u32p, _u64p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.c_uint64, _u64p, _u32p, _u64p, _u64p, _u64p]
         _lib = L
     return _lib
 
@@ -136,3 +140,27 @@ def time_sources(graph, nodes, sample, nthreads=0):
 
 def hw_threads():
     return lib().oracle_hw_threads()
+
+
+def order_packet_events(batch, table, num_hosts, round_end):
+    """Stretch C5 restatement (worker.rs:391-424, event.rs:84-155, manager.rs:459-464).
+    batch: dict of numpy arrays src_node, dst_node, src_host, dst_host (u32), send_time_ns,
+    src_event_id (u64); table: u64 [tn x tn] routing latencies.  Returns (deliver, order,
+    host_off, min_next, min_lat) or raises OracleError (3 = unordered events, the panic)."""
+    a = {k: np.ascontiguousarray(batch[k], dtype=np.uint32) for k in ("src_node", "dst_node", "src_host", "dst_host")}
+    send = np.ascontiguousarray(batch["send_time_ns"], dtype=np.uint64)
+    eid = np.ascontiguousarray(batch["src_event_id"], dtype=np.uint64)
+    table = np.ascontiguousarray(table, dtype=np.uint64)
+    n = len(send)
+    deliver = np.zeros(n, dtype=np.uint64)
+    order = np.zeros(n, dtype=np.uint32)
+    host_off = np.zeros(num_hosts + 1, dtype=np.uint64)
+    mn, ml = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().oracle_order_packet_events(
+        n, _p(a["src_node"], _u32p), _p(a["dst_node"], _u32p), _p(a["src_host"], _u32p), _p(a["dst_host"], _u32p),
+        _p(send, _u64p), _p(eid, _u64p), _p(table, _u64p), table.shape[0], num_hosts, round_end,
+        _p(deliver, _u64p), _p(order, _u32p), _p(host_off, _u64p), ctypes.byref(mn), ctypes.byref(ml))
+    if rc:
+        raise OracleError(rc, {1: "index out of range", 2: "time overflow",
+                               3: "events with no relative order (PanickingOrd panic)"}[rc])
+    return deliver, order, host_off, mn.value, ml.value

@@ -428,4 +428,58 @@ double oracle_time_sources(uint32_t V, int directed, uint64_t E, const uint32_t*
 
 int oracle_hw_threads(void) { return hw_threads(0); }
 
+// ---- stretch C5: one round's cross-host packet events ----------------------
+// Restates, per event i sent by src_host to dst_host at send_ns:
+//   Worker::send_packet (src/main/core/worker.rs:391-424):
+//     delay = RoutingInfo latency(src, dst)   -> table[src_node * tn + dst_node]
+//     update_lowest_used_latency(delay)       (runahead.rs:61-116: min over used latencies)
+//     deliver = current_time + delay (EmulatedTime + SimulationTime; overflow panics),
+//               raised to round_end if earlier (worker.rs:411-414)
+//     update_next_event_time(deliver)         (manager.rs:430-435, min at :459-464)
+//     push_packet_to_host(dst_host, deliver)  (worker.rs:644-654: one EventQueue per host)
+//   EventQueue pop order (event_queue.rs:38-49, BinaryHeap<Reverse<PanickingOrd<Event>>>):
+//     Event::partial_cmp (event.rs:84-99): time, then EventData (Packet < Local, event.rs:103-110),
+//     then PacketEventData (event.rs:131-155): src_host_id, then src_host_event_id; two events
+//     equal in all of these with different packets -> None -> PanickingOrd unwrap panic.
+// Output: order = per destination host (increasing HostId), that host's pop order;
+// host_off[h] .. host_off[h+1] = host h's events.  Error codes: 1 = bad index, 2 = time
+// overflow, 3 = two events with no relative order (the reference's panic).
+int oracle_order_packet_events(uint64_t n, const uint32_t* src_node, const uint32_t* dst_node,
+                               const uint32_t* src_host, const uint32_t* dst_host, const uint64_t* send_ns,
+                               const uint64_t* event_id, const uint64_t* table, uint32_t tn, uint32_t num_hosts,
+                               uint64_t round_end, uint64_t* deliver, uint32_t* order, uint64_t* host_off,
+                               uint64_t* min_next, uint64_t* min_lat) {
+    *min_next = UINT64_MAX;
+    *min_lat = UINT64_MAX;
+    std::vector<std::vector<uint32_t>> queues(num_hosts);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (src_node[i] >= tn || dst_node[i] >= tn || dst_host[i] >= num_hosts) return 1;
+        const uint64_t delay = table[(size_t)src_node[i] * tn + dst_node[i]];
+        if (send_ns[i] > UINT64_MAX - delay) return 2;
+        uint64_t t = send_ns[i] + delay;
+        if (t < round_end) t = round_end;
+        deliver[i] = t;
+        *min_lat = std::min(*min_lat, delay);
+        *min_next = std::min(*min_next, t);
+        queues[dst_host[i]].push_back((uint32_t)i);
+    }
+    auto less = [&](uint32_t a, uint32_t b) {
+        if (deliver[a] != deliver[b]) return deliver[a] < deliver[b];
+        if (src_host[a] != src_host[b]) return src_host[a] < src_host[b];
+        return event_id[a] < event_id[b];
+    };
+    uint64_t pos = 0;
+    for (uint32_t h = 0; h < num_hosts; ++h) {
+        host_off[h] = pos;
+        auto& q = queues[h];
+        std::sort(q.begin(), q.end(), less);
+        for (size_t k = 0; k < q.size(); ++k) {
+            if (k && !less(q[k - 1], q[k])) return 3;
+            order[pos++] = q[k];
+        }
+    }
+    host_off[num_hosts] = pos;
+    return 0;
+}
+
 }  // extern "C"

@@ -21,6 +21,7 @@ SRG_ERR_OOM = 7
 SRG_ERR_PARSE = 8
 SRG_ERR_RCCL = 9
 SRG_ERR_INTERNAL = 10
+SRG_ERR_EVENT_ORDER = 11
 
 SRG_PATH_DENSE_U32 = 0
 SRG_PATH_DENSE_U64 = 1
@@ -34,6 +35,7 @@ SRG_OPT_ALGORITHM = 4
 SRG_OPT_SPARSE_LOCALITY = 5
 SRG_OPT_SIMULATE_RANK = 6
 SRG_OPT_FW_TILE = 7
+SRG_OPT_FW_PACKED = 8
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2
@@ -59,6 +61,34 @@ class EdgeList(ctypes.Structure):
         ("packet_loss", ctypes.c_void_p),
         ("node_ids", ctypes.c_void_p),
     ]
+
+
+class EventBatch(ctypes.Structure):
+    _fields_ = [
+        ("num_events", ctypes.c_uint64),
+        ("src_node", ctypes.c_void_p),
+        ("dst_node", ctypes.c_void_p),
+        ("src_host", ctypes.c_void_p),
+        ("dst_host", ctypes.c_void_p),
+        ("send_time_ns", ctypes.c_void_p),
+        ("src_event_id", ctypes.c_void_p),
+        ("num_hosts", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("round_end_ns", ctypes.c_uint64),
+    ]
+
+
+class EventResult(ctypes.Structure):
+    _fields_ = [
+        ("min_next_event_ns", ctypes.c_uint64),
+        ("min_used_latency_ns", ctypes.c_uint64),
+        ("key_bits", ctypes.c_uint32),
+        ("radix_passes", ctypes.c_uint32),
+        ("ms_total", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class Stats(ctypes.Structure):
@@ -98,6 +128,7 @@ EXPORTS = [
     "srg_graph_num_vertices", "srg_graph_num_edges", "srg_graph_directed", "srg_graph_node_index",
     "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version", "srg_comm_unique_id", "srg_comm_init",
     "srg_local_group_create", "srg_local_group_release", "srg_comm_init_local", "srg_comm_size",
+    "srg_order_packet_events_device",
 ]
 
 _lib = None
@@ -168,6 +199,10 @@ def lib():
     L.srg_local_group_release.argtypes = [c.c_void_p]
     L.srg_comm_init_local.restype = c.c_int
     L.srg_comm_init_local.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_char_p, c.c_size_t]
+    L.srg_order_packet_events_device.restype = c.c_int
+    L.srg_order_packet_events_device.argtypes = [
+        c.c_void_p, c.POINTER(EventBatch), c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p,
+        c.POINTER(EventResult), c.c_char_p, c.c_size_t]
     L.srg_comm_size.restype = c.c_int
     L.srg_comm_size.argtypes = [c.c_void_p, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     _lib = L

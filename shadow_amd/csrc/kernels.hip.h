@@ -9,7 +9,7 @@
 //   D   [Vp x Vp] K     W with diagonal 0, then closed by blocked Floyd-Warshall.
 //   PRED[n  x Vp] u32   per used source row: the unique tight predecessor of t, or MULTI
 //   L   [n  x Vp] f32   left-fold loss per used source row (two buffers, Jacobi rounds)
-// K = uint32_t (saturating add: exact for every distance < 2^32-1, certified on the host)
+// K = uint32_t (INF = 2^31-1: exact for every distance < INF, certified on the host)
 //   or uint64_t (INF = 2^62, exact for every distance < 2^62).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -25,10 +25,16 @@ struct KeyOps;
 
 template <>
 struct KeyOps<uint32_t> {
-    static constexpr uint32_t INF = 0xFFFFFFFFu;
+    // INF = 2^31 - 1: every stored key is <= INF, so the sum of two keys never exceeds 2^32 - 2.
+    // That lets the FW product add two packed keys per 64-bit add with no carry between the
+    // halves (fw_tile_pk); the saturating add below then never saturates, and a used-row key
+    // equal to INF (unreachable, or a path >= 2^31 - 1 ns) sends the build to the u64 keys.
+    static constexpr uint32_t INF = 0x7FFFFFFFu;
     __device__ __forceinline__ static uint32_t add(uint32_t a, uint32_t b) {
         return __builtin_elementwise_add_sat(a, b);  // v_add_u32 ... clamp
     }
+    // keys <= INF: the sum never wraps, so the FW tiles use the plain (VOP2, full-rate) add
+    __device__ __forceinline__ static uint32_t add_nw(uint32_t a, uint32_t b) { return a + b; }
     __device__ __forceinline__ static uint32_t min2(uint32_t a, uint32_t b) { return a < b ? a : b; }
     __device__ __forceinline__ static uint32_t min3(uint32_t a, uint32_t b, uint32_t c) {
         // one v_min3_u32 (hipcc otherwise re-associates a min chain into a v_min tree:
@@ -43,6 +49,7 @@ template <>
 struct KeyOps<uint64_t> {
     static constexpr uint64_t INF = 1ull << 62;
     __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b) { return a + b; }
+    __device__ __forceinline__ static uint64_t add_nw(uint64_t a, uint64_t b) { return a + b; }
     __device__ __forceinline__ static uint64_t min2(uint64_t a, uint64_t b) { return a < b ? a : b; }
     __device__ __forceinline__ static uint64_t min3(uint64_t a, uint64_t b, uint64_t c) {
         return min2(min2(a, b), c);
@@ -172,23 +179,23 @@ __global__ void __launch_bounds__(512) fw_phase1(K* __restrict__ D, size_t ld, i
 #pragma unroll
             for (int x = i + 1; x < R; ++x)
 #pragma unroll
-                for (int b = 0; b < MC; ++b) Rv[x][b] = KeyOps<K>::min2(Rv[x][b], KeyOps<K>::add(Pv[x][i], Rv[i][b]));
+                for (int b = 0; b < MC; ++b) Rv[x][b] = KeyOps<K>::min2(Rv[x][b], KeyOps<K>::add_nw(Pv[x][i], Rv[i][b]));
 #pragma unroll
             for (int y = i + 1; y < R; ++y)
 #pragma unroll
-                for (int a = 0; a < MR; ++a) Cv[a][y] = KeyOps<K>::min2(Cv[a][y], KeyOps<K>::add(Cv[a][i], Pv[i][y]));
+                for (int a = 0; a < MR; ++a) Cv[a][y] = KeyOps<K>::min2(Cv[a][y], KeyOps<K>::add_nw(Cv[a][i], Pv[i][y]));
 #pragma unroll
             for (int x = i + 1; x < R; ++x)
 #pragma unroll
-                for (int y = i + 1; y < R; ++y) Pv[x][y] = KeyOps<K>::min2(Pv[x][y], KeyOps<K>::add(Pv[x][i], Pv[i][y]));
+                for (int y = i + 1; y < R; ++y) Pv[x][y] = KeyOps<K>::min2(Pv[x][y], KeyOps<K>::add_nw(Pv[x][i], Pv[i][y]));
         }
         // fold the R steps into the own elements
 #pragma unroll
         for (int a = 0; a < MR; ++a)
 #pragma unroll
             for (int b = 0; b < MC; ++b) {
-                K v = KeyOps<K>::min3(c[a][b], KeyOps<K>::add(Cv[a][0], Rv[0][b]), KeyOps<K>::add(Cv[a][1], Rv[1][b]));
-                c[a][b] = KeyOps<K>::min3(v, KeyOps<K>::add(Cv[a][2], Rv[2][b]), KeyOps<K>::add(Cv[a][3], Rv[3][b]));
+                K v = KeyOps<K>::min3(c[a][b], KeyOps<K>::add_nw(Cv[a][0], Rv[0][b]), KeyOps<K>::add_nw(Cv[a][1], Rv[1][b]));
+                c[a][b] = KeyOps<K>::min3(v, KeyOps<K>::add_nw(Cv[a][2], Rv[2][b]), KeyOps<K>::add_nw(Cv[a][3], Rv[3][b]));
             }
         if (g + 1 < T / R) publish(q ^ 1, k0 + R);
         __syncthreads();
@@ -311,31 +318,210 @@ __device__ __forceinline__ int tile_kept(int base, int idx, int x0, int x1) {
 // gridDim.z > 1 splits the pivot block's k range across workgroups (split-K): each split
 // reduces its share and merges with atomicMin, which is exact because min is associative and
 // commutative (used for the short launches on the multi-GPU critical path).
-template <class K, int T, int KC>
+template <class K, int T, int KC, bool PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J);
 
-template <class K, int T, int KC>
+// PK = true (u32 keys only): the pair-packed tile below (fw_tile_pk); false: add + min3.
+template <class K, int T, int KC, bool PK>
 __global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
-    fw_tile<K, T, KC>(D, ld, kb, tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1),
-                      tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1));
+    fw_tile<K, T, KC, PK>(D, ld, kb, tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1),
+                          tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1));
 }
 
 // Two tile sets in one launch (the pivot's row panel and column panel: they are independent
 // once the pivot tile is closed, and each is a single short wave of workgroups, so one launch
 // instead of two takes a tile latency off the FW critical path).  grid.x = na + nb tiles;
 // set s is nc_s columns wide, tiles flattened row-major.
-template <class K, int T, int KC>
+template <class K, int T, int KC, bool PK>
 __global__ void __launch_bounds__(256) fw_product_pair(K* __restrict__ D, size_t ld, int kb, TileSet a, int na,
                                                        int nca, TileSet b, int ncb) {
     int x = (int)blockIdx.x;
     const TileSet& t = x < na ? a : b;
     const int nc = x < na ? nca : ncb;
     if (x >= na) x -= na;
-    fw_tile<K, T, KC>(D, ld, kb, tile_kept(t.r0, x / nc, t.rx0, t.rx1), tile_kept(t.c0, x % nc, t.cx0, t.cx1));
+    fw_tile<K, T, KC, PK>(D, ld, kb, tile_kept(t.r0, x / nc, t.rx0, t.rx1), tile_kept(t.c0, x % nc, t.cx0, t.cx1));
 }
 
-template <class K, int T, int KC>
+// ---------------------------------------------------------------------------------------
+// u32 keys, pair-packed (PK = true, the dominant kernel).  Every u32 key is <= INF = 2^31-1,
+// so a sum of two keys is < 2^32 and one 64-bit add of two packed pairs
+//     (x_k | x_{k+1} << 32) + (y_k | y_{k+1} << 32)
+// yields both 32-bit sums exactly (no carry crosses the halves).  One v_lshl_add_u64 thus does
+// the adds of two relaxations and one v_min3_u32 folds both into the accumulator: one
+// full-rate and one half-rate VALU instruction per two relaxations, instead of two adds and a
+// min3 (profiles/r01_valu_rate_microbench.txt).
+// LDS image of a KC-deep chunk as k-pairs, rows of LDA = T + 2 pairs (16-B pad):
+//     Ap[kp][i] = A[i][k0+2kp] | A[i][k0+2kp+1] << 32
+//     Bp[kp][j] = B[k0+2kp][j] | B[k0+2kp+1][j] << 32
+// Thread (ty, tx) owns rows pk_rc(ty, e) and columns pk_rc(tx, e), e < M = T/16: two adjacent
+// rows/columns every 32, so one ds_read_b128 (two pairs) of 16 lanes covers 256 contiguous
+// bytes (conflict-free; the A reads are 4-address broadcasts).
+typedef unsigned long long u64p;
+
+__device__ __forceinline__ u64p add_pairs(u64p x, u64p y) {
+    u64p r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+__device__ __forceinline__ int pk_rc(int t, int e) { return 32 * (e >> 1) + 2 * t + (e & 1); }
+
+template <int T, int KC>
+struct PkStage {
+    static_assert(T % 32 == 0 && KC % 8 == 0, "pk tile");
+    static constexpr int LDA = T + 2;                    // pairs per LDS row
+    static constexpr int AV = T * KC / 4 / 256;          // A: 16-B vectors (4 k values) per thread
+    static constexpr int BT = (KC / 2) * (T / 4) / 256;  // B: pair-row tasks (two 16-B loads) per thread
+    static_assert(AV >= 1 && BT >= 1, "pk staging");
+    Vec16<uint32_t> a[AV], b0[BT], b1[BT];
+};
+
+template <int T, int KC>
+__device__ __forceinline__ void pk_load(PkStage<T, KC>& sg, const uint32_t* __restrict__ A,
+                                        const uint32_t* __restrict__ B, size_t ld, const uint32_t* arow, int k0) {
+    using S = PkStage<T, KC>;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < S::AV; ++q) {
+        const int v = tid + 256 * q, i = v / (KC / 4), kq = v % (KC / 4);
+        sg.a[q] = ld16(A + (size_t)arow[i] * ld + k0 + kq * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < S::BT; ++q) {
+        const int v = tid + 256 * q, p = v / (T / 4), jq = v % (T / 4);
+        const uint32_t* r0 = B + (size_t)(k0 + 2 * p) * ld + jq * 4;
+        sg.b0[q] = ld16(r0);
+        sg.b1[q] = ld16(r0 + ld);
+    }
+}
+
+template <int T, int KC>
+__device__ __forceinline__ void pk_store(const PkStage<T, KC>& sg, u64p* __restrict__ Ap, u64p* __restrict__ Bp) {
+    using S = PkStage<T, KC>;
+    constexpr int LDA = S::LDA;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < S::AV; ++q) {
+        const int v = tid + 256 * q, i = v / (KC / 4), kq = v % (KC / 4);
+        const uint32_t* x = sg.a[q].v;
+        Ap[(2 * kq) * LDA + i] = (u64p)x[0] | ((u64p)x[1] << 32);
+        Ap[(2 * kq + 1) * LDA + i] = (u64p)x[2] | ((u64p)x[3] << 32);
+    }
+#pragma unroll
+    for (int q = 0; q < S::BT; ++q) {
+        const int v = tid + 256 * q, p = v / (T / 4), jq = v % (T / 4);
+        const uint32_t* x = sg.b0[q].v;
+        const uint32_t* y = sg.b1[q].v;
+        VecN<u64p, 2> w0, w1;
+        w0.v[0] = (u64p)x[0] | ((u64p)y[0] << 32);
+        w0.v[1] = (u64p)x[1] | ((u64p)y[1] << 32);
+        w1.v[0] = (u64p)x[2] | ((u64p)y[2] << 32);
+        w1.v[1] = (u64p)x[3] | ((u64p)y[3] << 32);
+        stv<u64p, 2>(Bp + p * LDA + jq * 4, w0);
+        stv<u64p, 2>(Bp + p * LDA + jq * 4 + 2, w1);
+    }
+}
+
+template <int T, int KC>
+constexpr size_t pk_lds_bytes() {
+    return (size_t)2 * KC * (T + 2) * sizeof(u64p);  // double-buffered Ap + Bp
+}
+
+template <int T, int KC>
+__device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
+    using S = PkStage<T, KC>;
+    constexpr int M = T / 16;
+    constexpr int LDA = S::LDA;
+    constexpr int BUF = KC * LDA;  // pairs per LDS buffer: Ap (KC/2 rows) then Bp (KC/2 rows)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    u64p* lds = reinterpret_cast<u64p*>(smem_raw);
+    __shared__ uint32_t arow[T];
+    uint32_t* C = D + (size_t)I * T * ld + (size_t)J * T;
+    const uint32_t* A = D + (size_t)kb * T;                       // column block kb, rows via arow
+    const uint32_t* B = D + (size_t)kb * T * ld + (size_t)J * T;  // row block kb, cols J
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    if (tid < T) arow[tid] = I * T + tid;
+    __syncthreads();
+
+    constexpr int NCH = T / KC;
+    const int nsplit = (int)gridDim.z;
+    const int ch0 = (int)blockIdx.z * NCH / nsplit, ch1 = ((int)blockIdx.z + 1) * NCH / nsplit;
+    S sg;
+    pk_load<T, KC>(sg, A, B, ld, arow, ch0 * KC);
+    uint32_t c[M][M];
+    if (nsplit == 1) {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx);
+                c[a][2 * g] = v.v[0];
+                c[a][2 * g + 1] = v.v[1];
+            }
+    } else {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int b = 0; b < M; ++b) c[a][b] = KeyOps<uint32_t>::INF;
+    }
+    pk_store<T, KC>(sg, lds, lds + (KC / 2) * LDA);
+    __syncthreads();
+#pragma unroll 1
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const u64p* Ap = lds + ((ch - ch0) & 1) * BUF;
+        const u64p* Bp = Ap + (KC / 2) * LDA;
+        if (ch + 1 < ch1) pk_load<T, KC>(sg, A, B, ld, arow, (ch + 1) * KC);  // issue early
+#pragma unroll 4
+        for (int kp = 0; kp < KC / 2; ++kp) {
+            u64p ap[M], bp[M];
+#pragma unroll
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<u64p, 2> va = ldv<u64p, 2>(Ap + kp * LDA + 32 * g + 2 * ty);
+                VecN<u64p, 2> vb = ldv<u64p, 2>(Bp + kp * LDA + 32 * g + 2 * tx);
+                ap[2 * g] = va.v[0];
+                ap[2 * g + 1] = va.v[1];
+                bp[2 * g] = vb.v[0];
+                bp[2 * g + 1] = vb.v[1];
+            }
+#pragma unroll
+            for (int a = 0; a < M; ++a)
+#pragma unroll
+                for (int b = 0; b < M; ++b) {
+                    const u64p s = add_pairs(ap[a], bp[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                }
+        }
+        if (ch + 1 < ch1) {  // write late into the other buffer
+            u64p* An = lds + ((ch + 1 - ch0) & 1) * BUF;
+            pk_store<T, KC>(sg, An, An + (KC / 2) * LDA);
+        }
+        __syncthreads();
+    }
+    if (nsplit == 1) {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<uint32_t, 2> v;
+                v.v[0] = c[a][2 * g];
+                v.v[1] = c[a][2 * g + 1];
+                stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx, v);
+            }
+    } else {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int b = 0; b < M; ++b) atomicMin(C + (size_t)pk_rc(ty, a) * ld + pk_rc(tx, b), c[a][b]);
+    }
+}
+
+template <class K, int T, int KC, bool PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J) {
+    if constexpr (PK) {
+        static_assert(sizeof(K) == 4, "pair-packed tiles need u32 keys");
+        fw_tile_pk<T, KC>(reinterpret_cast<uint32_t*>(D), ld, kb, I, J);
+        return;
+    }
     using G = Geo<K, T>;
     constexpr int M = G::M;
     constexpr int VE = 16 / (int)sizeof(K);
@@ -400,8 +586,8 @@ __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, in
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b)
-                    c[a][b] = KeyOps<K>::min3(c[a][b], KeyOps<K>::add(a0[a], b0[b]),
-                                              KeyOps<K>::add(a1[a], b1[b]));
+                    c[a][b] = KeyOps<K>::min3(c[a][b], KeyOps<K>::add_nw(a0[a], b0[b]),
+                                              KeyOps<K>::add_nw(a1[a], b1[b]));
         }
         if (ch + 1 < ch1) {  // write late into the other buffer
             K* Ant = lds + ((ch + 1 - ch0) & 1) * BUF;

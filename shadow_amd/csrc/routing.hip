@@ -29,6 +29,7 @@
 #include "tight_sparse.hip.h"
 #include "comm.h"
 #include "sparse.hip.h"
+#include "events.hip.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -153,7 +154,7 @@ __global__ void k_fill(K* __restrict__ p, size_t count, K v) {
 
 template <class K>
 __device__ __forceinline__ K to_key(uint64_t l) {
-    if constexpr (sizeof(K) == 4) return l >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)l;
+    if constexpr (sizeof(K) == 4) return l >= KeyOps<K>::INF ? KeyOps<K>::INF : (uint32_t)l;
     else return (K)l;
 }
 
@@ -216,7 +217,7 @@ __global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __res
         const size_t i = bi * 64 + r, j = bj * 64 + tx;
         unsigned long long k = KW[i * ld + j];
         if (!directed) k = min(k, tb[tx][r]);
-        const uint32_t w = (uint32_t)(k >> 32);
+        const uint32_t w = min((uint32_t)(k >> 32), KeyOps<uint32_t>::INF);  // no edge / >= INF -> INF
         W[i * ld + j] = w;
         WL[i * ld + j] = (uint32_t)k;
         D[i * ld + j] = i == j ? 0u : w;
@@ -227,7 +228,7 @@ __global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __res
         for (uint32_t r = ty; r < 64; r += 4) {
             const size_t i = bj * 64 + r, j = bi * 64 + tx;
             const unsigned long long k = tb[r][tx];
-            const uint32_t w = (uint32_t)(k >> 32);
+            const uint32_t w = min((uint32_t)(k >> 32), KeyOps<uint32_t>::INF);
             W[i * ld + j] = w;
             WL[i * ld + j] = (uint32_t)k;
             D[i * ld + j] = w;
@@ -401,6 +402,7 @@ struct srg_ctx {
     int algorithm = SRG_ALGO_AUTO;   // dense FW / sparse batched Bellman-Ford
     bool sparse_locality = true;     // sparse: batch sources in BFS order
     int fw_tile = 0;                 // 0 = auto, 64 or 128
+    bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -416,12 +418,15 @@ struct srg_ctx {
         b_gblk, b_DST, b_scantmp, b_ess;
     // multi-rank: local sources, their output rows, exchange staging
     DevBuf b_lnodes, b_lpos, b_allpos, b_stage, b_red, b_outoff, b_outdst;
+    // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
+    DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
-                          &b_scantmp, &b_ess, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst})
+                          &b_scantmp, &b_ess, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst,
+                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
@@ -615,23 +620,23 @@ int split_for(int tiles, bool enable) {
     return sp;
 }
 
-template <class K, int T>
+template <class K, int T, bool PK>
 void fw_tiles(K* D, size_t ld, int kb, int ra, int rb, std::initializer_list<int> rx, int ca, int cb,
               std::initializer_list<int> cx, size_t lds, hipStream_t s, bool split = false) {
     const Rect r = make_rect(ra, rb, rx, ca, cb, cx);
     if (r.nr <= 0 || r.nc <= 0) return;
     const int sp = split_for<T>(r.nr * r.nc, split);
-    fw_product<K, T, KC><<<dim3(r.nc, r.nr, sp), 256, lds, s>>>(D, ld, kb, r.ts);
+    fw_product<K, T, KC, PK><<<dim3(r.nc, r.nr, sp), 256, lds, s>>>(D, ld, kb, r.ts);
 }
 
-template <class K, int T>
+template <class K, int T, bool PK>
 void fw_tiles_pair(K* D, size_t ld, int kb, const Rect& a, const Rect& b, size_t lds, hipStream_t s,
                    bool split = false) {
     const int na = std::max(0, a.nr) * std::max(0, a.nc), nb = std::max(0, b.nr) * std::max(0, b.nc);
     if (na + nb == 0) return;
     const int sp = split_for<T>(na + nb, split);
-    fw_product_pair<K, T, KC><<<dim3(na + nb, 1, sp), 256, lds, s>>>(D, ld, kb, a.ts, na, std::max(1, a.nc), b.ts,
-                                                                    std::max(1, b.nc));
+    fw_product_pair<K, T, KC, PK><<<dim3(na + nb, 1, sp), 256, lds, s>>>(D, ld, kb, a.ts, na, std::max(1, a.nc),
+                                                                        b.ts, std::max(1, b.nc));
 }
 
 // Blocked Floyd-Warshall over the rank's row blocks with a one-block lookahead:
@@ -639,12 +644,13 @@ void fw_tiles_pair(K* D, size_t ld, int kb, const Rect& a, const Rect& b, size_t
 //   panel on the auxiliary stream, and broadcasts the panel (T x Vp keys, in place) while
 //   every rank finishes the remaining tiles of kb; then each rank updates its own column
 //   panel of kb+1.  Single GPU: the same schedule with the broadcast elided.
-template <class K, int T>
+template <class K, int T, bool PK>
 void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax, int& prof_n) {
     const int nb = pl.nb;
-    const size_t lds = (size_t)4 * KC * (T + 16 / (int)sizeof(K)) * sizeof(K);  // double-buffered A^T + B
-    set_lds(fw_product<K, T, KC>, lds);
-    set_lds(fw_product_pair<K, T, KC>, lds);
+    // double-buffered LDS image: A^T + B (add + min3 tiles) or the k-pair image (packed tiles)
+    const size_t lds = PK ? pk_lds_bytes<T, KC>() : (size_t)4 * KC * (T + 16 / (int)sizeof(K)) * sizeof(K);
+    set_lds(fw_product<K, T, KC, PK>, lds);
+    set_lds(fw_product_pair<K, T, KC, PK>, lds);
     const bool multi = c.comm && c.comm->nranks > 1;
     const bool prof = c.profiling && nb > 2;
     if (prof) {
@@ -661,7 +667,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     // pivot 0
     if (pl.own(0)) {
         fw_phase1<K, T><<<1, 512, 0, st>>>(D, Vp, 0);
-        fw_tiles<K, T>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st, pl.G > 1);
+        fw_tiles<K, T, PK>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st, pl.G > 1);
     }
     if (multi) {
         HIP_CHECK(hipEventRecord(c.ev_c, st));
@@ -670,25 +676,25 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
         HIP_CHECK(hipEventRecord(c.ev_c, cs));
         HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
     }
-    fw_tiles<K, T>(D, Vp, 0, r0, r1, {0}, 0, 1, {}, lds, st);
+    fw_tiles<K, T, PK>(D, Vp, 0, r0, r1, {0}, 0, 1, {}, lds, st);
     for (int kb = 0; kb < nb; ++kb) {
         if (kb + 1 >= nb) {
-            fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb}, 0, nb, {kb}, lds, st);
+            fw_tiles<K, T, PK>(D, Vp, kb, r0, r1, {kb}, 0, nb, {kb}, lds, st);
             break;
         }
         const int k1 = kb + 1;
         // critical chain: row k1 (w.r.t. kb) -> close pivot k1 -> its row + column panels
         const bool sk = pl.G > 1;  // split-K the chain's short launches when the rest is short too
-        if (pl.own(k1)) fw_tiles<K, T>(D, Vp, kb, k1, k1 + 1, {}, 0, nb, {kb}, lds, st, sk);  // row k1
+        if (pl.own(k1)) fw_tiles<K, T, PK>(D, Vp, kb, k1, k1 + 1, {}, 0, nb, {kb}, lds, st, sk);  // row k1
         HIP_CHECK(hipEventRecord(c.ev_a, st));
-        fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb, k1}, k1, k1 + 1, {}, lds, st, sk);             // own col k1
+        fw_tiles<K, T, PK>(D, Vp, kb, r0, r1, {kb, k1}, k1, k1 + 1, {}, lds, st, sk);             // own col k1
         HIP_CHECK(hipEventRecord(c.ev_e, st));
         HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
         const Rect colp = make_rect(r0, r1, {k1}, k1, k1 + 1, {});  // own column panel of k1
         if (pl.own(k1)) {
             fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1);
             HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
-            fw_tiles_pair<K, T>(D, Vp, k1, make_rect(k1, k1 + 1, {}, 0, nb, {k1}), colp, lds, aux, sk);
+            fw_tiles_pair<K, T, PK>(D, Vp, k1, make_rect(k1, k1 + 1, {}, 0, nb, {k1}), colp, lds, aux, sk);
         }
         if (multi) {
             HIP_CHECK(hipEventRecord(c.ev_b, aux));
@@ -698,7 +704,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
             if (!pl.own(k1)) {  // the pivot tile arrives in the panel
                 HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
                 HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
-                fw_tiles_pair<K, T>(D, Vp, k1, Rect{TileSet{0, -1, -1, 0, -1, -1}, 0, 0}, colp, lds, aux, sk);
+                fw_tiles_pair<K, T, PK>(D, Vp, k1, Rect{TileSet{0, -1, -1, 0, -1, -1}, 0, 0}, colp, lds, aux, sk);
             }
         }
         HIP_CHECK(hipEventRecord(c.ev_d, aux));
@@ -706,7 +712,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
         const int nr = (r1 - r0) - (pl.own(kb) ? 1 : 0) - (pl.own(k1) ? 1 : 0);
         const bool timed = prof && nr > 0 && nb > 2;
         if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        fw_tiles<K, T>(D, Vp, kb, r0, r1, {kb, k1}, 0, nb, {kb, k1}, lds, st);
+        fw_tiles<K, T, PK>(D, Vp, kb, r0, r1, {kb, k1}, 0, nb, {kb, k1}, lds, st);
         if (timed) {
             HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
             prof_relax += (uint64_t)nr * (nb - 2) * T * T * T;
@@ -762,7 +768,12 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // ---- blocked Floyd-Warshall ----
     uint64_t prof_relax = 0;
     int prof_n = 0;
-    fw_blocked<K, T>(c, pl, D, Vp, st, prof_relax, prof_n);
+    if constexpr (sizeof(K) == 4) {
+        if (c.fw_packed) fw_blocked<K, T, true>(c, pl, D, Vp, st, prof_relax, prof_n);
+        else fw_blocked<K, T, false>(c, pl, D, Vp, st, prof_relax, prof_n);
+    } else {
+        fw_blocked<K, T, false>(c, pl, D, Vp, st, prof_relax, prof_n);
+    }
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
     if (prof_n && stats) {
@@ -1298,6 +1309,98 @@ void direct_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_
     }
 }
 
+// ---- stretch C5: packet-event batch (events.hip.h) ---------------------------------------
+inline uint32_t bit_width64(uint64_t v) { return v ? 64u - (uint32_t)__builtin_clzll(v) : 0u; }
+
+template <bool WIDE>
+void events_sort(srg_ctx& c, const EvIn& in, const uint64_t* deliver, const EvKeyFmt& f, uint32_t bits,
+                 uint32_t* out_order, uint64_t* host_off, hipStream_t st, uint32_t& passes) {
+    const uint64_t n = in.n;
+    unsigned long long* k0 = (unsigned long long*)c.b_ek0.get(n * 8);
+    unsigned long long* k1 = (unsigned long long*)c.b_ek1.get(n * 8);
+    unsigned long long* h0 = WIDE ? (unsigned long long*)c.b_eh0.get(n * 8) : nullptr;
+    unsigned long long* h1 = WIDE ? (unsigned long long*)c.b_eh1.get(n * 8) : nullptr;
+    uint32_t* i0 = (uint32_t*)c.b_ei0.get(n * 4);
+    uint32_t* i1 = (uint32_t*)c.b_ei1.get(n * 4);
+    k_ev_keys<WIDE><<<grid_for(n, 256 * 64), kThreads, 0, st>>>(in, deliver, f, k0, h0, i0);
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    const int nh = (int)(256 * (size_t)ntiles);
+    uint32_t* hist = (uint32_t*)c.b_ehist.get((size_t)nh * 4);
+    uint32_t* offs = (uint32_t*)c.b_eoffs.get((size_t)nh * 4);
+    size_t tb = 0;
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hist, offs, nh, st));
+    void* tmp = c.b_scantmp.get(tb);
+    passes = 0;
+    for (uint32_t p = 0; p < bits; p += 8) {
+        k_rs_hist<WIDE><<<ntiles, RS_THREADS, 0, st>>>(k0, h0, n, p, ntiles, hist);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, offs, nh, st));
+        k_rs_scatter<WIDE><<<ntiles, RS_THREADS, 0, st>>>(k0, h0, i0, k1, h1, i1, n, p, ntiles, offs);
+        std::swap(k0, k1);
+        std::swap(h0, h1);
+        std::swap(i0, i1);
+        ++passes;
+    }
+    HIP_CHECK(hipGetLastError());
+    uint32_t* flag = (uint32_t*)c.b_red.get(64);
+    HIP_CHECK(hipMemsetAsync(flag, 0, 4, st));
+    k_ev_finish<WIDE><<<grid_for(n, 256 * 64), kThreads, 0, st>>>(k0, h0, n, f.sh_dst, in.num_hosts, host_off, flag);
+    HIP_CHECK(hipMemcpyAsync(out_order, i0, n * 4, hipMemcpyDeviceToDevice, st));
+    uint32_t hflag = 0;
+    HIP_CHECK(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (hflag)
+        fail(SRG_ERR_EVENT_ORDER,
+             "called `Option::unwrap()` on a `None` value: two packet events with equal (time, src_host_id, "
+             "src_host_event_id) have no relative order");
+}
+
+void order_events_device(srg_ctx& c, const EvIn& in, uint64_t* deliver, uint32_t* out_order, uint64_t* host_off,
+                         hipStream_t st, srg_event_result* res) {
+    if (res) {
+        res->min_next_event_ns = UINT64_MAX;
+        res->min_used_latency_ns = UINT64_MAX;
+        res->key_bits = 0;
+        res->radix_passes = 0;
+    }
+    HIP_CHECK(hipMemsetAsync(host_off, 0, ((size_t)in.num_hosts + 1) * 8, st));
+    if (in.n == 0) {
+        HIP_CHECK(hipStreamSynchronize(st));
+        return;
+    }
+    if (in.n >= 0xFFFFFFFFull) fail(SRG_ERR_ARG, "event batch too large (>= 2^32 events)");
+    EvReduce* red = (EvReduce*)c.b_ered.get(sizeof(EvReduce));
+    EvReduce init{~0ull, 0ull, ~0ull, 0ull, ~0ull, 0u, 0u, 0u, 0u};
+    HIP_CHECK(hipMemcpyAsync(red, &init, sizeof(EvReduce), hipMemcpyHostToDevice, st));
+    k_ev_prep<<<grid_for(in.n, 256 * 64), kThreads, 0, st>>>(in, deliver, red);
+    HIP_CHECK(hipGetLastError());
+    EvReduce r;
+    HIP_CHECK(hipMemcpyAsync(&r, red, sizeof(EvReduce), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (r.bad & 2) fail(SRG_ERR_ARG, "event node position out of range (>= table_n)");
+    if (r.bad & 1) fail(SRG_ERR_ARG, "event dst_host out of range (>= num_hosts)");
+    if (r.bad & 4) fail(SRG_ERR_LATENCY_RANGE, "deliver time overflows EmulatedTime (send + latency)");
+    EvKeyFmt f{};
+    const uint32_t b_id = bit_width64(r.id_max - r.id_min), b_src = bit_width64(r.src_max),
+                   b_t = bit_width64(r.t_max - r.t_min), b_dst = bit_width64(r.dst_max);
+    f.t_min = r.t_min;
+    f.id_min = r.id_min;
+    f.sh_src = b_id;
+    f.sh_t = b_id + b_src;
+    f.sh_dst = b_id + b_src + b_t;
+    const uint32_t bits = f.sh_dst + b_dst;
+    if (bits > 128) fail(SRG_ERR_ARG, "event batch key wider than 128 bits");
+    uint32_t passes = 0;
+    // an all-equal key (bits == 0) needs no pass; a 1-event batch is trivially ordered
+    if (bits <= 64) events_sort<false>(c, in, deliver, f, bits, out_order, host_off, st, passes);
+    else events_sort<true>(c, in, deliver, f, bits, out_order, host_off, st, passes);
+    if (res) {
+        res->min_next_event_ns = r.t_min;
+        res->min_used_latency_ns = r.lat_min;
+        res->key_bits = bits;
+        res->radix_passes = passes;
+    }
+}
+
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
     T* d = (T*)b.get(std::max<size_t>(count, 1) * sizeof(T));
@@ -1438,6 +1541,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SPARSE_LOCALITY:
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
+        case SRG_OPT_FW_PACKED:
+            ctx->fw_packed = value != 0.0;
+            return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
             ctx->algorithm = (int)value;
@@ -1543,6 +1649,28 @@ int srg_comm_size(srg_ctx* ctx, int* nranks, int* rank) {
     return SRG_OK;
 }
 
-const char* srg_version(void) { return "shadow_amd routing 0.2 (gfx950, dense FW u32/u64 + tight-DAG loss, RCCL row-block FW)"; }
+int srg_order_packet_events_device(srg_ctx* ctx, const srg_event_batch* b, const uint64_t* table, uint32_t table_n,
+                                   uint64_t* out_deliver, uint32_t* out_order, uint64_t* out_host_off,
+                                   void* hip_stream, srg_event_result* res, char* errbuf, size_t errlen) {
+    if (!ctx || !b || !out_host_off ||
+        (b->num_events && (!table || !out_deliver || !out_order || !b->src_node || !b->dst_node || !b->src_host ||
+                           !b->dst_host || !b->send_time_ns || !b->src_event_id))) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return guard(errbuf, errlen, [&]() {
+        auto t0 = std::chrono::steady_clock::now();
+        HIP_CHECK(hipSetDevice(ctx->device));
+        hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+        EvIn in{b->num_events, b->src_node, b->dst_node, b->src_host, b->dst_host, b->send_time_ns,
+                b->src_event_id, table, table_n, b->num_hosts, b->round_end_ns};
+        order_events_device(*ctx, in, out_deliver, out_order, out_host_off, st, res);
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (res) res->ms_total = ms_since(t0);
+    });
+}
+
+const char* srg_version(void) { return "shadow_amd routing 0.3 (gfx950, dense FW u32/u64 + tight-DAG loss, RCCL row-block FW, sparse BF, event batches)"; }
 
 }  // extern "C"

@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(64) tight_sparse_u32(const uint32_t* __restric
     for (int i = 0; i < 32; ++i) {
         const uint32_t t = b * TB + i;
         uint32_t v = St[i][lane];
-        if (t >= V || t == s || d[i] == 0xFFFFFFFFu) v = PRED_NONE;
+        if (t >= V || t == s || d[i] == KeyOps<uint32_t>::INF) v = PRED_NONE;
         out[i] = v;
     }
 }

@@ -91,6 +91,39 @@ def test_random_vs_oracle(scan_router, kw):
     assert_parity(tab, lat, loss)
 
 
+@pytest.mark.parametrize("packed", [0, 1])
+@pytest.mark.parametrize("kw", [dict(V=300, density=0.1, seed=111, lat_hi=40, parallel=0.1),
+                                dict(V=390, density=0.2, seed=112, directed=True, lat_lo=10**6, lat_hi=10**8)],
+                         ids=["ties", "directed_wide"])
+def test_fw_kernels_match_oracle(router, packed, kw):
+    """Both u32 FW tile kernels (pair-packed 64-bit adds and add + min3) are bit-exact; V not a
+    multiple of the 128 tile exercises the padding."""
+    r = Router(0)
+    r.set_option(N.SRG_OPT_FW_PACKED, packed)
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), list(range(V)))
+    t = r.compute_shortest_paths(g, list(range(V)))
+    assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
+    assert_parity(t, lat, loss)
+    r.close()
+
+
+@pytest.mark.parametrize("lat_lo,lat_hi,kind", [(2**27, 2**28, "u32"), (2**29, 2**30 + 2**29, "u64")])
+def test_u32_key_bound(router, lat_lo, lat_hi, kind):
+    """u32 keys hold distances < INF = 2^31 - 1 (packed pair adds must not carry); longer used
+    paths must be detected and rerun on u64 keys, bit-exact either way."""
+    g = synth.random_graph(60, 0.08, 113, lat_lo=lat_lo, lat_hi=lat_hi)
+    nodes = list(range(60))
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = router.compute_shortest_paths(g, nodes)
+    exp = N.SRG_PATH_DENSE_U32 if kind == "u32" else N.SRG_PATH_DENSE_U64
+    assert int(lat.max()) >= 2**31 - 1 if kind == "u64" else int(lat.max()) < 2**31 - 1
+    assert t.stats["path_kind"] == exp
+    assert_parity(t, lat, loss)
+
+
 def test_subset_nodes_scrambled(scan_router):
     router = scan_router
     g = synth.random_graph(180, 0.1, 7, lat_hi=100)

@@ -76,6 +76,68 @@ __global__ void __launch_bounds__(256) k(unsigned* out, unsigned seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// Pair-packed adds: two u32 keys <= 0x7FFFFFFF per 64-bit register, so one 64-bit add yields two
+// exact 32-bit sums.  MODE 0: v_lshl_add_u64 + v_min3_u32 (= two min-plus relaxations);
+// MODE 1: v_lshl_add_u64 only; MODE 2: plain C++ u64 add + min3 (what the compiler emits).
+template <int MODE>
+__global__ void __launch_bounds__(256) k64(unsigned* out, unsigned seed) {
+    unsigned long long p[8], q[8];
+    unsigned c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        p[i] = ((unsigned long long)(seed * (threadIdx.x + i) & 0x3FFFFFFF) << 32) | (seed ^ (threadIdx.x * 7 + i));
+        q[i] = ((unsigned long long)(seed + i) << 32) | (threadIdx.x & 0xFFFF);
+        c[i] = 0x7FFFFFFFu - i;
+    }
+    for (int it = 0; it < N_ITER; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            unsigned long long s;
+            unsigned r;
+            if constexpr (MODE == 0) {
+                asm volatile("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(s) : "v"(p[i]), "v"(q[i]));
+                asm volatile("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(c[i]), "v"((unsigned)s), "v"((unsigned)(s >> 32)));
+            } else if constexpr (MODE == 1) {
+                unsigned long long s0, s1;
+                asm volatile("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(s0) : "v"(p[i]), "v"(q[i]));
+                asm volatile("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(s1) : "v"(s0), "v"(q[i]));
+                asm volatile("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(s) : "v"(s1), "v"(p[i]));
+                r = (unsigned)s;
+            } else {
+                s = p[i] + q[i];
+                asm volatile("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(c[i]), "v"((unsigned)s), "v"((unsigned)(s >> 32)));
+            }
+            c[i] = r;
+            p[i] ^= (unsigned)s & 0xFFFu;
+        }
+    }
+    unsigned sum = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sum += c[i] + (unsigned)p[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = sum;
+}
+
+template <int MODE>
+void run64(const char* name, int ninstr) {
+    unsigned* out;
+    hipMalloc(&out, 256 * 4096 * 4);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const int blocks = 256 * 8;
+    k64<MODE><<<blocks, 256>>>(out, 1);
+    hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) k64<MODE><<<blocks, 256>>>(out, r + 2);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double winst = 5.0 * blocks * 4 * (double)N_ITER * 8 * (ninstr + 1);  // + the xor
+    const double per_simd_cycle = winst / (1024.0 * ms * 1e-3 * 2.4e9);
+    printf("%-34s %8.3f ms  %.3f wave-instr/SIMD/cycle@2.4GHz (peak 0.5)\n", name, ms, per_simd_cycle);
+    hipFree(out);
+}
+
 __global__ void check_min(unsigned* res) {
     // xorshift per thread; values spread over every exponent incl. denormals and 0
     unsigned x = 2463534242u ^ (blockIdx.x * 256 + threadIdx.x) * 2654435761u;
@@ -137,6 +199,9 @@ int main() {
     run<8>("min_f32_e32 x3", 3);
     run<9>("min_u32_e32 x3", 3);
     run<10>("min_i32_e32 x3", 3);
+    run64<0>("lshl_add_u64 + min3 (2 relax)", 2);
+    run64<1>("lshl_add_u64 x3", 3);
+    run64<2>("u64 '+' (compiler) + min3", 2);
     // exactness: v_min3_f32 on u32 bit patterns in [0, 2^31) incl. the denormal range
     unsigned *d;
     hipMalloc(&d, 4 * 3);
