@@ -95,6 +95,8 @@ __global__ void __launch_bounds__(256) k_ev_prep(EvIn in, uint64_t* __restrict__
         dmax = dh > dmax ? dh : dmax;
         smax = sh > smax ? sh : smax;
     }
+    // wave, then workgroup reduction: one set of same-address atomics per workgroup (a grid of
+    // ~2k workgroups), not per wave -- same-address atomics serialise at the memory side
     tmin = wave_min(tmin);
     tmax = wave_max(tmax);
     imin = wave_min(imin);
@@ -102,16 +104,39 @@ __global__ void __launch_bounds__(256) k_ev_prep(EvIn in, uint64_t* __restrict__
     lmin = wave_min(lmin);
     dmax = wave_max(dmax);
     smax = wave_max(smax);
+    __shared__ unsigned long long s64[5][4];
+    __shared__ uint32_t s32[2][4];
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&red->t_min, tmin);
-        atomicMax(&red->t_max, tmax);
-        atomicMin(&red->id_min, imin);
-        atomicMax(&red->id_max, imax);
-        atomicMin(&red->lat_min, lmin);
-        atomicMax(&red->dst_max, dmax);
-        atomicMax(&red->src_max, smax);
+        s64[0][w] = tmin;
+        s64[1][w] = tmax;
+        s64[2][w] = imin;
+        s64[3][w] = imax;
+        s64[4][w] = lmin;
+        s32[0][w] = dmax;
+        s32[1][w] = smax;
     }
-    if (bad) atomicOr(&red->bad, bad);
+    if (bad) atomicOr(&red->bad, bad);  // invalid input only
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int nw = (int)(blockDim.x + 63) >> 6;
+        for (int q = 1; q < nw; ++q) {
+            s64[0][0] = min(s64[0][0], s64[0][q]);
+            s64[1][0] = max(s64[1][0], s64[1][q]);
+            s64[2][0] = min(s64[2][0], s64[2][q]);
+            s64[3][0] = max(s64[3][0], s64[3][q]);
+            s64[4][0] = min(s64[4][0], s64[4][q]);
+            s32[0][0] = max(s32[0][0], s32[0][q]);
+            s32[1][0] = max(s32[1][0], s32[1][q]);
+        }
+        atomicMin(&red->t_min, s64[0][0]);
+        atomicMax(&red->t_max, s64[1][0]);
+        atomicMin(&red->id_min, s64[2][0]);
+        atomicMax(&red->id_max, s64[3][0]);
+        atomicMin(&red->lat_min, s64[4][0]);
+        atomicMax(&red->dst_max, s32[0][0]);
+        atomicMax(&red->src_max, s32[1][0]);
+    }
 }
 
 // Composite key layout: field f occupies bits [sh_f, sh_f + width_f) of the 128-bit (hi:lo) key.

@@ -1371,7 +1371,7 @@ void order_events_device(srg_ctx& c, const EvIn& in, uint64_t* deliver, uint32_t
     EvReduce* red = (EvReduce*)c.b_ered.get(sizeof(EvReduce));
     EvReduce init{~0ull, 0ull, ~0ull, 0ull, ~0ull, 0u, 0u, 0u, 0u};
     HIP_CHECK(hipMemcpyAsync(red, &init, sizeof(EvReduce), hipMemcpyHostToDevice, st));
-    k_ev_prep<<<grid_for(in.n, 256 * 64), kThreads, 0, st>>>(in, deliver, red);
+    k_ev_prep<<<grid_for(in.n, 2048), kThreads, 0, st>>>(in, deliver, red);
     HIP_CHECK(hipGetLastError());
     EvReduce r;
     HIP_CHECK(hipMemcpyAsync(&r, red, sizeof(EvReduce), hipMemcpyDeviceToHost, st));

@@ -2,9 +2,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_multi_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t18.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu --fw-packed 0 > gpurun_out/b18c.json 2> gpurun_out/b18c.err && \
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu --fw-packed 1 > gpurun_out/b18p.json 2> gpurun_out/b18p.err && \
-timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --fw-packed 0 --simulate-rank 8:3 > gpurun_out/b18s.json 2> gpurun_out/b18s.err && \
-timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --fw-packed 0 --fw-tile 64 --simulate-rank 8:3 >> gpurun_out/b18s.json 2>> gpurun_out/b18s.err
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t20.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --graph events --steps 5 --warmup 1 > gpurun_out/b20e.json 2> gpurun_out/b20e.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof20e -o run -- python -u bench.py --graph events --steps 2 --warmup 1 --no-cpu > gpurun_out/p20e.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke20.log 2>&1
 echo done
