@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--fw-packed", type=int, default=1, help="u32 FW tiles: 1 = packed-pair adds, 0 = add + min3")
+    ap.add_argument("--scan-variant", type=int, default=None, help="u32 tight scan kernel (0 readlane, 1 scalar)")
     ap.add_argument("--simulate-rank", type=str, default=None,
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
                          "(outputs invalid; prints a diagnostic line, never the bench result)")
@@ -190,6 +191,8 @@ def main():
     if args.fw_tile:
         router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
     router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
+    if args.scan_variant is not None:
+        router.set_option(N.SRG_OPT_SCAN_VARIANT, args.scan_variant)
     if args.simulate_rank:
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)

@@ -322,8 +322,11 @@ template <class K, int T, int KC, bool PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J);
 
 // PK = true (u32 keys only): the pair-packed tile below (fw_tile_pk); false: add + min3.
+#ifndef SRG_PK_MINB
+#define SRG_PK_MINB 1  // workgroups per CU the packed tile is register-budgeted for
+#endif
 template <class K, int T, int KC, bool PK>
-__global__ void __launch_bounds__(256) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
+__global__ void __launch_bounds__(256, PK ? SRG_PK_MINB : 1) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
     fw_tile<K, T, KC, PK>(D, ld, kb, tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1),
                           tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1));
 }
@@ -371,8 +374,9 @@ struct PkStage {
     static_assert(T % 32 == 0 && KC % 8 == 0, "pk tile");
     static constexpr int LDA = T + 2;                    // pairs per LDS row
     static constexpr int AV = T * KC / 4 / 256;          // A: 16-B vectors (4 k values) per thread
-    static constexpr int BT = (KC / 2) * (T / 4) / 256;  // B: pair-row tasks (two 16-B loads) per thread
-    static_assert(AV >= 1 && BT >= 1, "pk staging");
+    static constexpr int BTN = (KC / 2) * (T / 4);       // B: pair-row tasks (two 16-B loads each)
+    static constexpr int BT = (BTN + 255) / 256;         //    per thread (the last one maybe partial)
+    static_assert(AV >= 1 && T * KC / 4 % 256 == 0, "pk staging");
     Vec16<uint32_t> a[AV], b0[BT], b1[BT];
 };
 
@@ -389,6 +393,7 @@ __device__ __forceinline__ void pk_load(PkStage<T, KC>& sg, const uint32_t* __re
 #pragma unroll
     for (int q = 0; q < S::BT; ++q) {
         const int v = tid + 256 * q, p = v / (T / 4), jq = v % (T / 4);
+        if (S::BTN % 256 != 0 && v >= S::BTN) break;
         const uint32_t* r0 = B + (size_t)(k0 + 2 * p) * ld + jq * 4;
         sg.b0[q] = ld16(r0);
         sg.b1[q] = ld16(r0 + ld);
@@ -410,6 +415,7 @@ __device__ __forceinline__ void pk_store(const PkStage<T, KC>& sg, u64p* __restr
 #pragma unroll
     for (int q = 0; q < S::BT; ++q) {
         const int v = tid + 256 * q, p = v / (T / 4), jq = v % (T / 4);
+        if (S::BTN % 256 != 0 && v >= S::BTN) break;
         const uint32_t* x = sg.b0[q].v;
         const uint32_t* y = sg.b1[q].v;
         VecN<u64p, 2> w0, w1;

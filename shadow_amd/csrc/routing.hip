@@ -403,6 +403,7 @@ struct srg_ctx {
     bool sparse_locality = true;     // sparse: batch sources in BFS order
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
+    int scan_variant = 1;            // u32 tight scan: 0 = vector entry batches + v_readlane, 1 = scalar entry loads (default)
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -584,7 +585,10 @@ Plan make_plan(int G, int g, uint32_t V, int T, const std::vector<uint32_t>& nod
     return p;
 }
 
-constexpr int KC = 32;
+#ifndef SRG_FW_KC
+#define SRG_FW_KC 32
+#endif
+constexpr int KC = SRG_FW_KC;
 
 // tiles of one min-plus product launch: rows [ra, rb) minus {rx...}, cols [ca, cb) minus {cx...}
 struct Rect {
@@ -694,6 +698,9 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
         if (pl.own(k1)) {
             fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1);
             HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
+            // the column panel of k1 rewrites tile (kb, k1) of panel kb: its broadcast (still the
+            // last one recorded in ev_c) must have left first
+            if (multi) HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
             fw_tiles_pair<K, T, PK>(D, Vp, k1, make_rect(k1, k1 + 1, {}, 0, nb, {k1}), colp, lds, aux, sk);
         }
         if (multi) {
@@ -719,7 +726,10 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
             ++prof_n;
         }
         HIP_CHECK(hipStreamWaitEvent(st, c.ev_d, 0));
-        if (multi) HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));  // panel k1 sent/received before it is reused
+        // receivers need panel k1 before their next updates; its owner only before it rewrites a
+        // tile of it (the column panel of k2 on aux, which waits above), so the owner's chain of
+        // k2 overlaps the broadcast of k1
+        if (multi && !pl.own(k1)) HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
     }
 }
 
@@ -945,9 +955,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
-                tight_sparse_u32<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc,
-                                                      V, nbT, nbS, eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED,
-                                                      Vp);
+                auto scan = c.scan_variant ? tight_sparse_u32_s : tight_sparse_u32;
+                scan<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbT, nbS, eblk,
+                                          ent_ro, (const uint32_t*)ent_w, ent_tl, PRED, Vp);
             } else {
                 tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, lnodes, nloc, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
                                                       PRED, Vp);
@@ -1543,6 +1553,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_FW_PACKED:
             ctx->fw_packed = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_SCAN_VARIANT:
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

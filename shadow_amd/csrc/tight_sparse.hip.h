@@ -308,6 +308,83 @@ __global__ void __launch_bounds__(64) tight_sparse_u32(const uint32_t* __restric
     }
 }
 
+// Variant with scalar entry loads: the entry index is wave-uniform, so (row offset, w, tl) are
+// read with s_load into SGPRs (no v_readlane per entry); the hit test is a wave-uniform branch
+// (one s_cbranch on the compare mask) and w enters the add as an SGPR operand.  Keys <= INF
+// (2^31 - 1) so the plain add never wraps.  Same static load schedule: 32 row loads in flight,
+// the next chunk's row for slot j issued right after slot j is consumed.
+__global__ void __launch_bounds__(64) tight_sparse_u32_s(const uint32_t* __restrict__ DST, size_t npad,
+                                                          uint32_t dst_bytes, const uint32_t* __restrict__ nodes,
+                                                          uint32_t n, uint32_t V, uint32_t nbT, uint32_t nbS,
+                                                          const uint32_t* __restrict__ eblk,
+                                                          const uint32_t* __restrict__ ent_ro,
+                                                          const uint32_t* __restrict__ ent_w,
+                                                          const uint32_t* __restrict__ ent_tl,
+                                                          uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ uint32_t St[TB][64];
+    uint32_t b, c;
+    sparse_block_coords(nbT, b, c);
+    if (c >= nbS) return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t r = c * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t voff = r * 4u;
+    v32u d;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (uint32_t)((b * TB + i) * npad * 4u), 0);
+        St[i][lane] = PRED_NONE;
+    }
+    const uint32_t e_beg = __builtin_amdgcn_readfirstlane(eblk[b]);
+    const uint32_t e_end = __builtin_amdgcn_readfirstlane(eblk[b + 1]);  // a multiple of 64 apart
+    if (e_beg < e_end) {
+        // 16-entry groups as 64-B aligned uniform loads -> s_load_dwordx16 (e is a multiple of 32)
+        struct alignas(64) U16 {
+            uint32_t v[16];
+        };
+        auto ld16u = [](const uint32_t* p) { return *reinterpret_cast<const U16*>(p); };
+        uint32_t A[32];
+        {
+            const U16 r0 = ld16u(ent_ro + e_beg), r1 = ld16u(ent_ro + e_beg + 16);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                A[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r0.v[j], 0);
+                A[16 + j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r1.v[j], 0);
+            }
+        }
+        for (uint32_t e = e_beg; e < e_end; e += 32) {
+            const U16 w0 = ld16u(ent_w + e), w1 = ld16u(ent_w + e + 16);
+            const U16 t0 = ld16u(ent_tl + e), t1 = ld16u(ent_tl + e + 16);
+            const U16 n0 = ld16u(ent_ro + e + 32), n1 = ld16u(ent_ro + e + 48);  // next chunk / sentinel pad
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const uint32_t w = j < 16 ? w0.v[j] : w1.v[j - 16];
+                const uint32_t tl = j < 16 ? t0.v[j] : t1.v[j - 16];
+                const uint32_t nro = j < 16 ? n0.v[j] : n1.v[j - 16];
+                const uint32_t x = A[j] + w;
+                const bool hit = x == d[tl];
+                if (__builtin_expect(__ballot(hit) != 0, 0)) {
+                    if (hit) {
+                        const uint32_t st = St[tl][lane];
+                        St[tl][lane] = (st == PRED_NONE) ? e + j : PRED_MULTI;
+                    }
+                }
+                A[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nro, 0);
+            }
+        }
+    }
+    if (r >= n) return;
+    const uint32_t s = nodes[r];
+    uint32_t* out = PRED + (size_t)r * ldp + b * TB;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t t = b * TB + i;
+        uint32_t v = St[i][lane];
+        if (t >= V || t == s || d[i] == KeyOps<uint32_t>::INF) v = PRED_NONE;
+        out[i] = v;
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,

@@ -110,7 +110,26 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("lat_lo,lat_hi,kind", [(2**27, 2**28, "u32"), (2**29, 2**30 + 2**29, "u64")])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_scan_variants_match_oracle(variant):
+    """Both u32 tight-scan kernels (vector entry batches + readlane, scalar entry loads)."""
+    r = Router(0)
+    r.set_option(N.SRG_OPT_SCAN_VARIANT, variant)
+    r.set_option(N.SRG_OPT_SPARSE_THRESHOLD, 1.0)
+    for kw in (dict(V=300, density=0.1, seed=121, lat_hi=30, parallel=0.2),
+               dict(V=257, density=0.4, seed=122, directed=True, lat_lo=10**6, lat_hi=10**8)):
+        kw = dict(kw)
+        V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+        g = synth.random_graph(V, dens, seed, **kw)
+        nodes = np.random.default_rng(seed).permutation(V).tolist()
+        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+        t = r.compute_shortest_paths(g, nodes)
+        assert t.stats["scan_kind"] == N.SRG_SCAN_SPARSE
+        assert_parity(t, lat, loss)
+    r.close()
+
+
+@pytest.mark.parametrize("lat_lo,lat_hi,kind",[(2**27, 2**28, "u32"), (2**29, 2**30 + 2**29, "u64")])
 def test_u32_key_bound(router, lat_lo, lat_hi, kind):
     """u32 keys hold distances < INF = 2^31 - 1 (packed pair adds must not carry); longer used
     paths must be detected and rerun on u64 keys, bit-exact either way."""
@@ -205,6 +224,41 @@ def test_c1_full_vs_oracle(router):
     nodes = list(range(1000))
     lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, nthreads=16)
     assert_parity(router.compute_shortest_paths(e, nodes), lat, loss)
+
+
+@pytest.mark.slow
+def test_c3_bench_size_sampled_rows(router):
+    """Config C3 at the bench's full size (10 000-vertex Atlas-like complete graph, the headline
+    workload) through the device entry: 8 seeded oracle rows bit-exact, plus size-independent
+    properties over the whole 10^8-pair table (diagonal = self-loops, symmetric latency, every
+    latency <= the direct edge, every loss in [0, 1])."""
+    import torch
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+    V = 10000
+    e = synth.atlas_like(V, seed=V)
+    dg = DeviceGraph(e)
+    nodes_t = torch.arange(V, dtype=torch.int32, device="cuda:0")
+    ol = torch.empty((V, V), dtype=torch.int64, device="cuda:0")
+    os_ = torch.empty((V, V), dtype=torch.float32, device="cuda:0")
+    st = compute_shortest_paths_device(router, dg, nodes_t, ol, os_)
+    torch.cuda.synchronize()
+    assert st["path_kind"] == N.SRG_PATH_DENSE_U32
+    lat_t = ol.cpu().numpy().view(np.uint64)
+    loss_t = os_.cpu().numpy()
+    del ol, os_
+    rows = np.random.default_rng(V).choice(V, 8, replace=False).tolist()
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), list(range(V)), rows=rows, nthreads=16)
+    assert np.array_equal(lat_t[rows], lat)
+    assert bits_equal(loss_t[rows], loss)
+    assert np.array_equal(np.diag(lat_t), e.latency_ns[:V])
+    off = ~np.eye(V, dtype=bool)
+    assert np.array_equal(lat_t[off], lat_t.T[off])
+    direct = np.full((V, V), np.iinfo(np.uint64).max, dtype=np.uint64)
+    m = e.src != e.dst
+    direct[e.src[m], e.dst[m]] = e.latency_ns[m]
+    direct[e.dst[m], e.src[m]] = e.latency_ns[m]
+    assert np.all(lat_t[off] <= direct[off])
+    assert np.all((loss_t >= 0) & (loss_t <= 1))
 
 
 @pytest.mark.slow
