@@ -122,7 +122,7 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
 #define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles: 1 (default) = two relaxations per 64-bit add of
                                      packed key pairs + v_min3; 0 = one add per relaxation */
-#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 1 (default) = scalar (s_load) entry reads, 0 = vector entry batches broadcast with
+#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 2 (default) = entries grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches broadcast with
                                      v_readlane */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 

@@ -403,7 +403,7 @@ struct srg_ctx {
     bool sparse_locality = true;     // sparse: batch sources in BFS order
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
-    int scan_variant = 1;            // u32 tight scan: 0 = vector entry batches + v_readlane, 1 = scalar entry loads (default)
+    int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default)
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -416,7 +416,7 @@ struct srg_ctx {
     DevBuf b_stats, b_flags, b_multi, b_pos, b_cnt;
     // sparse tight scan
     DevBuf b_ecnt, b_eoff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu, b_grpe, b_cscent,
-        b_gblk, b_DST, b_scantmp, b_ess;
+        b_gblk, b_DST, b_scantmp, b_ess, b_rlen, b_roff;
     // multi-rank: local sources, their output rows, exchange staging
     DevBuf b_lnodes, b_lpos, b_allpos, b_stage, b_red, b_outoff, b_outdst;
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
@@ -426,7 +426,7 @@ struct srg_ctx {
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
-                          &b_scantmp, &b_ess, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst,
+                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst,
                           &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
@@ -687,17 +687,17 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
             break;
         }
         const int k1 = kb + 1;
-        // critical chain: row k1 (w.r.t. kb) -> close pivot k1 -> its row + column panels
+        // critical chain on the (high-priority) aux stream, concurrent with the bulk tiles of kb
+        // on st: row k1 + own column k1 (w.r.t. kb) in one launch -> close pivot k1 -> its row +
+        // column panels.  The chain's tiles are disjoint from the bulk's; both only read panel kb.
         const bool sk = pl.G > 1;  // split-K the chain's short launches when the rest is short too
-        if (pl.own(k1)) fw_tiles<K, T, PK>(D, Vp, kb, k1, k1 + 1, {}, 0, nb, {kb}, lds, st, sk);  // row k1
-        HIP_CHECK(hipEventRecord(c.ev_a, st));
-        fw_tiles<K, T, PK>(D, Vp, kb, r0, r1, {kb, k1}, k1, k1 + 1, {}, lds, st, sk);             // own col k1
-        HIP_CHECK(hipEventRecord(c.ev_e, st));
+        HIP_CHECK(hipEventRecord(c.ev_a, st));  // st: bulk of kb-1 (row k1 w.r.t. kb-1) done
         HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
+        const Rect rowr = pl.own(k1) ? make_rect(k1, k1 + 1, {}, 0, nb, {kb}) : Rect{TileSet{0, -1, -1, 0, -1, -1}, 0, 0};
+        fw_tiles_pair<K, T, PK>(D, Vp, kb, rowr, make_rect(r0, r1, {kb, k1}, k1, k1 + 1, {}), lds, aux, sk);
         const Rect colp = make_rect(r0, r1, {k1}, k1, k1 + 1, {});  // own column panel of k1
         if (pl.own(k1)) {
             fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1);
-            HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
             // the column panel of k1 rewrites tile (kb, k1) of panel kb: its broadcast (still the
             // last one recorded in ev_c) must have left first
             if (multi) HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
@@ -710,7 +710,6 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
             HIP_CHECK(hipEventRecord(c.ev_c, cs));
             if (!pl.own(k1)) {  // the pivot tile arrives in the panel
                 HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
-                HIP_CHECK(hipStreamWaitEvent(aux, c.ev_e, 0));
                 fw_tiles_pair<K, T, PK>(D, Vp, k1, Rect{TileSet{0, -1, -1, 0, -1, -1}, 0, 0}, colp, lds, aux, sk);
             }
         }
@@ -931,11 +930,30 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     n_ess = E_ess;
     const size_t npad = ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
+    // run layout (entries grouped by target, SRG_OPT_SCAN_VARIANT 2): run offsets from indeg
+    const bool runs = sizeof(K) == 4 && c.scan_variant == 2;
+    const uint32_t NT = nw64 * 64;  // == nbT * TB targets
+    uint32_t* roff = nullptr;
+    uint64_t E_runs = 0;
+    if (runs) {
+        uint32_t* rlen = (uint32_t*)c.b_rlen.get(((size_t)NT + 1) * 4);
+        roff = (uint32_t*)c.b_roff.get(((size_t)NT + 1) * 4);
+        k_run_len<<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, V, NT, rlen);
+        size_t tb3 = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, rlen, roff, (int)(NT + 1), st));
+        void* tmp3 = c.b_scantmp.get(std::max(tb3, tbytes));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp3, tb3, rlen, roff, (int)(NT + 1), st));
+        uint32_t tot = 0;
+        HIP_CHECK(hipMemcpyAsync(&tot, roff + NT, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        E_runs = tot;
+    }
+    const uint64_t E_layout = runs ? E_runs : E_pad;
     const bool sparse = (double)E_ess <= c.sparse_threshold * (double)V * (double)V &&
-                        E_pad + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
+                        E_layout + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
     if (sparse) {
         scan_kind = SRG_SCAN_SPARSE;
-        const size_t Eb = E_pad + 256;
+        const size_t Eb = E_layout + 256;
         uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
         uint32_t* ent_ro = (uint32_t*)c.b_entkey.get(Eb * 4);
         K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
@@ -946,8 +964,12 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
         k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
             ess, W, WL, Vp, V, nw64, std::max<size_t>(npad, 64), eoff, eblk, cscoff, cscfill, ent_ro, ent_w, ent_tl,
-            ent_u, ent_b, cscent);
-        k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
+            ent_u, ent_b, cscent, roff);
+        if (runs)
+            k_run_pad<K><<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, roff, V, NT, ent_ro, ent_w, ent_tl,
+                                                                          ent_u, ent_b);
+        else
+            k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
         HIP_CHECK(hipGetLastError());
         if (nloc) {
             const uint32_t nbS = (uint32_t)(npad / 64);
@@ -955,9 +977,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
-                auto scan = c.scan_variant ? tight_sparse_u32_s : tight_sparse_u32;
-                scan<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbT, nbS, eblk,
-                                          ent_ro, (const uint32_t*)ent_w, ent_tl, PRED, Vp);
+                auto scan = runs ? tight_sparse_u32_runs : c.scan_variant ? tight_sparse_u32_s : tight_sparse_u32;
+                scan<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbT, nbS,
+                                          runs ? roff : eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED, Vp);
             } else {
                 tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, lnodes, nloc, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
                                                       PRED, Vp);
@@ -1555,7 +1577,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = value != 0.0;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:

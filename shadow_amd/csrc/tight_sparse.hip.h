@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(256) k_ess_fill(const unsigned long long* __re
                                                    uint32_t* __restrict__ csc_fill, uint32_t* __restrict__ ent_ro,
                                                    K* __restrict__ ent_w, uint32_t* __restrict__ ent_tl,
                                                    uint32_t* __restrict__ ent_u, float* __restrict__ ent_b,
-                                                   uint32_t* __restrict__ csc_ent) {
+                                                   uint32_t* __restrict__ csc_ent, const uint32_t* __restrict__ roff) {
     const uint32_t lane = threadIdx.x & 63;
     const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
     const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
@@ -121,13 +121,14 @@ __global__ void __launch_bounds__(256) k_ess_fill(const unsigned long long* __re
         const uint32_t tl = lane & 31u;
         const uint32_t rank = (uint32_t)__popcll(hm & ((1ull << tl) - 1ull));
         const size_t qb = (size_t)b * V + u;
-        const uint32_t e = eblk[b] + (eoff[qb] - eoff[(size_t)b * V]) + rank;
+        const uint32_t k = atomicAdd(&csc_fill[t], 1u);
+        // block layout: u-sorted within the 32-target block; run layout: grouped by target
+        const uint32_t e = roff ? roff[t] + k : eblk[b] + (eoff[qb] - eoff[(size_t)b * V]) + rank;
         ent_ro[e] = (uint32_t)((size_t)u * npad * sizeof(K));
         ent_w[e] = W[(size_t)u * ld + t];
         ent_tl[e] = tl;
         ent_u[e] = u;
         ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));
-        const uint32_t k = atomicAdd(&csc_fill[t], 1u);
         csc_ent[csc_off[t] + k] = e;
     }
 }
@@ -370,6 +371,104 @@ __global__ void __launch_bounds__(64) tight_sparse_u32_s(const uint32_t* __restr
                     }
                 }
                 A[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nro, 0);
+            }
+        }
+    }
+    if (r >= n) return;
+    const uint32_t s = nodes[r];
+    uint32_t* out = PRED + (size_t)r * ldp + b * TB;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t t = b * TB + i;
+        uint32_t v = St[i][lane];
+        if (t >= V || t == s || d[i] == KeyOps<uint32_t>::INF) v = PRED_NONE;
+        out[i] = v;
+    }
+}
+
+// ---- run layout (SRG_OPT_SCAN_VARIANT 2) -------------------------------------------------
+// Entries grouped by TARGET: target t's essential in-arcs occupy [roff[t], roff[t] + indeg[t]),
+// the run padded with sentinels to a multiple of RUN_CHUNK, runs of one 32-target block
+// contiguous.  Every RUN_CHUNK-entry chunk then has ONE target, so the scan reads d[tl] once per
+// chunk (instead of a register-indexed read per entry) and counts hits in registers with no
+// per-entry branch; St is touched once per chunk, only when a lane hit.
+constexpr uint32_t RUN_CHUNK = 16;
+
+__global__ void k_run_len(const uint32_t* __restrict__ indeg, uint32_t V, uint32_t NT, uint32_t* __restrict__ rlen) {
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t <= NT; t += (size_t)gridDim.x * blockDim.x)
+        rlen[t] = (t < V && t < NT) ? (indeg[t] + RUN_CHUNK - 1) / RUN_CHUNK * RUN_CHUNK : 0u;
+}
+
+template <class K>
+__global__ void k_run_pad(const uint32_t* __restrict__ indeg, const uint32_t* __restrict__ roff, uint32_t V,
+                          uint32_t NT, uint32_t* __restrict__ ent_ro, K* __restrict__ ent_w,
+                          uint32_t* __restrict__ ent_tl, uint32_t* __restrict__ ent_u, float* __restrict__ ent_b) {
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t <= NT; t += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t beg = roff[t] + ((t < V && t < NT) ? indeg[t] : 0u);
+        const uint32_t end = t < NT ? roff[t + 1] : roff[NT] + 256u;  // + tail read by the prefetch
+        for (uint32_t e = beg; e < end; ++e) {
+            ent_ro[e] = 0;
+            ent_w[e] = KeyOps<K>::INF;
+            ent_tl[e] = (uint32_t)(t % TB);
+            ent_u[e] = 0;
+            ent_b[e] = 1.0f;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) tight_sparse_u32_runs(const uint32_t* __restrict__ DST, size_t npad,
+                                                             uint32_t dst_bytes, const uint32_t* __restrict__ nodes,
+                                                             uint32_t n, uint32_t V, uint32_t nbT, uint32_t nbS,
+                                                             const uint32_t* __restrict__ roff,
+                                                             const uint32_t* __restrict__ ent_ro,
+                                                             const uint32_t* __restrict__ ent_w,
+                                                             const uint32_t* __restrict__ ent_tl,
+                                                             uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ uint32_t St[TB][64];
+    uint32_t b, c;
+    sparse_block_coords(nbT, b, c);
+    if (c >= nbS) return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t r = c * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t voff = r * 4u;
+    v32u d;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (uint32_t)((b * TB + i) * npad * 4u), 0);
+        St[i][lane] = PRED_NONE;
+    }
+    const uint32_t e_beg = __builtin_amdgcn_readfirstlane(roff[b * TB]);
+    const uint32_t e_end = __builtin_amdgcn_readfirstlane(roff[b * TB + TB]);  // a multiple of RUN_CHUNK apart
+    if (e_beg < e_end) {
+        struct alignas(64) U16 {
+            uint32_t v[RUN_CHUNK];
+        };
+        auto ld16u = [](const uint32_t* p) { return *reinterpret_cast<const U16*>(p); };
+        uint32_t A[RUN_CHUNK];
+        {
+            const U16 r0 = ld16u(ent_ro + e_beg);
+#pragma unroll
+            for (uint32_t j = 0; j < RUN_CHUNK; ++j) A[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r0.v[j], 0);
+        }
+        for (uint32_t e = e_beg; e < e_end; e += RUN_CHUNK) {
+            const U16 w0 = ld16u(ent_w + e);
+            const U16 n0 = ld16u(ent_ro + e + RUN_CHUNK);  // the next chunk's rows (or the sentinel tail)
+            const uint32_t tl = __builtin_amdgcn_readfirstlane(ent_tl[e]);
+            const uint32_t dd = d[tl];
+            uint32_t cnt = 0, lastj = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < RUN_CHUNK; ++j) {
+                const bool hit = A[j] + w0.v[j] == dd;
+                cnt += hit ? 1u : 0u;
+                lastj = hit ? j : lastj;
+                A[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, n0.v[j], 0);
+            }
+            if (__ballot(cnt != 0)) {
+                if (cnt) {
+                    const uint32_t st = St[tl][lane];
+                    St[tl][lane] = (st == PRED_NONE && cnt == 1) ? e + lastj : PRED_MULTI;
+                }
             }
         }
     }

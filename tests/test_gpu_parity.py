@@ -110,9 +110,9 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_scan_variants_match_oracle(variant):
-    """Both u32 tight-scan kernels (vector entry batches + readlane, scalar entry loads)."""
+    """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs."""
     r = Router(0)
     r.set_option(N.SRG_OPT_SCAN_VARIANT, variant)
     r.set_option(N.SRG_OPT_SPARSE_THRESHOLD, 1.0)

@@ -2,7 +2,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_sparse_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t23.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --graph ba --steps 2 --warmup 1 --no-cpu > gpurun_out/b23ba.json 2> gpurun_out/b23ba.err && \
-timeout -k 10 300 python -u bench.py --graph ba --steps 2 --warmup 1 --no-cpu --no-locality > gpurun_out/b23ban.json 2> gpurun_out/b23ban.err
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t25.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/b25.json 2> gpurun_out/b25.err && \
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --simulate-rank 8:3 > gpurun_out/b25s.json 2> gpurun_out/b25s.err && \
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --simulate-rank 4:1 >> gpurun_out/b25s.json 2>> gpurun_out/b25s.err && \
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --simulate-rank 2:0 >> gpurun_out/b25s.json 2>> gpurun_out/b25s.err
 echo done
