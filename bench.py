@@ -121,6 +121,51 @@ def bench_events(args, n=10**7, hosts=10000):
                       "cpu_baseline": cpu}), flush=True)
 
 
+def init_strong_router(local, dev):
+    """RCCL-backed router for the multi-GPU build, with an agreed go/no-go on every rank: librccl
+    must load everywhere before the collective init, and a small multi-rank build must equal the
+    single-GPU build bit for bit.  (None, reason) -> the caller runs independent replicas."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from shadow_amd import Router, synth
+    from shadow_amd import dist as sd
+
+    def agree(ok):
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    try:
+        Router.comm_unique_id()  # loads librccl (no collective)
+        ok = True
+    except Exception as e:  # noqa: BLE001
+        log(f"librccl: {e}")
+        ok = False
+    if not agree(ok):
+        return None, "librccl unavailable"
+    try:
+        router = sd.init_router(local)
+    except Exception as e:  # noqa: BLE001
+        log(f"RCCL communicator: {e}")
+        router = None
+    if not agree(router is not None):
+        return None, "RCCL communicator init failed"
+    g = synth.random_graph(300, 0.05, 1234, lat_hi=1000)
+    nodes = list(range(300))
+    try:
+        got = router.compute_shortest_paths(g, nodes)
+        ref = Router(local).compute_shortest_paths(g, nodes)
+        ok = np.array_equal(got.latency_ns, ref.latency_ns) and np.array_equal(
+            got.packet_loss.view(np.uint32), ref.packet_loss.view(np.uint32))
+    except Exception as e:  # noqa: BLE001
+        log(f"multi-rank sanity build: {e}")
+        ok = False
+    if not agree(ok):
+        return None, "multi-rank sanity check failed"
+    return router, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,12 +224,15 @@ def main():
     out_lat = torch.empty((V, V), dtype=torch.int64, device=dev)
     out_loss = torch.empty((V, V), dtype=torch.float32, device=dev)
     strong = world > 1 and not args.replicas
+    fallback = None
     if strong:
-        from shadow_amd import dist as sd
-        router = sd.init_router(local)
-        if args.no_gather:
+        router, fallback = init_strong_router(local, dev)
+        if router is None:
+            log(f"[rank {rank}] multi-rank build unavailable ({fallback}): running independent replicas")
+            strong = False
+        elif args.no_gather:
             router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
-    else:
+    if not strong:
         router = Router(local)
     if args.no_locality:
         router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
@@ -288,6 +336,7 @@ def main():
             "config": {"workload": f"{gdesc}, all {V} nodes used, edge list resident in HBM",
                        "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
                        "parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single",
+                       **({"fallback": fallback} if fallback else {}),
                        "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
             "apsp_wall_ms": round(ms_per_step, 3),
             "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange")},
