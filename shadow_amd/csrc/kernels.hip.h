@@ -477,23 +477,30 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
         const u64p* Ap = lds + ((ch - ch0) & 1) * BUF;
         const u64p* Bp = Ap + (KC / 2) * LDA;
         if (ch + 1 < ch1) pk_load<T, KC>(sg, A, B, ld, arow, (ch + 1) * KC);  // issue early
-#pragma unroll 4
-        for (int kp = 0; kp < KC / 2; ++kp) {
-            u64p ap[M], bp[M];
+        // operands of k-pair kp+1 are read from LDS while kp is folded (two register sets)
+        u64p ap[2][M], bp[2][M];
+        auto rd = [&](int kp, u64p* xa, u64p* xb) {
 #pragma unroll
             for (int g = 0; g < M / 2; ++g) {
                 VecN<u64p, 2> va = ldv<u64p, 2>(Ap + kp * LDA + 32 * g + 2 * ty);
                 VecN<u64p, 2> vb = ldv<u64p, 2>(Bp + kp * LDA + 32 * g + 2 * tx);
-                ap[2 * g] = va.v[0];
-                ap[2 * g + 1] = va.v[1];
-                bp[2 * g] = vb.v[0];
-                bp[2 * g + 1] = vb.v[1];
+                xa[2 * g] = va.v[0];
+                xa[2 * g + 1] = va.v[1];
+                xb[2 * g] = vb.v[0];
+                xb[2 * g + 1] = vb.v[1];
             }
+        };
+        rd(0, ap[0], bp[0]);
+#pragma unroll
+        for (int kp = 0; kp < KC / 2; ++kp) {
+            if (kp + 1 < KC / 2) rd(kp + 1, ap[(kp + 1) & 1], bp[(kp + 1) & 1]);
+            const u64p* xa = ap[kp & 1];
+            const u64p* xb = bp[kp & 1];
 #pragma unroll
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b) {
-                    const u64p s = add_pairs(ap[a], bp[b]);
+                    const u64p s = add_pairs(xa[a], xb[b]);
                     c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         }
