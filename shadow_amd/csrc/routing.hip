@@ -977,9 +977,17 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
-                auto scan = runs ? tight_sparse_u32_runs : c.scan_variant ? tight_sparse_u32_s : tight_sparse_u32;
-                scan<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbT, nbS,
-                                          runs ? roff : eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED, Vp);
+                if (runs) {
+                    constexpr uint32_t TBR = 16;
+                    const uint32_t nbR = NT / TBR;
+                    tight_sparse_u32_runs<TBR><<<8u * nbR * ((nbS + 7) / 8), 64, 0, st>>>(
+                        (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbR, nbS, roff, ent_ro,
+                        (const uint32_t*)ent_w, ent_tl, PRED, Vp);
+                } else {
+                    auto scan = c.scan_variant ? tight_sparse_u32_s : tight_sparse_u32;
+                    scan<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbT, nbS,
+                                              eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED, Vp);
+                }
             } else {
                 tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, lnodes, nloc, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
                                                       PRED, Vp);

@@ -416,6 +416,9 @@ __global__ void k_run_pad(const uint32_t* __restrict__ indeg, const uint32_t* __
     }
 }
 
+// TBR targets per wave (16: the waves resident on one XCD then all work on the same source
+// block, whose DST column block (V x 256 B) stays L2-resident)
+template <uint32_t TBR>
 __global__ void __launch_bounds__(64) tight_sparse_u32_runs(const uint32_t* __restrict__ DST, size_t npad,
                                                              uint32_t dst_bytes, const uint32_t* __restrict__ nodes,
                                                              uint32_t n, uint32_t V, uint32_t nbT, uint32_t nbS,
@@ -424,22 +427,23 @@ __global__ void __launch_bounds__(64) tight_sparse_u32_runs(const uint32_t* __re
                                                              const uint32_t* __restrict__ ent_w,
                                                              const uint32_t* __restrict__ ent_tl,
                                                              uint32_t* __restrict__ PRED, size_t ldp) {
-    __shared__ uint32_t St[TB][64];
+    typedef uint32_t vdu __attribute__((ext_vector_type(TBR)));
+    __shared__ uint32_t St[TBR][64];
     uint32_t b, c;
-    sparse_block_coords(nbT, b, c);
+    sparse_block_coords(nbT, b, c);  // nbT = number of TBR-target blocks
     if (c >= nbS) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t r = c * 64 + lane;
     const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
     const uint32_t voff = r * 4u;
-    v32u d;
+    vdu d;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (uint32_t)((b * TB + i) * npad * 4u), 0);
+    for (uint32_t i = 0; i < TBR; ++i) {
+        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, (uint32_t)((b * TBR + i) * npad * 4u), 0);
         St[i][lane] = PRED_NONE;
     }
-    const uint32_t e_beg = __builtin_amdgcn_readfirstlane(roff[b * TB]);
-    const uint32_t e_end = __builtin_amdgcn_readfirstlane(roff[b * TB + TB]);  // a multiple of RUN_CHUNK apart
+    const uint32_t e_beg = __builtin_amdgcn_readfirstlane(roff[b * TBR]);
+    const uint32_t e_end = __builtin_amdgcn_readfirstlane(roff[b * TBR + TBR]);  // a multiple of RUN_CHUNK apart
     if (e_beg < e_end) {
         struct alignas(64) U16 {
             uint32_t v[RUN_CHUNK];
@@ -454,7 +458,7 @@ __global__ void __launch_bounds__(64) tight_sparse_u32_runs(const uint32_t* __re
         for (uint32_t e = e_beg; e < e_end; e += RUN_CHUNK) {
             const U16 w0 = ld16u(ent_w + e);
             const U16 n0 = ld16u(ent_ro + e + RUN_CHUNK);  // the next chunk's rows (or the sentinel tail)
-            const uint32_t tl = __builtin_amdgcn_readfirstlane(ent_tl[e]);
+            const uint32_t tl = __builtin_amdgcn_readfirstlane(ent_tl[e]) % TBR;
             const uint32_t dd = d[tl];
             uint32_t cnt = 0, lastj = 0;
 #pragma unroll
@@ -474,10 +478,10 @@ __global__ void __launch_bounds__(64) tight_sparse_u32_runs(const uint32_t* __re
     }
     if (r >= n) return;
     const uint32_t s = nodes[r];
-    uint32_t* out = PRED + (size_t)r * ldp + b * TB;
+    uint32_t* out = PRED + (size_t)r * ldp + b * TBR;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        const uint32_t t = b * TB + i;
+    for (uint32_t i = 0; i < TBR; ++i) {
+        const uint32_t t = b * TBR + i;
         uint32_t v = St[i][lane];
         if (t >= V || t == s || d[i] == KeyOps<uint32_t>::INF) v = PRED_NONE;
         out[i] = v;
