@@ -978,7 +978,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
                 if (runs) {
-                    constexpr uint32_t TBR = 16;
+                    constexpr uint32_t TBR = 8;
                     const uint32_t nbR = NT / TBR;
                     tight_sparse_u32_runs<TBR><<<8u * nbR * ((nbS + 7) / 8), 64, 0, st>>>(
                         (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbR, nbS, roff, ent_ro,
