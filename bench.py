@@ -58,8 +58,10 @@ def cpu_baseline(edges, target_s, threads):
 
 
 def load_traffic(kernel_substr):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
-    p = os.path.join(ROOT, "profiles", "fw_pmc_latest.json")
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (profiles/fw_pmc_latest.json for the FW tile, profiles/sparse_pmc_latest.json for k_sparse_bf)."""
+    name = "sparse_pmc_latest.json" if "sparse" in kernel_substr else "fw_pmc_latest.json"
+    p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:
             d = json.load(f)
@@ -180,6 +182,8 @@ def main():
                     help="atlas = C3 (headline), ba = C4, events = C5 stretch (10^7 packet events)")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
+    ap.add_argument("--sparse-group", type=int, default=None, help="sparse: label rows in flight per wave (4/8)")
+    ap.add_argument("--sparse-wgs", type=int, default=None, help="sparse: resident batches per CU (1/2)")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--fw-packed", type=int, default=1, help="u32 FW tiles: 1 = packed-pair adds, 0 = add + min3")
@@ -239,6 +243,10 @@ def main():
     if args.fw_tile:
         router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
     router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
+    if args.sparse_group is not None:
+        router.set_option(N.SRG_OPT_SPARSE_GROUP, args.sparse_group)
+    if args.sparse_wgs is not None:
+        router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
     if args.scan_variant is not None:
         router.set_option(N.SRG_OPT_SCAN_VARIANT, args.scan_variant)
     if args.simulate_rank:
@@ -289,10 +297,13 @@ def main():
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         srcs = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = load_traffic("k_sparse_bf")
         roofline = {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford)",
                     "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                    "frac": round(achieved / 8000.0, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 3),
-                    "bytes_per_source": per_src, "sources_per_launch": int(srcs)}
+                    "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
+                    "bytes_per_source": per_src, "sources_per_launch": int(srcs), "traffic_source": tsrc,
+                    # measured HBM bytes per launch over this run's launch time: the real HBM rate
+                    "traffic_GBps": round(traffic / (avg_ms * 1e-3) / 1e9, 1) if traffic else None}
     elif agg.get("prof_launches"):
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         relax = agg["prof_relaxations"] / agg["prof_launches"]

@@ -124,6 +124,8 @@ void srg_destroy(srg_ctx* ctx);
                                      packed key pairs + v_min3; 0 = one add per relaxation */
 #define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 2 (default) = entries grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches broadcast with
                                      v_readlane */
+#define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
+#define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

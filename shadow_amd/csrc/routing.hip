@@ -401,6 +401,8 @@ struct srg_ctx {
     bool gather_output = true;       // multi-rank: every rank ends with all n x n outputs
     int algorithm = SRG_ALGO_AUTO;   // dense FW / sparse batched Bellman-Ford
     bool sparse_locality = true;     // sparse: batch sources in BFS order
+    int sparse_group = 8;            // sparse: label rows in flight per wave (4, 8)
+    int sparse_wgs_per_cu = 2;       // sparse: resident batches (workgroups) per CU
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
     int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default)
@@ -1204,12 +1206,15 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
 
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * 2));
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)c.sparse_wgs_per_cu));
     const size_t lds = ((size_t)(V + 63) / 64) * 4 * 8 + sp_scratch_bytes();
     if (nbatch) {
         if (lds > 160 * 1024) fail(SRG_ERR_INTERNAL, "sparse path: flag bitmaps exceed LDS (V too large)");
         unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
-        set_lds(k_sparse_bf, lds);
+        // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
+        // registers); 4 ties with 8 at 2 workgroups per CU
+        auto kern = c.sparse_group == 4 ? k_sparse_bf<4> : k_sparse_bf<SP_G>;
+        set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
                      P.selflat, P.selfloss, out_lat, out_loss, fl};
         if (c.profiling) {
@@ -1220,7 +1225,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
             }
             HIP_CHECK(hipEventRecord(c.prof_events[0], st));
         }
-        k_sparse_bf<<<grid, SP_THREADS, lds, st>>>(a);
+        kern<<<grid, SP_THREADS, lds, st>>>(a);
         HIP_CHECK(hipGetLastError());
         if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
     }
@@ -1587,6 +1592,14 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SCAN_VARIANT:
             if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_GROUP:
+            if (value != 4 && value != 8) return SRG_ERR_ARG;
+            ctx->sparse_group = (int)value;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_WGS_PER_CU:
+            if (value != 1 && value != 2) return SRG_ERR_ARG;
+            ctx->sparse_wgs_per_cu = (int)value;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

@@ -34,7 +34,7 @@ constexpr unsigned long long LBL_INF = ~0ull;
 constexpr int SP_WAVES = 16;           // waves per workgroup (1024 threads)
 constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_CAP = 128;            // active-arc list entries per wave
-constexpr int SP_G = 8;                // label rows in flight per wave
+constexpr int SP_G = 8;                // label rows in flight per wave (default; SRG_OPT_SPARSE_GROUP)
 constexpr size_t sp_scratch_bytes() {
     return (size_t)SP_WAVES * (128 + 4 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 4 * SP_CAP) * 4
                                                                    : (size_t)64 * 65 * 8;
@@ -131,6 +131,7 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
 // pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
 // sweep (the out-neighbours of changed vertices, pushed when a vertex changes).  A sweep
 // only visits marked vertices, 64 per wave step (one bitmap word pair).
+template <int G>
 __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
@@ -225,16 +226,16 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                 uint32_t n = 0;
                 unsigned long long changed = 0;  // window vertices whose label dropped
                 auto process = [&](uint32_t cnt) {
-                    // (3) consume the list in groups of SP_G rows, all loads of a group in flight
+                    // (3) consume the list in groups of G rows, all loads of a group in flight
                     int cur = -1;
                     unsigned long long best = 0, old = 0;
-                    for (uint32_t j0 = 0; j0 < cnt; j0 += SP_G) {
-                        unsigned long long row[SP_G];
+                    for (uint32_t j0 = 0; j0 < cnt; j0 += G) {
+                        unsigned long long row[G];
 #pragma unroll
-                        for (int q = 0; q < SP_G; ++q)
+                        for (int q = 0; q < G; ++q)
                             if (j0 + q < cnt) row[q] = ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]);
 #pragma unroll
-                        for (int q = 0; q < SP_G; ++q) {
+                        for (int q = 0; q < G; ++q) {
                             const uint32_t e = j0 + q;
                             if (e >= cnt) break;
                             const uint32_t tag = w_vi[e];

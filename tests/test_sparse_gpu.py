@@ -53,6 +53,19 @@ def test_bf_random_vs_oracle(bf_router, kw):
     assert bits_equal(t.packet_loss, loss)
 
 
+@pytest.mark.parametrize("group,wgs", [(4, 2), (4, 1), (8, 1)])
+def test_bf_launch_variants(bf_router, group, wgs):
+    """Every selectable rows-in-flight / workgroups-per-CU variant is bit-exact too."""
+    bf_router.set_option(N.SRG_OPT_SPARSE_GROUP, group)
+    bf_router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, wgs)
+    g = synth.random_graph(1000, 0.01, 207, lat_hi=100, parallel=0.1)
+    nodes = list(range(1000))
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
 def test_bf_subset_scrambled(bf_router):
     g = synth.random_graph(400, 0.02, 208, lat_hi=60)
     nodes = np.random.default_rng(3).permutation(400)[:130].tolist()

@@ -1,0 +1,47 @@
+"""Per-launch PMC averages of the sparse kernel k_sparse_bf from a tools/pmc_sparse.sh output
+directory -> profiles/sparse_pmc_latest.json (read by bench.py --graph ba).
+
+usage: python tools/pmc_extract_sparse.py PMC_DIR SOURCE_TEXT
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB and on gfx950
+FETCH_SIZE counts half the bytes of wide coalesced reads, so hbm = 2*FETCH + WRITE (an upper
+estimate for the sparse kernel, whose label reads are 512-byte wave rows but whose CSR reads are
+partly narrow).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    d, source = sys.argv[1], sys.argv[2]
+    acc = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_sparse_bf" not in r["Kernel_Name"]:
+                continue
+            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    avg = {c: sum(v) / len(v) for c, v in acc.items()}
+    fetch, write = avg.get("FETCH_SIZE", 0.0), avg.get("WRITE_SIZE", 0.0)
+    out = {"source": source, "kernel": "srg::k_sparse_bf(srg::SparseArgs)",
+           "launches_averaged": len(acc.get("FETCH_SIZE", [])),
+           "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
+           "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
+           "hbm_bytes_per_launch_low": int((fetch + write) * 1024),
+           "note": "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB->B, gfx950 half-count correction); "
+                   "_low = FETCH_SIZE + WRITE_SIZE without the correction"}
+    for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+              "SQ_WAIT_INST_ANY", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+        if c in avg:
+            out[c] = avg[c]
+    p = os.path.join(ROOT, "profiles", "sparse_pmc_latest.json")
+    json.dump(out, open(p, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
