@@ -126,6 +126,8 @@ void srg_destroy(srg_ctx* ctx);
                                      v_readlane */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
+#define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
+                                        0 = a single bucket (plain Bellman-Ford); default 2 */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

@@ -120,6 +120,7 @@ struct SparseArgs {
     uint64_t* out_lat;           // [rows][ncols]
     float* out_loss;
     uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2] total evaluations (lo)
+    uint32_t delta;              // bucket width in ns (0xFFFFFFFF = one bucket: plain Bellman-Ford)
 };
 
 __device__ __forceinline__ unsigned long long ld_label(const unsigned long long* p) {
@@ -140,11 +141,12 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     unsigned long long* fcur = fprev + nw;
     unsigned long long* mark = fcur + nw;
     unsigned long long* mnext = mark + nw;
-    __shared__ uint32_t s_batch, s_changed;
+    unsigned long long* pend = mnext + nw;  // changed, but above the bucket bound: not pushed yet
+    __shared__ uint32_t s_batch, s_changed, s_pend;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (4 x SP_CAP);
     // the output transpose tile [64][65] u64 reuses the same region after convergence
-    uint32_t* scratch = reinterpret_cast<uint32_t*>(mnext + nw);
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(pend + nw);
     uint32_t* w_st = scratch + wave * (128 + 4 * SP_CAP);
     uint32_t* w_lo = w_st + 64;
     uint32_t* w_u = w_lo + 64;
@@ -179,7 +181,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
             fcur[w] = 0;
             mark[w] = 0;
             mnext[w] = 0;
+            pend[w] = 0;
         }
+        if (threadIdx.x == 0) s_pend = 0;
+        // bucket bound (delta-stepping): a changed vertex is pushed to its out-neighbours only
+        // once some lane's new latency is below the bound; the others wait in `pend` until the
+        // bucket is exhausted and the bound moves on.  Any push order reaches the same unique
+        // lexicographic fixpoint; the order only changes the work.
+        uint32_t bound = a.delta;
         __syncthreads();
         if (wave == 0) atomicOr(&fprev[my_src >> 6], 1ull << (my_src & 63));
         for (uint32_t q = wave; q < 64; q += SP_WAVES) {
@@ -224,7 +233,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                 //     ones (source vertex changed last sweep), grouped by target vertex, each
                 //     group led by the vertex's own row (w_vi high bit set)
                 uint32_t n = 0;
-                unsigned long long changed = 0;  // window vertices whose label dropped
+                unsigned long long changed = 0;  // window vertices whose label dropped (pushed now)
+                unsigned long long deferred = 0; // ... whose new label is above the bound
                 auto process = [&](uint32_t cnt) {
                     // (3) consume the list in groups of G rows, all loads of a group in flight
                     int cur = -1;
@@ -242,7 +252,10 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                             if (tag & 0x80000000u) {  // a new vertex: its current label
                                 if (cur >= 0 && __ballot(best < old)) {
                                     if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
-                                    changed |= 1ull << cur;
+                                    if (__ballot(best < old && (uint32_t)(best >> 32) < bound))
+                                        changed |= 1ull << cur;
+                                    else
+                                        deferred |= 1ull << cur;
                                 }
                                 cur = (int)(tag & 63u);
                                 old = best = row[q];
@@ -256,7 +269,10 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                     }
                     if (cur >= 0 && __ballot(best < old)) {
                         if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
-                        changed |= 1ull << cur;
+                        if (__ballot(best < old && (uint32_t)(best >> 32) < bound))
+                            changed |= 1ull << cur;
+                        else
+                            deferred |= 1ull << cur;
                     }
                 };
                 for (uint32_t f0 = 0; f0 < total; f0 += 64) {
@@ -316,6 +332,12 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                     }
                 }
                 if (n) process(n);
+                if ((deferred | changed) && lane == 0) {
+                    // this wave owns window w for the sweep: a vertex pushed now leaves `pend`
+                    const unsigned long long p = (pend[w] | deferred) & ~changed;
+                    pend[w] = p;
+                    if (p) s_pend = 1;
+                }
                 // (4) mark the out-neighbours of the changed vertices for the next sweep
                 if (changed) {
                     if (lane == 0) atomicOr(&fcur[w], changed);
@@ -366,7 +388,34 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                 mnext[w] = 0;
             }
             __syncthreads();
-            if (!more) break;
+            if (!more) {
+                if (!s_pend) break;
+                // bucket exhausted: release every deferred vertex (pushed as if it had just
+                // changed) and move the bound on.  Releasing only those below the new bound was
+                // measured slower on C4 (more, emptier sweeps).
+                __syncthreads();  // every thread has read s_pend
+                bound = bound > 0xFFFFFFFFu - a.delta ? 0xFFFFFFFFu : bound + a.delta;
+                for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+                    fprev[w] = pend[w];
+                    pend[w] = 0;
+                }
+                __syncthreads();
+                if (threadIdx.x == 0) s_pend = 0;
+                for (uint32_t w = wave; w < nw; w += SP_WAVES) {
+                    unsigned long long mk = fprev[w];
+                    while (mk) {
+                        const uint32_t b = (uint32_t)__builtin_ctzll(mk);
+                        mk &= mk - 1;
+                        push_out(w * 64 + b);
+                    }
+                }
+                __syncthreads();
+                for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+                    mark[w] = mnext[w];
+                    mnext[w] = 0;
+                }
+                __syncthreads();
+            }
         }
         max_sweeps = sweeps > max_sweeps ? sweeps : max_sweeps;
         // ---- output rows: 64 targets x 64 sources tiles transposed through LDS ----

@@ -66,6 +66,32 @@ def test_bf_launch_variants(bf_router, group, wgs):
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
 
 
+@pytest.mark.parametrize("div", [1, 4, 16, 1000])
+@pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], dict(V=1000, density=0.01, seed=207, lat_hi=100, parallel=0.1)],
+                         ids=lambda k: f"V{k['V']}_s{k['seed']}")
+def test_bf_delta_buckets(bf_router, kw, div):
+    """Delta-stepping buckets (deferred pushes) reach the same fixpoint bit for bit."""
+    bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, div)
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    nodes = list(range(V))
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
+def test_bf_delta_ba_sampled(bf_router):
+    e = synth.barabasi_albert(3000, 4, seed=31)
+    bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, 8)
+    nodes = list(range(3000))
+    t = bf_router.compute_shortest_paths(e, nodes)
+    rows = np.random.default_rng(31).choice(3000, 16, replace=False).tolist()
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, nthreads=16)
+    assert np.array_equal(t.latency_ns[rows], lat) and bits_equal(t.packet_loss[rows], loss)
+
+
 def test_bf_subset_scrambled(bf_router):
     g = synth.random_graph(400, 0.02, 208, lat_hi=60)
     nodes = np.random.default_rng(3).permutation(400)[:130].tolist()
