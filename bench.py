@@ -302,7 +302,7 @@ def main():
         srcs = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
         traffic, tsrc = load_traffic("k_sparse_bf")
-        roofline = {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford)",
+        roofline = {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford, delta-stepping buckets)",
                     "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                     "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
                     "bytes_per_source": per_src, "sources_per_launch": int(srcs), "traffic_source": tsrc,
