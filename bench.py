@@ -186,6 +186,7 @@ def main():
     ap.add_argument("--sparse-wgs", type=int, default=None, help="sparse: resident batches per CU (1/2)")
     ap.add_argument("--sparse-delta-div", type=int, default=None,
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
+    ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--fw-packed", type=int, default=1, help="u32 FW tiles: 1 = packed-pair adds, 0 = add + min3")
@@ -247,6 +248,8 @@ def main():
     router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
     if args.sparse_group is not None:
         router.set_option(N.SRG_OPT_SPARSE_GROUP, args.sparse_group)
+    if args.sparse_delta_all is not None:
+        router.set_option(N.SRG_OPT_SPARSE_DELTA_ALL, args.sparse_delta_all)
     if args.sparse_delta_div is not None:
         router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, args.sparse_delta_div)
     if args.sparse_wgs is not None:

@@ -127,7 +127,9 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
-                                        0 = a single bucket (plain Bellman-Ford); default 2 */
+                                        0 = a single bucket (plain Bellman-Ford); default 1 */
+#define SRG_OPT_SPARSE_DELTA_ALL 13  /* sparse: 1 = a dropped vertex is pushed only when every dropped lane is
+                                        below the bucket bound, 0 (default) = when any is */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

@@ -403,7 +403,8 @@ struct srg_ctx {
     bool sparse_locality = true;     // sparse: batch sources in BFS order
     int sparse_group = 8;            // sparse: label rows in flight per wave (4, 8)
     int sparse_wgs_per_cu = 2;       // sparse: resident batches (workgroups) per CU
-    int sparse_delta_div = 2;        // sparse: bucket width = max edge latency / this (0 = plain BF)
+    bool sparse_delta_all = false;   // sparse: bucket test over every dropped lane (else any lane)
+    int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
     int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default)
@@ -1217,10 +1218,11 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         auto kern = c.sparse_group == 4 ? k_sparse_bf<4> : k_sparse_bf<SP_G>;
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
-                     P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu};
+                     P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.es.max_lat / (unsigned long long)c.sparse_delta_div);
+        a.all_lanes = c.sparse_delta_all ? 1u : 0u;
         if (c.profiling) {
             while (c.prof_events.size() < 2) {
                 hipEvent_t e;
@@ -1608,6 +1610,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SPARSE_DELTA_DIV:
             if (!(value >= 0.0 && value <= 1e6)) return SRG_ERR_ARG;
             ctx->sparse_delta_div = (int)value;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_DELTA_ALL:
+            ctx->sparse_delta_all = value != 0.0;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

@@ -121,7 +121,14 @@ struct SparseArgs {
     float* out_loss;
     uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2] total evaluations (lo)
     uint32_t delta;              // bucket width in ns (0xFFFFFFFF = one bucket: plain Bellman-Ford)
+    uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
 };
+
+// a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
+// (all_lanes = 1) dropped lane's new latency is below the bucket bound
+__device__ __forceinline__ bool bucket_ready(bool dropped, bool below, uint32_t all_lanes) {
+    return all_lanes ? __ballot(dropped && !below) == 0 : __ballot(dropped && below) != 0;
+}
 
 __device__ __forceinline__ unsigned long long ld_label(const unsigned long long* p) {
     // L1-bypassing load: rows written by other waves of this workgroup in the previous sweep
@@ -252,7 +259,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                             if (tag & 0x80000000u) {  // a new vertex: its current label
                                 if (cur >= 0 && __ballot(best < old)) {
                                     if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
-                                    if (__ballot(best < old && (uint32_t)(best >> 32) < bound))
+                                    if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
                                         changed |= 1ull << cur;
                                     else
                                         deferred |= 1ull << cur;
@@ -269,7 +276,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                     }
                     if (cur >= 0 && __ballot(best < old)) {
                         if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
-                        if (__ballot(best < old && (uint32_t)(best >> 32) < bound))
+                        if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
                             changed |= 1ull << cur;
                         else
                             deferred |= 1ull << cur;

@@ -66,12 +66,14 @@ def test_bf_launch_variants(bf_router, group, wgs):
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
 
 
+@pytest.mark.parametrize("all_lanes", [0, 1])
 @pytest.mark.parametrize("div", [1, 4, 16, 1000])
 @pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], dict(V=1000, density=0.01, seed=207, lat_hi=100, parallel=0.1)],
                          ids=lambda k: f"V{k['V']}_s{k['seed']}")
-def test_bf_delta_buckets(bf_router, kw, div):
+def test_bf_delta_buckets(bf_router, kw, div, all_lanes):
     """Delta-stepping buckets (deferred pushes) reach the same fixpoint bit for bit."""
     bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, div)
+    bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_ALL, all_lanes)
     kw = dict(kw)
     V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
     g = synth.random_graph(V, dens, seed, **kw)
