@@ -180,6 +180,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--graph", choices=["atlas", "ba", "events"], default="atlas",
                     help="atlas = C3 (headline), ba = C4, events = C5 stretch (10^7 packet events)")
+    ap.add_argument("--entry", choices=["host", "device"], default="device",
+                    help="host = srg_compute_shortest_paths (host edge list in, host table out: H2D + D2H "
+                         "included); device = srg_compute_shortest_paths_device (inputs/outputs in HBM)")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
     ap.add_argument("--sparse-group", type=int, default=None, help="sparse: label rows in flight per wave (4/8)")
@@ -260,8 +263,19 @@ def main():
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)
 
-    def step():
-        return compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
+    if args.entry == "host":
+        import numpy as np
+        h_nodes = np.arange(V, dtype=np.uint32)
+        h_lat = np.empty((V, V), dtype=np.uint64)
+        h_loss = np.empty((V, V), dtype=np.float32)
+        h_lat.fill(0)  # fault the pages in once: the caller's Vecs are already allocated
+        h_loss.fill(0)
+
+        def step():
+            return router.compute_shortest_paths(edges, h_nodes, h_lat, h_loss).stats
+    else:
+        def step():
+            return compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
 
     for i in range(args.warmup):
         s = step()
@@ -340,7 +354,7 @@ def main():
         print(json.dumps({"diagnostic": "simulated rank (collectives elided, outputs invalid)",
                           "simulate_rank": args.simulate_rank, "ms_per_step": round(ms_per_step, 3),
                           "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in
-                                           ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange")},
+                                           ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")},
                           "roofline": roofline}), flush=True)
         return
     if rank == 0:
@@ -357,7 +371,7 @@ def main():
                        **({"fallback": fallback} if fallback else {}),
                        "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
             "apsp_wall_ms": round(ms_per_step, 3),
-            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange")},
+            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")},
             "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
             "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
             "roofline": roofline, "cpu_baseline": cpu,

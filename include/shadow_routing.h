@@ -87,6 +87,10 @@ typedef struct srg_stats {
     int32_t nranks;             /* ranks in the communicator (1 = single GPU) */
     int32_t rank;               /* this rank */
     uint64_t local_sources;     /* used sources routed by this rank */
+    /* host entry: the caller's output arrays are page-locked concurrently with H2D + FW, then
+     * finished rows leave while later kernels run; ms_d2h above is only the exposed tail.   */
+    double ms_host_register;    /* page-locking time (hidden; -1 = not used / failed)      */
+    uint64_t d2h_overlapped_bytes; /* output bytes copied to the host while kernels ran    */
 } srg_stats;
 
 #define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */

@@ -195,6 +195,69 @@ void dijkstra_dense(const Graph& g, uint32_t start, std::vector<PP>& score, std:
     }
 }
 
+// Dense-matrix Dijkstra for complete / near-complete graphs (mode 2, a fast CHECKER for the
+// full-size configs).  Parallel edges are collapsed to their lexicographic-min (latency, loss)
+// -- PathProperties ordering, mod.rs:305-313 -- which cannot change any score: the fold
+// 1-(1-L)(1-p) is monotone in p.  Each step finalises the unvisited vertex with the
+// lexicographically smallest score (linear scan, no heap), then relaxes its row with the
+// same strict-< rule as petgraph.  The lexicographic score of every vertex is the unique
+// fixpoint lexmin over its latency-tight predecessors (positive latencies), so this equals
+// the heap Dijkstra bit for bit; tests/test_oracle.py pins mode 2 against mode 1.
+struct DenseW {
+    uint32_t V = 0;
+    std::vector<uint64_t> lat;   // UINT64_MAX = no edge
+    std::vector<float> loss;
+    void build(const Graph& g) {
+        V = g.V;
+        lat.assign((size_t)V * V, UINT64_MAX);
+        loss.assign((size_t)V * V, 0.0f);
+        auto put = [&](uint32_t a, uint32_t b, const PP& w) {
+            const size_t k = (size_t)a * V + b;
+            if (lat[k] == UINT64_MAX || pp_less(w, PP{lat[k], loss[k]})) {
+                lat[k] = w.lat;
+                loss[k] = w.loss;
+            }
+        };
+        for (size_t e = 0; e < g.esrc.size(); ++e) {
+            const uint32_t s = g.esrc[e], t = g.edst[e];
+            if (s == t) continue;  // a self-loop never improves a score (positive latency)
+            put(s, t, g.ew[e]);
+            if (!g.directed) put(t, s, g.ew[e]);
+        }
+    }
+};
+
+void dijkstra_matrix(const DenseW& w, uint32_t start, std::vector<PP>& score, std::vector<uint8_t>& seen,
+                     std::vector<uint8_t>& visited) {
+    const uint32_t V = w.V;
+    score.assign(V, PP{UINT64_MAX, 1.0f});
+    seen.assign(V, 0);
+    visited.assign(V, 0);
+    score[start] = PP{0, 0.0f};
+    seen[start] = 1;
+    for (;;) {
+        uint32_t best = UINT32_MAX;
+        for (uint32_t v = 0; v < V; ++v)
+            if (seen[v] && !visited[v] && (best == UINT32_MAX || pp_less(score[v], score[best]))) best = v;
+        if (best == UINT32_MAX) break;
+        visited[best] = 1;
+        const PP sb = score[best];
+        const uint64_t* lrow = &w.lat[(size_t)best * V];
+        const float* prow = &w.loss[(size_t)best * V];
+        for (uint32_t t = 0; t < V; ++t) {
+            if (lrow[t] == UINT64_MAX || visited[t]) continue;
+            // PathProperties::add without volatile: -ffp-contract=off + SSE round every op
+            const float x = 1.0f - sb.loss, y = 1.0f - prow[t];
+            const float prod = x * y;
+            const PP ns{sb.lat + lrow[t], 1.0f - prod};
+            if (!seen[t] || pp_less(ns, score[t])) {
+                score[t] = ns;
+                seen[t] = 1;
+            }
+        }
+    }
+}
+
 void set_err(char* buf, size_t len, const std::string& m) {
     if (buf && len) {
         std::snprintf(buf, len, "%s", m.c_str());
@@ -252,6 +315,7 @@ extern "C" {
 //   mode 0: reference-equivalent plumbing: HashMap scores, linear `nodes.contains` filter,
 //           per-source HashMap, one merged HashMap (rayon collect), then dense copy-out.
 //   mode 1: same Dijkstra semantics with dense scores and O(1) membership (fast checker).
+//   mode 2: dense-matrix Dijkstra (dijkstra_matrix; checker for complete graphs, O(V^2)/source).
 // rows/num_rows: if rows != NULL only those source POSITIONS are computed and out_* is
 //           [num_rows x n]; the error checks that need all rows (n^2) are then per-row.
 // Returns 0 or SRG-style codes (2 no edge, 3 multi edge, 4 unreachable, 1 arg).
@@ -317,6 +381,22 @@ int oracle_compute_shortest_paths(uint32_t V, int directed, uint64_t E, const ui
                 }
             }
         }
+    } else if (mode == 2) {
+        DenseW w;
+        w.build(g);
+        parallel_for(R, nthreads, [&](uint32_t r) {
+            std::vector<PP> score;
+            std::vector<uint8_t> seen, visited;
+            dijkstra_matrix(w, nodes[row_pos[r]], score, seen, visited);
+            for (uint32_t j = 0; j < n; ++j) {
+                uint32_t t = nodes[j];
+                if (seen[t]) {
+                    out_lat[(size_t)r * n + j] = score[t].lat;
+                    out_loss[(size_t)r * n + j] = score[t].loss;
+                    filled[(size_t)r * n + j] = 1;
+                }
+            }
+        });
     } else {
         parallel_for(R, nthreads, [&](uint32_t r) {
             std::vector<PP> score;

@@ -120,6 +120,8 @@ class Stats(ctypes.Structure):
         ("nranks", ctypes.c_int32),
         ("rank", ctypes.c_int32),
         ("local_sources", ctypes.c_uint64),
+        ("ms_host_register", ctypes.c_double),
+        ("d2h_overlapped_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):

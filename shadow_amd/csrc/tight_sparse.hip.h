@@ -546,13 +546,13 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
                                                      const float* __restrict__ self_loss,
                                                      const uint32_t* __restrict__ cols, uint32_t ncols,
                                                      const uint32_t* __restrict__ rowpos, float* __restrict__ out_loss,
-                                                     uint32_t* __restrict__ max_sweeps) {
+                                                     uint32_t* __restrict__ max_sweeps, uint32_t row0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     uint32_t* U = reinterpret_cast<uint32_t*>(smem_raw);
     float* Bf = reinterpret_cast<float*>(U + V);
     float* L = Bf + V;
     __shared__ uint32_t changed;
-    const uint32_t r = blockIdx.x;
+    const uint32_t r = row0 + blockIdx.x;  // launched in row chunks (host entry: D2H per chunk)
     const uint32_t s = nodes[r];
     const uint32_t* prow = PRED + (size_t)r * ldp;
     for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) {

@@ -169,11 +169,15 @@ class Router:
         except Exception:
             pass
 
-    def _run(self, fn, edges, nodes):
+    def _run(self, fn, edges, nodes, out_lat=None, out_loss=None):
         nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
         n = len(nodes)
-        out_lat = np.zeros((n, n), dtype=np.uint64)
-        out_loss = np.zeros((n, n), dtype=np.float32)
+        if out_lat is None:
+            out_lat = np.zeros((n, n), dtype=np.uint64)
+        if out_loss is None:
+            out_loss = np.zeros((n, n), dtype=np.float32)
+        assert out_lat.dtype == np.uint64 and out_lat.size == n * n and out_lat.flags.c_contiguous
+        assert out_loss.dtype == np.float32 and out_loss.size == n * n and out_loss.flags.c_contiguous
         st = N.Stats()
         err = ctypes.create_string_buffer(1024)
         el = edges.as_struct()
@@ -183,8 +187,10 @@ class Router:
             _raise(rc, err.value.decode(errors="replace"))
         return PathTable(nodes, out_lat, out_loss, st.as_dict())
 
-    def compute_shortest_paths(self, edges, nodes):
-        return self._run(N.lib().srg_compute_shortest_paths, edges, nodes)
+    def compute_shortest_paths(self, edges, nodes, out_lat=None, out_loss=None):
+        """Host entry (srg_compute_shortest_paths): host edge list in, host n x n table out.
+        out_lat (u64) / out_loss (f32) may be caller-provided n x n arrays (reused buffers)."""
+        return self._run(N.lib().srg_compute_shortest_paths, edges, nodes, out_lat, out_loss)
 
     # ---- multi-GPU (include/shadow_routing.h srg_comm_*) ----------------------------------
     @staticmethod

@@ -138,3 +138,15 @@ def test_gpu_events_errors(gpu_router):
     b["dst_host"][4] = 9
     with pytest.raises(Exception):
         ev.order_packet_events(gpu_router, b, table, 9, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_gpu_events_c5_full_size(gpu_router):
+    """Config C5 at full size: the bench's 10^7-event round (synthetic_round(1e7, 10 000 hosts,
+    seed 7)) against a 10k x 10k routing table, every output compared with the oracle."""
+    n, H = 10**7, 10000
+    b, re = ev.synthetic_round(n, H, H, seed=7)
+    table = np.random.default_rng(7).integers(10**6, 10**8, (H, H), dtype=np.uint64)
+    res = check(gpu_router, b, table, H, re)
+    assert res["key_bits"] > 0

@@ -49,10 +49,32 @@ def test_oracle_golden(fx):
         assert ei.value.code == fx["expect_code"]
         return
     lat, loss = fixture_expect(fx)
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         ol, of = oracle.compute_shortest_paths(e.as_tuple(), fx["nodes"], mode=mode)
         assert np.array_equal(ol, lat)
         assert np.array_equal(of.view(np.uint32), loss)
+
+
+@pytest.mark.parametrize("kw", [dict(V=300, density=0.3, seed=5, lat_hi=5, parallel=0.3),
+                                dict(V=257, density=0.1, seed=6, directed=True, lat_hi=1000, loss_hi=1e-6),
+                                dict(V=200, density=1.0, seed=8, lat_hi=3, parallel=0.5)],
+                         ids=["ties_parallel", "directed_tiny_loss", "complete_ties"])
+def test_oracle_matrix_mode_pinned(kw):
+    """mode 2 (dense-matrix Dijkstra, the full-size checker) == mode 1 (petgraph heap Dijkstra)
+    bit for bit on graphs with latency ties, parallel edges and tiny losses."""
+    kw = dict(kw)
+    V, d, s = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, d, s, **kw)
+    nodes = np.random.default_rng(s).permutation(V)[: V - 7].tolist()
+    try:
+        a = oracle.compute_shortest_paths(g.as_tuple(), nodes, mode=1)
+    except oracle.OracleError as e1:
+        with pytest.raises(oracle.OracleError) as e2:
+            oracle.compute_shortest_paths(g.as_tuple(), nodes, mode=2)
+        assert e2.value.code == e1.code
+        return
+    b = oracle.compute_shortest_paths(g.as_tuple(), nodes, mode=2)
+    assert np.array_equal(a[0], b[0]) and bits_equal(a[1], b[1])
 
 
 def test_oracle_rows_subset_matches_full():

@@ -139,6 +139,54 @@ def test_ba_auto_sparse_sampled(V):
     r.close()
 
 
+@pytest.mark.slow
+def test_c4_full_size_sampled_rows():
+    """Config C4 at full size (barabasi_albert(50000, 4, seed=50000), all 50 000 nodes used; the
+    2.5e9-pair table stays in HBM) through the device entry: 64 seeded oracle rows bit-exact,
+    plus whole-table properties computed on the device: diagonal = the self-loops, symmetric
+    latency, latency <= the direct edge on every arc, the Bellman inequality
+    D[s][t] <= D[s][u] + w(u,t) over every source for 256 sampled arcs, loss in [0, 1]."""
+    import torch
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+    V = 50000
+    dev = torch.device("cuda", 0)
+    e = synth.barabasi_albert(V, 4, seed=V)
+    dg = DeviceGraph(e)
+    nodes_t = torch.arange(V, dtype=torch.int32, device=dev)
+    ol = torch.empty((V, V), dtype=torch.int64, device=dev)
+    os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
+    r = Router(0)
+    st = compute_shortest_paths_device(r, dg, nodes_t, ol, os_)
+    torch.cuda.synchronize()
+    assert st["path_kind"] == N.SRG_PATH_SPARSE_U32
+    rows = np.random.default_rng(V).choice(V, 64, replace=False)
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), list(range(V)), rows=rows.tolist(), nthreads=16)
+    ri = torch.from_numpy(rows.astype(np.int64)).to(dev)
+    assert np.array_equal(ol[ri].cpu().numpy().view(np.uint64), lat)
+    assert bits_equal(os_[ri].cpu().numpy(), loss)
+    idx = torch.arange(V, device=dev)
+    assert bool((ol[idx, idx] == 1_000_000).all())
+    B = 4096
+    for i0 in range(0, V, B):
+        i1 = min(V, i0 + B)
+        assert torch.equal(ol[i0:i1], ol[:, i0:i1].t().contiguous()), f"latency not symmetric in rows {i0}:{i1}"
+    m = e.src != e.dst
+    s_ = torch.from_numpy(e.src[m].astype(np.int64)).to(dev)
+    t_ = torch.from_numpy(e.dst[m].astype(np.int64)).to(dev)
+    w_ = torch.from_numpy(e.latency_ns[m].view(np.int64)).to(dev)
+    assert bool((ol[s_, t_] <= w_).all()) and bool((ol[t_, s_] <= w_).all())
+    pick = torch.from_numpy(np.random.default_rng(1).choice(int(m.sum()), 256, replace=False)).to(dev)
+    for k in pick.tolist():
+        u, t, w = int(s_[k]), int(t_[k]), int(w_[k])
+        col_t, col_u = ol[:, t].clone(), ol[:, u].clone()
+        col_t[t] = 0  # the diagonal holds the self-loop, the Bellman inequality uses D[t][t] = 0
+        col_u[u] = 0
+        assert bool((col_t <= col_u + w).all()) and bool((col_u <= col_t + w).all())
+    assert float(os_.min()) >= 0.0 and float(os_.max()) <= 1.0
+    del ol, os_
+    r.close()
+
+
 @pytest.mark.parametrize("G", [2, 3])
 def test_bf_multi_rank(G):
     e = synth.barabasi_albert(2500, 3, seed=77)
