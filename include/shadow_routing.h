@@ -126,14 +126,17 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
 #define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles: 1 (default) = two relaxations per 64-bit add of
                                      packed key pairs + v_min3; 0 = one add per relaxation */
-#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 2 (default) = entries grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches broadcast with
-                                     v_readlane */
+#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 3 = source columns staged in LDS per u-chunk,
+                                     2 (default) = entries grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry
+                                     batches broadcast with v_readlane */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
                                         0 = a single bucket (plain Bellman-Ford); default 1 */
 #define SRG_OPT_SPARSE_DELTA_ALL 13  /* sparse: 1 = a dropped vertex is pushed only when every dropped lane is
                                         below the bucket bound, 0 (default) = when any is */
+#define SRG_OPT_SPARSE_GLOBAL_BITMAPS 14 /* sparse: 1 = keep the per-batch vertex bitmaps in global memory
+                                        (automatic when 5V/8 bytes do not fit the LDS budget) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

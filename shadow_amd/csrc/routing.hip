@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -246,15 +247,17 @@ __global__ void k_init_d(const K* __restrict__ W, K* __restrict__ D, size_t ld) 
     }
 }
 
-// INF anywhere in a used row (u32 certification) -- t < V only
+// INF in a used (row, column) pair (u32 certification).  Only used columns can change an
+// output: a stored key <= INF plus an edge w > 0 never falsely equals a finite D[s][t], so an
+// unreachable UNUSED vertex leaves the u32 result exact.
 template <class K>
-__global__ void k_certify(const K* __restrict__ D, size_t ld, const uint32_t* __restrict__ nodes, uint32_t n,
-                          uint32_t V, Flags* flags) {
-    const size_t total = (size_t)n * V;
+__global__ void k_certify(const K* __restrict__ D, size_t ld, const uint32_t* __restrict__ rows, uint32_t nrows,
+                          const uint32_t* __restrict__ cols, uint32_t ncols, Flags* flags) {
+    const size_t total = (size_t)nrows * ncols;
     uint32_t hit = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / V, t = i - r * V;
-        hit |= D[(size_t)nodes[r] * ld + t] == KeyOps<K>::INF;
+        const size_t r = i / ncols, j = i - r * ncols;
+        hit |= D[(size_t)rows[r] * ld + cols[j]] == KeyOps<K>::INF;
     }
     if (hit) atomicOr(&flags->inf_in_used_row, 1u);
 }
@@ -406,9 +409,10 @@ struct srg_ctx {
     int sparse_wgs_per_cu = 2;       // sparse: resident batches (workgroups) per CU
     bool sparse_delta_all = false;   // sparse: bucket test over every dropped lane (else any lane)
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
+    bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
-    int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default)
+    int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default), 3 = LDS-staged u-chunks
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -895,9 +899,17 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
 
     // u32 certification: no saturated key in any used row (every rank must agree)
     HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
-    if (nloc) k_certify<K><<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(D, Vp, lnodes, nloc, V, P.flags);
+    if (nloc) k_certify<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, Vp, lnodes, nloc, nodes, n, P.flags);
     const uint32_t inf_any = reduce_flag(&P.flags->inf_in_used_row);
-    if (sizeof(K) == 4 && inf_any) return false;  // saturated or unreachable: redo in u64
+    if (sizeof(K) == 4 && inf_any) {
+        // a used pair at INF: unreachable -- unless some path could reach 2^31-1 ns, in which case
+        // the u64 keys decide (the u32 FW work is redone)
+        const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (V > 1 ? V - 1 : 1);
+        if (bound >= KeyOps<uint32_t>::INF) return false;
+        fail(SRG_ERR_UNREACHABLE,
+             "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
+             "from another used node)");
+    }
 
     // latency outputs (+ diagonal self-loops) of the own rows, right after FW
     HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
@@ -950,52 +962,85 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         c.comm->allgatherv(ess, offs.data(), lens.data(), cs);
         st_after_cs();
     }
-    const size_t NQ = (size_t)nbT * V;
-    uint32_t* ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
-    uint32_t* eoff = (uint32_t*)c.b_eoff.get(NQ * 4);
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
-    uint32_t* eblk = (uint32_t*)c.b_gblk.get(((size_t)nbT + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    k_ess_count<<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(ess, V, nw64, ecnt, indeg);
-    HIP_CHECK(hipGetLastError());
-    size_t tb0 = 0, tb2 = 0;
-    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ecnt, eoff, (int)NQ, st));
-    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, indeg, cscoff, (int)(nw64 * 64 + 1), st));
-    size_t tbytes = std::max(tb0, tb2);
-    void* tmp = c.b_scantmp.get(tbytes);
-    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ecnt, eoff, (int)NQ, st));
-    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(nw64 * 64 + 1), st));
-    k_ess_blocks<<<1, 1, 0, st>>>(eoff, ecnt, V, nbT, eblk);
-    uint32_t tail[3];
-    HIP_CHECK(hipMemcpyAsync(&tail[0], eoff + NQ - 1, 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&tail[1], ecnt + NQ - 1, 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&tail[2], eblk + nbT, 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    const uint64_t E_ess = (uint64_t)tail[0] + tail[1];
-    const uint64_t E_pad = tail[2];  // padded entry count (blocks rounded up to 64)
-    n_ess = E_ess;
     const size_t npad = ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
-    // run layout (entries grouped by target, SRG_OPT_SCAN_VARIANT 2): run offsets from indeg
-    const bool runs = sizeof(K) == 4 && c.scan_variant == 2;
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
-    uint32_t* roff = nullptr;
-    uint64_t E_runs = 0;
-    if (runs) {
-        uint32_t* rlen = (uint32_t*)c.b_rlen.get(((size_t)NT + 1) * 4);
-        roff = (uint32_t*)c.b_roff.get(((size_t)NT + 1) * 4);
-        k_run_len<<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, V, NT, rlen);
-        size_t tb3 = 0;
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, rlen, roff, (int)(NT + 1), st));
-        void* tmp3 = c.b_scantmp.get(std::max(tb3, tbytes));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp3, tb3, rlen, roff, (int)(NT + 1), st));
-        uint32_t tot = 0;
-        HIP_CHECK(hipMemcpyAsync(&tot, roff + NT, 4, hipMemcpyDeviceToHost, st));
+    // LDS-staged scan (SRG_OPT_SCAN_VARIANT 3, default): entries by (target tile, u-chunk, target)
+    const bool lds = sizeof(K) == 4 && c.scan_variant == 3;
+    const uint32_t nK = (V + LS_UC - 1) / LS_UC, nbTT = (NT + LS_TT - 1) / LS_TT;
+    const size_t NQ3 = (size_t)nbTT * nK * LS_TT;
+    uint32_t *ls_cnt = nullptr, *ls_nr = nullptr, *ls_roff = nullptr;
+    // 32-target blocks (variants 0/1) and target runs (variant 2)
+    const bool runs = sizeof(K) == 4 && c.scan_variant == 2;
+    uint32_t *ecnt = nullptr, *eoff = nullptr, *eblk = nullptr, *roff = nullptr;
+    const size_t NQ = (size_t)nbT * V;
+    uint64_t E_ess = 0, E_layout = 0;
+    size_t tbytes = 0;
+    if (lds) {
+        ls_cnt = (uint32_t*)c.b_ecnt.get(NQ3 * 4);
+        ls_nr = (uint32_t*)c.b_gblk.get(NQ3 * 4);
+        uint32_t* ls_rlen = (uint32_t*)c.b_rlen.get((NQ3 + 1) * 4);
+        ls_roff = (uint32_t*)c.b_eoff.get((NQ3 + 1) * 4);
+        HIP_CHECK(hipMemsetAsync(ls_cnt, 0, NQ3 * 4, st));  // target windows past nw64 stay empty
+        HIP_CHECK(hipMemsetAsync(ls_nr, 0, NQ3 * 4, st));
+        HIP_CHECK(hipMemsetAsync(ls_rlen, 0, (NQ3 + 1) * 4, st));
+        const size_t nwaves = (size_t)nw64 * nK;
+        k_ls_count<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, V, nw64, nK, ls_cnt, ls_nr, ls_rlen,
+                                                                            indeg);
+        HIP_CHECK(hipGetLastError());
+        size_t ta = 0, tc = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, ls_rlen, ls_roff, (int)(NQ3 + 1), st));
+        tbytes = std::max(ta, tc);
+        void* tmp = c.b_scantmp.get(tbytes);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(NT + 1), st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ls_rlen, ls_roff, (int)(NQ3 + 1), st));
+        uint32_t tail[2];
+        HIP_CHECK(hipMemcpyAsync(&tail[0], cscoff + NT, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tail[1], ls_roff + NQ3, 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
-        E_runs = tot;
+        E_ess = tail[0];
+        E_layout = tail[1];
+    } else {
+        ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
+        eoff = (uint32_t*)c.b_eoff.get(NQ * 4);
+        eblk = (uint32_t*)c.b_gblk.get(((size_t)nbT + 1) * 4);
+        k_ess_count<<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(ess, V, nw64, ecnt, indeg);
+        HIP_CHECK(hipGetLastError());
+        size_t tb0 = 0, tb2 = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ecnt, eoff, (int)NQ, st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, indeg, cscoff, (int)(nw64 * 64 + 1), st));
+        tbytes = std::max(tb0, tb2);
+        void* tmp = c.b_scantmp.get(tbytes);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ecnt, eoff, (int)NQ, st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(nw64 * 64 + 1), st));
+        k_ess_blocks<<<1, 1, 0, st>>>(eoff, ecnt, V, nbT, eblk);
+        uint32_t tail[3];
+        HIP_CHECK(hipMemcpyAsync(&tail[0], eoff + NQ - 1, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tail[1], ecnt + NQ - 1, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tail[2], eblk + nbT, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        E_ess = (uint64_t)tail[0] + tail[1];
+        E_layout = tail[2];  // padded entry count (blocks rounded up to 64)
+        // run layout (entries grouped by target, variant 2): run offsets from indeg
+        if (runs) {
+            uint32_t* rlen = (uint32_t*)c.b_rlen.get(((size_t)NT + 1) * 4);
+            roff = (uint32_t*)c.b_roff.get(((size_t)NT + 1) * 4);
+            k_run_len<<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, V, NT, rlen);
+            size_t tb3 = 0;
+            HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, rlen, roff, (int)(NT + 1), st));
+            void* tmp3 = c.b_scantmp.get(std::max(tb3, tbytes));
+            HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp3, tb3, rlen, roff, (int)(NT + 1), st));
+            uint32_t tot = 0;
+            HIP_CHECK(hipMemcpyAsync(&tot, roff + NT, 4, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            E_layout = tot;
+        }
     }
-    const uint64_t E_layout = runs ? E_runs : E_pad;
+    n_ess = E_ess;
     const bool sparse = (double)E_ess <= c.sparse_threshold * (double)V * (double)V &&
                         E_layout + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
     if (sparse) {
@@ -1008,15 +1053,24 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         uint32_t* ent_u = (uint32_t*)c.b_grpe.get(Eb * 4);
         float* ent_b = (float*)c.b_entb.get(Eb * 4);
         uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
-        HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
-        k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
-            ess, W, WL, Vp, V, nw64, std::max<size_t>(npad, 64), eoff, eblk, cscoff, cscfill, ent_ro, ent_w, ent_tl,
-            ent_u, ent_b, cscent, roff);
-        if (runs)
-            k_run_pad<K><<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, roff, V, NT, ent_ro, ent_w, ent_tl,
-                                                                          ent_u, ent_b);
-        else
-            k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
+        if (lds) {
+            if constexpr (sizeof(K) == 4) {
+                const size_t nwaves = (size_t)nw64 * nK;
+                k_ls_fill<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK, ls_cnt,
+                                                                                   ls_roff, cscoff, ent_ro, ent_w,
+                                                                                   ent_u, ent_b, cscent);
+            }
+        } else {
+            HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+            k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
+                ess, W, WL, Vp, V, nw64, std::max<size_t>(npad, 64), eoff, eblk, cscoff, cscfill, ent_ro, ent_w,
+                ent_tl, ent_u, ent_b, cscent, roff);
+            if (runs)
+                k_run_pad<K><<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, roff, V, NT, ent_ro, ent_w,
+                                                                              ent_tl, ent_u, ent_b);
+            else
+                k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
+        }
         HIP_CHECK(hipGetLastError());
         if (nloc) {
             const uint32_t nbS = (uint32_t)(npad / 64);
@@ -1024,7 +1078,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
-                if (runs) {
+                if (lds) {
+                    tight_lds_u32<<<8u * nbTT * ((nbS + 7) / 8), LS_WAVES * 64, 0, st>>>(
+                        (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, (uint32_t)Vp, nbTT, nbS, nK,
+                        ls_nr, ls_roff, ent_ro, (const uint32_t*)ent_w, PRED, Vp);
+                } else if (runs) {
                     constexpr uint32_t TBR = 8;
                     const uint32_t nbR = NT / TBR;
                     tight_sparse_u32_runs<TBR><<<8u * nbR * ((nbS + 7) / 8), 64, 0, st>>>(
@@ -1042,6 +1100,22 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             HIP_CHECK(hipGetLastError());
             k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
             HIP_CHECK(hipGetLastError());
+            if (const char* dbg = std::getenv("SRG_DEBUG_PRED")) {
+                // debugging aid: the tight predecessor VERTEX per (used row, target), -1 none, -2 multi
+                std::vector<uint32_t> pr((size_t)nloc * Vp), eu(E_layout + 256);
+                HIP_CHECK(hipMemcpyAsync(pr.data(), PRED, pr.size() * 4, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(eu.data(), ent_u, eu.size() * 4, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                if (FILE* f = std::fopen(dbg, "wb")) {
+                    for (uint32_t r = 0; r < nloc; ++r)
+                        for (uint32_t t = 0; t < V; ++t) {
+                            const uint32_t p = pr[(size_t)r * Vp + t];
+                            const int32_t u = p == PRED_NONE ? -1 : p == PRED_MULTI ? -2 : (int32_t)eu[p];
+                            std::fwrite(&u, 4, 1, f);
+                        }
+                    std::fclose(f);
+                }
+            }
             ms_scan = tm.lap();
             const size_t lds_rows = (size_t)V * 12;
             if (lds_rows <= 150 * 1024) {
@@ -1260,17 +1334,28 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
 
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)c.sparse_wgs_per_cu));
-    const size_t lds = ((size_t)(V + 63) / 64) * 5 * 8 + sp_scratch_bytes();
+    uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)c.sparse_wgs_per_cu));
+    // label slots (V x 64 x 8 B per resident batch) within about half of the free HBM
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const size_t slot_bytes = (size_t)V * 64 * 8;
+    grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
+    const uint32_t nwv = (V + 63) / 64;
+    const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
+    // bitmaps in LDS while a CU still fits the requested workgroups, else in global memory
+    const bool gbits = c.sparse_global_bitmaps ||
+                       bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / c.sparse_wgs_per_cu;
+    const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
     if (nbatch) {
-        if (lds > 160 * 1024) fail(SRG_ERR_INTERNAL, "sparse path: flag bitmaps exceed LDS (V too large)");
-        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
+        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * slot_bytes);
+        unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
-        auto kern = c.sparse_group == 4 ? k_sparse_bf<4> : k_sparse_bf<SP_G>;
+        auto kern = gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true> : k_sparse_bf<SP_G, true>)
+                          : (c.sparse_group == 4 ? k_sparse_bf<4, false> : k_sparse_bf<SP_G, false>);
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
-                     P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u};
+                     P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.es.max_lat / (unsigned long long)c.sparse_delta_div);
@@ -1288,13 +1373,17 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
     }
     // every rank agrees on the outcome before any exchange
-    if (multi) c.comm->allreduce_max_u32(fl, 2, st);
-    uint32_t hfl[4] = {0, 0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(hfl, fl, 16, hipMemcpyDeviceToHost, st));
+    if (multi) {
+        c.comm->allreduce_max_u32(fl, 2, st);
+        c.comm->allreduce_max_u32(fl + 5, 1, st);
+    }
+    uint32_t hfl[6] = {0, 0, 0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(hfl, fl, 24, hipMemcpyDeviceToHost, st));
     const double ms_sssp = tm.lap();
     if (hfl[0]) {
-        const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (V > 1 ? V - 1 : 1);
-        if (bound >= 0xFFFFFFFFull) return false;  // maybe saturated: decide on the u64 path
+        // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
+        // finite (>= 2^32-1 ns) path; otherwise the pair is unreachable -- the reference's panic
+        if (hfl[5]) return false;  // decide on the u64 path
         fail(SRG_ERR_UNREACHABLE,
              "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
              "from another used node)");
@@ -1701,7 +1790,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = value != 0.0;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
+            if (value != 0 && value != 1 && value != 2 && value != 3) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
@@ -1718,6 +1807,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_SPARSE_DELTA_ALL:
             ctx->sparse_delta_all = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_GLOBAL_BITMAPS:
+            ctx->sparse_global_bitmaps = value != 0.0;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

@@ -119,9 +119,11 @@ struct SparseArgs {
     const float* self_loss;
     uint64_t* out_lat;           // [rows][ncols]
     float* out_loss;
-    uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2] total evaluations (lo)
+    uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2..3] total evaluations,
+                                 // [5] some relaxation saturated the u32 latency key (a path >= 2^32-1 ns)
     uint32_t delta;              // bucket width in ns (0xFFFFFFFF = one bucket: plain Bellman-Ford)
     uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
+    unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
@@ -135,16 +137,19 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
     return __builtin_nontemporal_load(p);
 }
 
-// LDS bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
+// Vertex bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
 // pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
 // sweep (the out-neighbours of changed vertices, pushed when a vertex changes).  A sweep
-// only visits marked vertices, 64 per wave step (one bitmap word pair).
-template <int G>
+// only visits marked vertices, 64 per wave step (one bitmap word pair).  The five bitmaps take
+// 5 V / 8 bytes: in LDS up to V ~ 190k (GB = false), beyond that in a per-workgroup global
+// slice (GB = true; the same accesses, separated by the same barriers, L2-resident).
+template <int G, bool GB>
 __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
     const uint32_t nw = (V + 63) / 64;  // 64-vertex windows
-    unsigned long long* fprev = reinterpret_cast<unsigned long long*>(smem_raw);
+    unsigned long long* fprev =
+        GB ? a.gbits + (size_t)blockIdx.x * 5 * nw : reinterpret_cast<unsigned long long*>(smem_raw);
     unsigned long long* fcur = fprev + nw;
     unsigned long long* mark = fcur + nw;
     unsigned long long* mnext = mark + nw;
@@ -153,7 +158,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (4 x SP_CAP);
     // the output transpose tile [64][65] u64 reuses the same region after convergence
-    uint32_t* scratch = reinterpret_cast<uint32_t*>(pend + nw);
+    uint32_t* scratch = GB ? reinterpret_cast<uint32_t*>(smem_raw) : reinterpret_cast<uint32_t*>(pend + nw);
     uint32_t* w_st = scratch + wave * (128 + 4 * SP_CAP);
     uint32_t* w_lo = w_st + 64;
     uint32_t* w_u = w_lo + 64;
@@ -164,6 +169,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
     uint32_t max_sweeps = 0;
     unsigned long long evals = 0;
+    uint32_t saturated = 0;  // a finite label + arc reached 2^32-1: INF may then mean "too long", not unreachable
 
     auto push_out = [&](uint32_t v) {  // mark the out-neighbours of v for the next sweep
         const uint32_t o0 = a.out_off[v], o1 = a.out_off[v + 1];
@@ -269,6 +275,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                             } else {
                                 const unsigned long long c =
                                     row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(w_b[e]));
+                                saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
                                 best = c < best ? c : best;
                                 ++evals;
                             }
@@ -458,6 +465,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
         if (bad) atomicOr(&a.flags[0], 1u);
     }
     if (threadIdx.x == 0) atomicMax(&a.flags[1], max_sweeps);
+    if (__ballot(saturated) && lane == 0) atomicOr(&a.flags[5], 1u);
     if (lane == 0 && evals) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[2]), evals);
 }
 

@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "kernels.hip.h"
 
 namespace srg {
@@ -485,6 +487,230 @@ __global__ void __launch_bounds__(64) tight_sparse_u32_runs(const uint32_t* __re
         uint32_t v = St[i][lane];
         if (t >= V || t == s || d[i] == KeyOps<uint32_t>::INF) v = PRED_NONE;
         out[i] = v;
+    }
+}
+
+// ---- LDS-staged scan (SRG_OPT_SCAN_VARIANT 3, the default) -------------------------------
+// The gather scans above pull one 256-B DST row out of L2 per (entry, 64-source block): 7.8e10
+// checks at C3 deliver 312 GB through the texture path, which caps them at ~4 clk per
+// wave-entry.  Here a workgroup owns a 64-source block x LS_TT targets tile and walks the
+// sources' DST columns in u-chunks of LS_UC rows staged ONCE into LDS (LS_UC x 256 B); every
+// essential entry (u, t) of the tile's targets with u in the chunk then costs one conflict-free
+// ds_read_b32 (lane = source) plus ~3.5 VALU ops:
+//     m = min(m, (D[s][u] + w) ^ D[s][t])      -- m == 0 <=> some entry of the run is tight
+// and only a run with a tight lane (rare: ~1 per (s, t) over all chunks) re-tests its entries
+// for the count / the entry index.  Layout: entries grouped by (target tile b, u-chunk k,
+// target), each (target, chunk) run padded with sentinels to a multiple of LS_R, so that a
+// run has one target; per (b, k, target) the run count lives in ls_nr.
+//   ent_lo[e] = (u - k*LS_UC) * 256   (LDS byte offset of u's staged row)
+//   ent_w[e] = W[u][t], ent_u[e] = u, ent_b[e] = 1 - loss(u,t)   (shared with k_loss_rows)
+// Roofline: LDS bytes, 256 B per wave-entry at 128 B/clk/CU.
+constexpr uint32_t LS_WAVES = 8;               // waves per workgroup (512 threads)
+constexpr uint32_t LS_TW = 32;                 // targets per wave (D[s][t] in a 32-register vector)
+constexpr uint32_t LS_TT = LS_WAVES * LS_TW;   // targets per workgroup tile
+constexpr uint32_t LS_UC = 128;                // u rows per staged chunk (32 KB of LDS)
+constexpr uint32_t LS_R = 4;                   // entries per run granule
+
+// per (target tile b, chunk k, target tt): entries / runs.  One wave per (64-target window,
+// chunk), lane = target; also accumulates indeg[t] for the CSC lists.
+__global__ void __launch_bounds__(256) k_ls_count(const unsigned long long* __restrict__ ess, uint32_t V,
+                                                   uint32_t nw64, uint32_t nK, uint32_t* __restrict__ cnt,
+                                                   uint32_t* __restrict__ nruns, uint32_t* __restrict__ rlen,
+                                                   uint32_t* __restrict__ indeg) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    if (wave >= (size_t)nw64 * nK) return;
+    const uint32_t w64 = (uint32_t)(wave / nK), k = (uint32_t)(wave % nK);
+    const uint32_t t = w64 * 64 + lane, b = t / LS_TT, tt = t % LS_TT;
+    const uint32_t u0 = k * LS_UC, u1 = min(V, u0 + LS_UC);
+    uint32_t c = 0;
+    for (uint32_t u = u0; u < u1; ++u) c += (uint32_t)((ess[(size_t)u * nw64 + w64] >> lane) & 1ull);
+    const size_t q = ((size_t)b * nK + k) * LS_TT + tt;
+    cnt[q] = c;
+    const uint32_t r = (c + LS_R - 1) / LS_R;
+    nruns[q] = r;
+    rlen[q] = r * LS_R;
+    if (c) atomicAdd(&indeg[t], c);
+}
+
+// entries of (b, k, t) at roff[q]...: u-sorted, then sentinels (w = INF never tight).  The
+// CSC list of t holds its entries in chunk order: rank = entries of t in chunks < k.
+__global__ void __launch_bounds__(256) k_ls_fill(const unsigned long long* __restrict__ ess,
+                                                  const uint32_t* __restrict__ W, const uint32_t* __restrict__ WL,
+                                                  size_t ld, uint32_t V, uint32_t nw64, uint32_t nK,
+                                                  const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ roff,
+                                                  const uint32_t* __restrict__ csc_off, uint32_t* __restrict__ ent_lo,
+                                                  uint32_t* __restrict__ ent_w, uint32_t* __restrict__ ent_u,
+                                                  float* __restrict__ ent_b, uint32_t* __restrict__ csc_ent) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    if (wave >= (size_t)nw64 * nK) return;
+    const uint32_t w64 = (uint32_t)(wave / nK), k = (uint32_t)(wave % nK);
+    const uint32_t t = w64 * 64 + lane, b = t / LS_TT, tt = t % LS_TT;
+    const size_t qb = (size_t)b * nK * LS_TT + tt;
+    const size_t q = qb + (size_t)k * LS_TT;
+    uint32_t crank = 0;
+    for (uint32_t k2 = 0; k2 < k; ++k2) crank += cnt[qb + (size_t)k2 * LS_TT];
+    const uint32_t cbase = t < V ? csc_off[t] : 0u;
+    const uint32_t u0 = k * LS_UC, u1 = min(V, u0 + LS_UC);
+    uint32_t e = roff[q];
+    for (uint32_t u = u0; u < u1; ++u) {
+        if (!((ess[(size_t)u * nw64 + w64] >> lane) & 1ull)) continue;
+        ent_lo[e] = (u - u0) * 256u;
+        ent_w[e] = W[(size_t)u * ld + t];
+        ent_u[e] = u;
+        ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));
+        csc_ent[cbase + crank++] = e;
+        ++e;
+    }
+    const uint32_t end = roff[q] + (cnt[q] + LS_R - 1) / LS_R * LS_R;
+    for (; e < end; ++e) {
+        ent_lo[e] = 0;
+        ent_w[e] = KeyOps<uint32_t>::INF;
+        ent_u[e] = 0;
+        ent_b[e] = 1.0f;
+    }
+}
+
+typedef uint32_t v32u_ls __attribute__((ext_vector_type(32)));
+struct alignas(16) LsWin {
+    uint32_t v[16];
+};
+__device__ __forceinline__ LsWin ls_win(const uint32_t* p) { return *reinterpret_cast<const LsWin*>(p); }
+
+// grid: 8 * nbTT * ceil(nbS / 8) workgroups (XCD-aware: the workgroups of one XCD share
+// source blocks, so the staged DST column block stays in that XCD's L2).  PRED rows of the
+// tile start as PRED_NONE; a target whose runs hold a tight entry for some lane (rare) is
+// queued in LDS and resolved after the chunk: count + entry index, read-modify-write of
+// PRED (only this workgroup owns those (source, target) pairs).
+__global__ void __launch_bounds__(512, 2) tight_lds_u32(const uint32_t* __restrict__ DST, size_t npad,
+                                                         uint32_t dst_bytes, const uint32_t* __restrict__ nodes,
+                                                         uint32_t n, uint32_t V, uint32_t Vp, uint32_t nbTT,
+                                                         uint32_t nbS, uint32_t nK, const uint32_t* __restrict__ nruns,
+                                                         const uint32_t* __restrict__ roff,
+                                                         const uint32_t* __restrict__ ent_lo,
+                                                         const uint32_t* __restrict__ ent_w,
+                                                         uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ __attribute__((aligned(16))) uint32_t chunk[LS_UC * 64];
+    __shared__ uint32_t hitq[LS_WAVES][LS_TW][2];  // per wave: (target j, first entry) with a tight lane
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r = c * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t voff = r * 4u;  // row offsets go into the VGPR offset: range-checked (rows past DST read 0)
+    const uint32_t t0 = b * LS_TT + wave * LS_TW;
+    const bool active = t0 < Vp;  // a wave past the padded width still stages and syncs
+    const bool own_row = active && r < n;
+    const uint32_t s = r < n ? nodes[r] : 0xFFFFFFFFu;
+    uint32_t* out = PRED + (size_t)r * ldp + t0;
+    v32u_ls dd;
+#pragma unroll
+    for (uint32_t j = 0; j < LS_TW; ++j)
+        dd[j] = active ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + (t0 + j) * (uint32_t)npad * 4u, 0, 0)
+                       : KeyOps<uint32_t>::INF;
+    if (own_row) {
+        const uint4 none = make_uint4(PRED_NONE, PRED_NONE, PRED_NONE, PRED_NONE);
+#pragma unroll
+        for (uint32_t j = 0; j < LS_TW; j += 4) *reinterpret_cast<uint4*>(out + j) = none;
+    }
+    // staging: thread tid copies rows tid/16 + 32 i (i < LS_UC/32), 16 B at column (tid%16)*4
+    constexpr uint32_t ROWS_PER_PASS = LS_WAVES * 64 / 16;
+    constexpr uint32_t SR = LS_UC / ROWS_PER_PASS;
+    const uint32_t srow = tid >> 4, scol = (tid & 15) * 4;
+    uint4 sv[SR];
+    auto stage_load = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t i = 0; i < SR; ++i) {
+            const uint32_t u = k * LS_UC + srow + ROWS_PER_PASS * i;
+            const uint32_t off = u * (uint32_t)npad * 4u + (c * 64 + scol) * 4u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);  // rows >= V read 0
+            sv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    auto stage_store = [&]() {
+#pragma unroll
+        for (uint32_t i = 0; i < SR; ++i)
+            *reinterpret_cast<uint4*>(&chunk[(srow + ROWS_PER_PASS * i) * 64 + scol]) = sv[i];
+    };
+    stage_load(0);
+    stage_store();
+    __syncthreads();
+    const unsigned char* lrow = reinterpret_cast<const unsigned char*>(chunk) + lane * 4u;  // this source's column
+    auto lds_ld = [&](uint32_t byte_off) { return *reinterpret_cast<const uint32_t*>(lrow + byte_off); };
+    for (uint32_t k = 0; k < nK; ++k) {
+        if (k + 1 < nK) stage_load(k + 1);  // issue early, write late
+        if (active) {
+            // per target: D[s][t] from the register vector (uniform index), a 16-entry window of
+            // (ls_lo, w) in SGPRs, one scalar-load wait per target; up to 4 runs from the
+            // window, longer runs (rare) in a loop.  m = 0 in a lane <=> a tight entry there.
+            const size_t q0 = ((size_t)b * nK + k) * LS_TT + wave * LS_TW;
+            const uint32_t* nrp = nruns + q0;
+            uint32_t e_c = (uint32_t)__builtin_amdgcn_readfirstlane(roff[q0]);
+            uint32_t nq = 0;
+            for (uint32_t j = 0; j < LS_TW; ++j) {
+                const uint32_t nr_c = nrp[j];
+                if (nr_c) {
+                    const LsWin lo_c = ls_win(ent_lo + e_c), w_c = ls_win(ent_w + e_c);
+                    const uint32_t dj = dd[j];
+                    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        if (nr_c > i) {
+                            const uint32_t x0 = lds_ld(lo_c.v[4 * i]), x1 = lds_ld(lo_c.v[4 * i + 1]);
+                            const uint32_t x2 = lds_ld(lo_c.v[4 * i + 2]), x3 = lds_ld(lo_c.v[4 * i + 3]);
+                            m = min(m, min((x0 + w_c.v[4 * i]) ^ dj, (x1 + w_c.v[4 * i + 1]) ^ dj));
+                            m = min(m, min((x2 + w_c.v[4 * i + 2]) ^ dj, (x3 + w_c.v[4 * i + 3]) ^ dj));
+                        }
+                    }
+                    for (uint32_t ri = 4; ri < nr_c; ++ri) {
+                        const uint32_t e = e_c + LS_R * ri;
+                        const uint4 lo = *reinterpret_cast<const uint4*>(ent_lo + e);
+                        const uint4 wv = *reinterpret_cast<const uint4*>(ent_w + e);
+                        const uint32_t x0 = lds_ld(lo.x), x1 = lds_ld(lo.y), x2 = lds_ld(lo.z), x3 = lds_ld(lo.w);
+                        m = min(m, min((x0 + wv.x) ^ dj, (x1 + wv.y) ^ dj));
+                        m = min(m, min((x2 + wv.z) ^ dj, (x3 + wv.w) ^ dj));
+                    }
+                    if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                        if (lane == 0) {
+                            hitq[wave][nq][0] = j;
+                            hitq[wave][nq][1] = e_c;
+                        }
+                        ++nq;
+                    }
+                }
+                e_c += LS_R * nr_c;
+            }
+            // resolve the queued targets: count the tight entries per lane, keep the entry index
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t qi = 0; qi < nq; ++qi) {
+                const uint32_t j = hitq[wave][qi][0], e0 = hitq[wave][qi][1];
+                const uint32_t runs = nrp[j];
+                const uint32_t t = t0 + j;
+                const uint32_t dj = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + t * (uint32_t)npad * 4u, 0, 0);
+                uint32_t cnt = 0, last = 0;
+                for (uint32_t ri = 0; ri < runs; ++ri) {
+                    const uint32_t e = e0 + LS_R * ri;
+                    const uint4 lo = *reinterpret_cast<const uint4*>(ent_lo + e);
+                    const uint4 wv = *reinterpret_cast<const uint4*>(ent_w + e);
+                    const uint32_t h0 = lds_ld(lo.x) + wv.x == dj, h1 = lds_ld(lo.y) + wv.y == dj;
+                    const uint32_t h2 = lds_ld(lo.z) + wv.z == dj, h3 = lds_ld(lo.w) + wv.w == dj;
+                    cnt += h0 + h1 + h2 + h3;
+                    last = h3 ? e + 3 : h2 ? e + 2 : h1 ? e + 1 : h0 ? e : last;
+                }
+                if (cnt && own_row && t < V && t != s && dj != KeyOps<uint32_t>::INF) {
+                    const uint32_t sj = out[j];
+                    out[j] = (sj == PRED_NONE && cnt == 1) ? last : PRED_MULTI;
+                }
+            }
+        }
+        if (k + 1 < nK) {
+            __syncthreads();  // every wave is done with chunk k
+            stage_store();
+            __syncthreads();
+        }
     }
 }
 

@@ -110,9 +110,10 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_scan_variants_match_oracle(variant):
-    """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs."""
+    """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs,
+    LDS-staged u-chunks (the default)."""
     r = Router(0)
     r.set_option(N.SRG_OPT_SCAN_VARIANT, variant)
     r.set_option(N.SRG_OPT_SPARSE_THRESHOLD, 1.0)
@@ -150,6 +151,26 @@ def test_subset_nodes_scrambled(scan_router):
     nodes = rng.permutation(180)[:77].tolist()
     lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
     assert_parity(router.compute_shortest_paths(g, nodes), lat, loss)
+
+
+def test_unused_isolated_vertex_keeps_u32(router):
+    """certification covers used (row, column) pairs only, so an isolated UNUSED vertex
+    (unreachable from everything) keeps the u32 keys; an isolated USED vertex with small
+    latencies (max_lat * (V-1) < 2^31-1) is the reference's panic without a u64 rerun."""
+    g = synth.atlas_like(300, seed=3)
+    V = g.num_vertices + 1
+    iso = Edges(V, np.r_[g.src, V - 1], np.r_[g.dst, V - 1], np.r_[g.latency_ns, 1_000_000],
+                np.r_[g.packet_loss, 0.0], False)
+    nodes = list(range(V - 1))
+    lat, loss = oracle.compute_shortest_paths(iso.as_tuple(), nodes)
+    t = router.compute_shortest_paths(iso, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
+    assert_parity(t, lat, loss)
+    small = synth.random_graph(100, 0.2, 5, lat_hi=10)
+    iso2 = Edges(101, np.r_[small.src, 100], np.r_[small.dst, 100], np.r_[small.latency_ns, 7],
+                 np.r_[small.packet_loss, 0.0], False)
+    with pytest.raises(RoutingPanic):
+        router.compute_shortest_paths(iso2, list(range(101)))
 
 
 def test_deterministic_bytes(router):

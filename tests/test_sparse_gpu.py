@@ -84,6 +84,38 @@ def test_bf_delta_buckets(bf_router, kw, div, all_lanes):
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
 
 
+@pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], CASES[5]], ids=lambda k: f"V{k['V']}_s{k['seed']}")
+def test_bf_global_bitmaps(bf_router, kw):
+    """Vertex bitmaps in global memory (the layout for V beyond the LDS budget) are bit-exact."""
+    bf_router.set_option(N.SRG_OPT_SPARSE_GLOBAL_BITMAPS, 1)
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    nodes = list(range(V))
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
+def test_bf_unreachable_ms_latencies_no_fallback(bf_router):
+    """an unreachable used pair with ms-scale latencies (max_lat * (V-1) >> 2^32) is the
+    reference's panic straight from the sparse path (no saturated relaxation happened); an
+    isolated UNUSED vertex does not disturb the sparse u32 result."""
+    e = synth.barabasi_albert(3000, 4, seed=41)
+    V = e.num_vertices + 1  # vertex 3000: isolated, only its self-loop
+    iso = Edges(V, np.r_[e.src, V - 1], np.r_[e.dst, V - 1], np.r_[e.latency_ns, 1_000_000],
+                np.r_[e.packet_loss, 0.0], False)
+    with pytest.raises(RoutingPanic):
+        bf_router.compute_shortest_paths(iso, list(range(V)))
+    nodes = list(range(V - 1))
+    t = bf_router.compute_shortest_paths(iso, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    rows = [0, 1234, 2999]
+    lat, loss = oracle.compute_shortest_paths(iso.as_tuple(), nodes, rows=rows, nthreads=16)
+    assert np.array_equal(t.latency_ns[rows], lat) and bits_equal(t.packet_loss[rows], loss)
+
+
 def test_bf_delta_ba_sampled(bf_router):
     e = synth.barabasi_albert(3000, 4, seed=31)
     bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, 8)
