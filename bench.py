@@ -2,9 +2,12 @@
 
 Workload (BASELINE.json metric, config C3): 10,000-vertex Atlas-like complete GML graph
 (shadow_amd.synth.atlas_like(10000, seed=10000); 49,995,000 undirected edges + 10,000
-self-loops), all 10,000 nodes used.  One step = srg_compute_shortest_paths_device on the
-edge list already resident in HBM -> every (latency_ns, packet_loss) of the 10^8 used pairs
-written to HBM (dense W build, blocked FW, tight-DAG loss pass, extraction).
+self-loops), all 10,000 nodes used.  One step = the host entry srg_compute_shortest_paths, the
+"APSP wall time" SURVEY §8(d) defines: the host edge list (1.0 GB) in, H2D, dense W build,
+blocked FW, tight-DAG loss pass, extraction, and every (latency_ns, packet_loss) of the 10^8
+used pairs back in host memory (1.2 GB D2H, overlapped with the scan).  --entry device times
+srg_compute_shortest_paths_device (inputs and outputs resident in HBM); the host-entry run also
+reports that time as device_entry_ms.
 
 value = source-SSSPs/s over the whole job (sources routed per second, all ranks).
 N > 1: ONE 10k-vertex RoutingInfo per step built by all N GPUs together ("scaling":
@@ -37,37 +40,88 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(edges, target_s, threads):
-    """Reference-equivalent CPU pipeline (oracle, 'port') on a bounded sample of sources."""
+def cpu_info():
+    """Host CPU model, machine CPU count, and the CPU share this job is given."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    # the GPU pool grants each GPU job a CPU share (OMP_NUM_THREADS, 16 per GPU on the MI355X
+    # boxes); the affinity mask shows the whole machine there, so the share sets the threads
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return {"cpu_model": model, "machine_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "threads": max(1, min(share, aff))}
+
+
+def cpu_rate(edges, target_s, threads, mode, seed=12345):
+    """Sources/s of an oracle pipeline on growing random samples of the graph's sources until
+    about target_s seconds of CPU work (oracle.time_sources_mode; setup excluded)."""
     import numpy as np
     import oracle
     g = edges.as_tuple()
-    nodes = np.arange(edges.num_vertices, dtype=np.uint32)
-    rng = np.random.default_rng(12345)
-    done, spent = 0, 0.0
+    V = edges.num_vertices
+    nodes = np.arange(V, dtype=np.uint32)
+    rng = np.random.default_rng(seed)
+    done, spent, setup = 0, 0.0, 0.0
     k = threads
-    while spent < target_s:
-        sample = rng.choice(edges.num_vertices, size=k, replace=False).astype(np.uint32)
-        spent += oracle.time_sources(g, nodes, sample, nthreads=threads)
+    while spent < target_s and done < V:
+        k = min(k, V - done) if done < V else k
+        sample = rng.choice(V, size=k, replace=False).astype(np.uint32)
+        t, setup = oracle.time_sources_mode(g, nodes, sample, nthreads=threads, mode=mode)
+        spent += t
         done += k
-        log(f"cpu baseline: {done} sources in {spent:.1f}s")
-        if spent > 0:
-            k = max(threads, min(4 * k, int(threads * max(1.0, (target_s - spent) / max(spent / done * threads, 1e-3)))))
-            k = min(k, edges.num_vertices)
-    return done / spent, done, spent
+        log(f"cpu baseline mode {mode}: {done} sources in {spent:.1f}s (setup {setup:.1f}s)")
+        k = max(threads, min(4 * k, int(k * max(1.0, (target_s - spent) / max(t, 1e-3)))))
+    return done / spent, done, spent, setup
 
 
-def load_traffic(kernel_substr):
+def cpu_baselines(edges, target_s, desc):
+    """SURVEY §8(d) CPU baseline on the box's host cores: the reference-equivalent pipeline
+    (HashMap-score petgraph Dijkstra + linear nodes.contains + HashMap merge, like rayon x
+    petgraph, mod.rs:190-208) and a CPU-best variant (dense scores, O(1) membership, dense rows;
+    the dense-matrix Dijkstra on dense graphs).  Both on a bounded random sample of sources,
+    extrapolated to all sources at the measured per-source rate."""
+    info = cpu_info()
+    th = info["threads"]
+    V = edges.num_vertices
+    dense = edges.num_edges * 8 > V * V
+    ref, k0, s0, _ = cpu_rate(edges, target_s, th, 0)
+    best, k1, s1, setup1 = cpu_rate(edges, max(3.0, target_s / 2), th, 2 if dense else 1)
+    return {"value": round(ref, 3), "unit": "source-SSSPs/s", "cores": th, "kind": "port",
+            "sample": f"{k0} random sources of {desc}, reference-equivalent pipeline (HashMap-score petgraph "
+                      f"Dijkstra + linear nodes.contains + HashMap merge, mod.rs:190-208) on {th} threads, {s0:.1f}s",
+            "extrapolated": True, "full_run_estimate_s": round(V / ref, 1),
+            **info,
+            "best": {"value": round(best, 3), "unit": "source-SSSPs/s", "cores": th,
+                     "algorithm": ("dense-matrix Dijkstra, O(V^2) per source" if dense else
+                                   "heap Dijkstra with dense scores") + ", O(1) membership, dense output rows",
+                     "sample": f"{k1} random sources, {s1:.1f}s (+{setup1:.1f}s one-time setup)",
+                     "extrapolated": True, "full_run_estimate_s": round(V / best + setup1, 1)}}
+
+
+def load_traffic(kernel_substr, workload_key):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (profiles/fw_pmc_latest.json for the FW tile, profiles/sparse_pmc_latest.json for k_sparse_bf)."""
+    (profiles/fw_pmc_latest.json for the FW tile, profiles/sparse_pmc_latest.json for k_sparse_bf),
+    only when that summary was collected on this run's workload and options (else None)."""
     name = "sparse_pmc_latest.json" if "sparse" in kernel_substr else "fw_pmc_latest.json"
     p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), d.get("source")
     except Exception:
         return None, None
+    if d.get("workload_key") != workload_key:
+        return None, f"{d.get('source')} (workload {d.get('workload_key')!r} != this run's {workload_key!r})"
+    return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
 def bench_events(args, n=10**7, hosts=10000):
@@ -175,12 +229,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--vertices", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--graph", choices=["atlas", "ba", "events"], default="atlas",
-                    help="atlas = C3 (headline), ba = C4, events = C5 stretch (10^7 packet events)")
-    ap.add_argument("--entry", choices=["host", "device"], default="device",
+    ap.add_argument("--graph", choices=["atlas", "complete", "ba", "events"], default="atlas",
+                    help="atlas = C3 (headline; C2 with --vertices 4096), complete = C1, ba = C4, "
+                         "events = C5 stretch (10^7 packet events)")
+    ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default=None,
+                    help="BASELINE.json config preset (sets --graph / --vertices)")
+    ap.add_argument("--entry", choices=["host", "device"], default=None,
                     help="host = srg_compute_shortest_paths (host edge list in, host table out: H2D + D2H "
                          "included); device = srg_compute_shortest_paths_device (inputs/outputs in HBM)")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
@@ -198,8 +255,17 @@ def main():
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
                          "(outputs invalid; prints a diagnostic line, never the bench result)")
     args = ap.parse_args()
+    if args.config:
+        args.graph, args.vertices = {"c1": ("complete", 1000), "c2": ("atlas", 4096), "c3": ("atlas", 10000),
+                                     "c4": ("ba", 50000), "c5": ("events", 10000)}[args.config]
     if args.graph == "ba" and args.vertices == 10000 and "--vertices" not in sys.argv:
         args.vertices = 50000
+    if args.graph == "complete" and args.vertices == 10000 and "--vertices" not in sys.argv:
+        args.vertices = 1000
+    if args.entry is None:
+        # the headline: host edge list in, host table out.  C4's 30 GB table is
+        # benchmarked device-resident by default (a host copy of it is 0.5 s of PCIe alone).
+        args.entry = "device" if args.graph == "ba" else "host"
 
     import torch
     import torch.distributed as dist
@@ -224,7 +290,12 @@ def main():
     t0 = time.time()
     if args.graph == "atlas":
         edges = synth.atlas_like(V, seed=seed)
-        gdesc = f"C3 atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph"
+        cname = {10000: "C3", 4096: "C2"}.get(V, "atlas")
+        gdesc = f"{cname} atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph"
+    elif args.graph == "complete":
+        seed = args.seed if args.seed is not None else 1001
+        edges = synth.complete_random(V, seed=seed)
+        gdesc = f"C1 complete_random({V}, seed={seed}): complete undirected graph, random latency/loss"
     else:
         edges = synth.barabasi_albert(V, 4, seed=seed)
         gdesc = f"C4 barabasi_albert({V}, m=4, seed={seed}): sparse undirected graph"
@@ -309,6 +380,19 @@ def main():
     value = (1 if strong else world) * V * args.steps / elapsed
 
     kind = s["path_kind"]
+    # the device-resident time of the same build (inputs and outputs in HBM): the kernel pipeline
+    # alone, reported beside the host-entry headline
+    dev_ms = None
+    if args.entry == "host" and world == 1 and not args.simulate_rank:
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(2):
+            compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
+        torch.cuda.synchronize(dev)
+        dev_ms = (time.perf_counter() - t1) * 1e3 / 2
+    wkey = (f"{args.graph}:{V}:{seed}:packed{args.fw_packed}:tile{args.fw_tile or 128}:"
+            f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
+            f"w{args.sparse_wgs or 2}")
     roofline = None
     if agg.get("prof_launches") and kind == 3:
         # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
@@ -318,7 +402,7 @@ def main():
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         srcs = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic("k_sparse_bf")
+        traffic, tsrc = load_traffic("k_sparse_bf", wkey)
         roofline = {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford, delta-stepping buckets)",
                     "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                     "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
@@ -329,7 +413,7 @@ def main():
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         relax = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
-        traffic, tsrc = load_traffic("fw_product")
+        traffic, tsrc = load_traffic("fw_product", wkey)
         roofline = {"bound": "valu", "kernel": ("fw_product<u32,128,32,packed> (FW phase 3, non-lookahead tiles)" if args.fw_packed else "fw_product<u32,128,32> (FW phase 3, non-lookahead tiles)") if kind == 0 else "fw_product<u64,64,32> (FW phase 3)", "achieved": round(achieved, 3),
                     "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
@@ -338,40 +422,38 @@ def main():
                     "traffic_source": tsrc}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        try:
-            aff = len(os.sched_getaffinity(0))
-        except Exception:
-            aff = os.cpu_count() or 1
-        threads = max(1, min(16, aff))
-        v, k, sec = cpu_baseline(edges, args.cpu_seconds, threads)
-        cpu = {"value": round(v, 3), "unit": "source-SSSPs/s", "cores": threads, "kind": "port",
-               "sample": f"{k} random sources of the same 10k-vertex graph, reference-equivalent pipeline "
-                         f"(HashMap-score Dijkstra + linear nodes.contains + HashMap merge), {sec:.1f}s"}
+    if rank == 0 and world == 1 and not args.no_cpu and not args.simulate_rank:
+        cpu = cpu_baselines(edges, args.cpu_seconds, gdesc.split(":")[0])
 
+    brk = ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")
     if args.simulate_rank:
         n = args.steps
         print(json.dumps({"diagnostic": "simulated rank (collectives elided, outputs invalid)",
                           "simulate_rank": args.simulate_rank, "ms_per_step": round(ms_per_step, 3),
-                          "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in
-                                           ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")},
+                          "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
                           "roofline": roofline}), flush=True)
         return
     if rank == 0:
         n = args.steps
+        entry_desc = ("host entry srg_compute_shortest_paths: host edge list in, host n x n table out "
+                      "(H2D + kernels + D2H in the step)" if args.entry == "host" else
+                      "device entry srg_compute_shortest_paths_device: edge list resident in HBM, table left in HBM")
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "source-SSSPs/s", "n_gpus": world, "steps": n,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "u64+f32" if kind == 1 else "u32+f32",
             "data": "synthetic",
-            "config": {"workload": f"{gdesc}, all {V} nodes used, edge list resident in HBM",
-                       "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
+            "config": {"workload": f"{gdesc}, all {V} nodes used, {entry_desc}",
+                       "entry": args.entry, "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
                        "parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single",
                        **({"fallback": fallback} if fallback else {}),
                        "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
             "apsp_wall_ms": round(ms_per_step, 3),
-            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")},
+            "ms_h2d": round(agg.get("ms_h2d", 0) / n, 3), "ms_d2h": round(agg.get("ms_d2h", 0) / n, 3),
+            "d2h_overlapped_GB": round(agg.get("d2h_overlapped_bytes", 0) / n / 1e9, 3),
+            "device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None,
+            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
             "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
             "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
             "roofline": roofline, "cpu_baseline": cpu,

@@ -91,6 +91,9 @@ typedef struct srg_stats {
      * finished rows leave while later kernels run; ms_d2h above is only the exposed tail.   */
     double ms_host_register;    /* page-locking time (hidden; -1 = not used / failed)      */
     uint64_t d2h_overlapped_bytes; /* output bytes copied to the host while kernels ran    */
+    uint64_t min_latency_ns;    /* host entry: min latency over all n^2 outputs, diagonal included
+                                   (RoutingInfo::get_smallest_latency_ns, mod.rs:474-476);
+                                   UINT64_MAX when n = 0                                       */
 } srg_stats;
 
 #define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */
@@ -163,6 +166,34 @@ int srg_get_direct_paths(srg_ctx* ctx, const srg_edge_list* graph,
                          const uint32_t* nodes, uint32_t num_nodes,
                          uint64_t* out_latency_ns, float* out_packet_loss,
                          srg_stats* stats, char* errbuf, size_t errlen);
+
+/* ---- RoutingInfo, dense-backed ------------------------------------------
+ * Replaces generate_routing_info (src/main/core/sim_config.rs:425-462) and RoutingInfo<u32>
+ * (mod.rs:428-477).  The reference builds two n^2-entry HashMaps (mod.rs:190-208 and
+ * sim_config.rs:448-450); here the table is the dense n x n SoA the GPU wrote plus a GML-id ->
+ * position index, so building it costs one host-entry call (srg_compute_shortest_paths).     */
+typedef struct srg_routing_info srg_routing_info;
+/* gml_ids[num_ids]: the used nodes' GML ids (ip_assignment.get_nodes(), any order); they are
+ * resolved with graph->node_ids (node_id_to_index, mod.rs:126-128; NULL = id == index).
+ * use_shortest_paths = network.use_shortest_path (configuration.rs:286-292).  Errors carry the
+ * reference's context prefix ("Failed to compute shortest paths between graph nodes: ...").   */
+int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
+                           int use_shortest_paths, srg_routing_info** out, srg_stats* stats,
+                           char* errbuf, size_t errlen);
+void srg_routing_info_free(srg_routing_info* ri);
+uint32_t srg_routing_info_num_nodes(const srg_routing_info* ri);
+/* RoutingInfo::path (mod.rs:444-446): 1 and the path's properties, or 0 (None).              */
+int srg_routing_info_path(const srg_routing_info* ri, uint32_t start_id, uint32_t end_id,
+                          uint64_t* latency_ns, float* packet_loss);
+/* RoutingInfo::increment_packet_count (mod.rs:449-456): saturating, thread-safe.              */
+void srg_routing_info_increment_packet_count(srg_routing_info* ri, uint32_t start_id, uint32_t end_id);
+uint64_t srg_routing_info_packet_count(srg_routing_info* ri, uint32_t start_id, uint32_t end_id);
+/* RoutingInfo::get_smallest_latency_ns (mod.rs:474-476): 1 and the min over all entries
+ * (diagonal included), or 0 (None, empty table).                                               */
+int srg_routing_info_smallest_latency_ns(const srg_routing_info* ri, uint64_t* out);
+/* Borrowed dense tables (row-major by position) and the GML id of each position.             */
+void srg_routing_info_tables(const srg_routing_info* ri, const uint64_t** latency_ns, const float** packet_loss,
+                             const uint32_t** gml_ids, uint32_t* n);
 
 /* ---- ingest: GML text -> graph (NetworkGraph::parse, mod.rs:134-181) --------------- */
 typedef struct srg_graph srg_graph;  /* opaque host-side parsed graph */

@@ -53,6 +53,11 @@ def lib():
         L.oracle_time_sources.argtypes = [
             ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, _u32p, _u32p, _u64p, _f32p, _u32p,
             ctypes.c_uint32, _u32p, ctypes.c_uint32, ctypes.c_int, _u64p]
+        L.oracle_time_sources_mode.restype = ctypes.c_double
+        L.oracle_time_sources_mode.argtypes = [
+            ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, _u32p, _u32p, _u64p, _f32p, _u32p,
+            ctypes.c_uint32, _u32p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+            _u64p]
         L.oracle_hw_threads.restype = ctypes.c_int
         L.oracle_order_packet_events.restype = ctypes.c_int
         L.oracle_order_packet_events.argtypes = [
@@ -136,6 +141,21 @@ def time_sources(graph, nodes, sample, nthreads=0):
     return lib().oracle_time_sources(
         V, d, len(src), _p(src, _u32p), _p(dst, _u32p), _p(lat, _u64p), _p(loss, _f32p),
         _p(nodes, _u32p), len(nodes), _p(sample, _u32p), len(sample), nthreads, ctypes.byref(cs))
+
+
+def time_sources_mode(graph, nodes, sample, nthreads=0, mode=0):
+    """CPU-baseline timer: mode 0 reference-equivalent, 1 CPU-best heap Dijkstra (sparse), 2 CPU-best
+    dense-matrix Dijkstra.  Returns (seconds for the sample, one-time setup seconds)."""
+    V, d, src, dst, lat, loss, _ = _graph_arrays(graph)
+    nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+    sample = np.ascontiguousarray(sample, dtype=np.uint32)
+    cs = ctypes.c_uint64()
+    setup = ctypes.c_double()
+    t = lib().oracle_time_sources_mode(
+        V, d, len(src), _p(src, _u32p), _p(dst, _u32p), _p(lat, _u64p), _p(loss, _f32p),
+        _p(nodes, _u32p), len(nodes), _p(sample, _u32p), len(sample), nthreads, mode, ctypes.byref(setup),
+        ctypes.byref(cs))
+    return t, setup.value
 
 
 def hw_threads():

@@ -506,6 +506,59 @@ double oracle_time_sources(uint32_t V, int directed, uint64_t E, const uint32_t*
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// CPU-baseline timer with a choice of pipeline (bench.py cpu_baseline):
+//   mode 0: the reference-equivalent pipeline above (oracle_time_sources)
+//   mode 1: "CPU-best" for sparse graphs: the same heap Dijkstra with dense scores, O(1)
+//           membership (position table instead of nodes.contains) and a dense output row
+//   mode 2: "CPU-best" for dense graphs: dense-matrix Dijkstra (dijkstra_matrix), dense rows
+// *setup_s = one-time preparation (graph build; mode 2 also the dense weight matrix), NOT in
+// the returned seconds; the returned time covers the sample's sources (and mode 0's merge).
+double oracle_time_sources_mode(uint32_t V, int directed, uint64_t E, const uint32_t* src, const uint32_t* dst,
+                                const uint64_t* lat, const float* loss, const uint32_t* nodes, uint32_t n,
+                                const uint32_t* sample, uint32_t k, int nthreads, int mode, double* setup_s,
+                                uint64_t* checksum) {
+    if (mode == 0) {
+        auto s0 = std::chrono::steady_clock::now();
+        Graph g0;
+        g0.build(V, directed, E, src, dst, lat, loss, nullptr);
+        if (setup_s) *setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+        return oracle_time_sources(V, directed, E, src, dst, lat, loss, nodes, n, sample, k, nthreads, checksum);
+    }
+    auto s0 = std::chrono::steady_clock::now();
+    Graph g;
+    g.build(V, directed, E, src, dst, lat, loss, nullptr);
+    DenseW w;
+    if (mode == 2) w.build(g);
+    std::vector<int32_t> pos_of(V, -1);
+    for (uint32_t i = 0; i < n; ++i) pos_of[nodes[i]] = (int32_t)i;
+    std::vector<uint64_t> out_lat((size_t)k * n);
+    std::vector<float> out_loss((size_t)k * n);
+    if (setup_s) *setup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+    nthreads = hw_threads(nthreads);
+    auto t0 = std::chrono::steady_clock::now();
+    parallel_for(k, nthreads, [&](uint32_t r) {
+        std::vector<PP> score;
+        std::vector<uint8_t> seen, visited;
+        const uint32_t s = nodes[sample[r]];
+        if (mode == 2) dijkstra_matrix(w, s, score, seen, visited);
+        else dijkstra_dense(g, s, score, seen, visited);
+        uint64_t* ol = &out_lat[(size_t)r * n];
+        float* of = &out_loss[(size_t)r * n];
+        for (uint32_t v = 0; v < V; ++v) {
+            const int32_t p = pos_of[v];
+            if (p >= 0 && seen[v]) {
+                ol[p] = score[v].lat;
+                of[p] = score[v].loss;
+            }
+        }
+    });
+    auto t1 = std::chrono::steady_clock::now();
+    uint64_t cs = 0;
+    for (uint64_t v : out_lat) cs += v;
+    if (checksum) *checksum = cs;
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
 int oracle_hw_threads(void) { return hw_threads(0); }
 
 // ---- stretch C5: one round's cross-host packet events ----------------------

@@ -123,6 +123,7 @@ class Stats(ctypes.Structure):
         ("local_sources", ctypes.c_uint64),
         ("ms_host_register", ctypes.c_double),
         ("d2h_overlapped_bytes", ctypes.c_uint64),
+        ("min_latency_ns", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -136,7 +137,9 @@ EXPORTS = [
     "srg_graph_num_vertices", "srg_graph_num_edges", "srg_graph_directed", "srg_graph_node_index",
     "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version", "srg_comm_unique_id", "srg_comm_init",
     "srg_local_group_create", "srg_local_group_release", "srg_comm_init_local", "srg_comm_size",
-    "srg_order_packet_events_device",
+    "srg_order_packet_events_device", "srg_routing_info_build", "srg_routing_info_free", "srg_routing_info_num_nodes",
+    "srg_routing_info_path", "srg_routing_info_increment_packet_count", "srg_routing_info_packet_count",
+    "srg_routing_info_smallest_latency_ns", "srg_routing_info_tables",
 ]
 
 _lib = None
@@ -211,6 +214,24 @@ def lib():
     L.srg_order_packet_events_device.argtypes = [
         c.c_void_p, c.POINTER(EventBatch), c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p,
         c.POINTER(EventResult), c.c_char_p, c.c_size_t]
+    L.srg_routing_info_build.restype = c.c_int
+    L.srg_routing_info_build.argtypes = [c.c_void_p, c.POINTER(EdgeList), c.c_void_p, c.c_uint32, c.c_int,
+                                         c.POINTER(c.c_void_p), c.POINTER(Stats), c.c_char_p, c.c_size_t]
+    L.srg_routing_info_free.restype = None
+    L.srg_routing_info_free.argtypes = [c.c_void_p]
+    L.srg_routing_info_num_nodes.restype = c.c_uint32
+    L.srg_routing_info_num_nodes.argtypes = [c.c_void_p]
+    L.srg_routing_info_path.restype = c.c_int
+    L.srg_routing_info_path.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, _u64p, _f32p]
+    L.srg_routing_info_increment_packet_count.restype = None
+    L.srg_routing_info_increment_packet_count.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32]
+    L.srg_routing_info_packet_count.restype = c.c_uint64
+    L.srg_routing_info_packet_count.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32]
+    L.srg_routing_info_smallest_latency_ns.restype = c.c_int
+    L.srg_routing_info_smallest_latency_ns.argtypes = [c.c_void_p, _u64p]
+    L.srg_routing_info_tables.restype = None
+    L.srg_routing_info_tables.argtypes = [c.c_void_p, c.POINTER(_u64p), c.POINTER(_f32p), c.POINTER(_u32p),
+                                          c.POINTER(c.c_uint32)]
     L.srg_comm_size.restype = c.c_int
     L.srg_comm_size.argtypes = [c.c_void_p, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     _lib = L

@@ -356,6 +356,19 @@ __global__ void k_rows_copy(const unsigned char* __restrict__ src, unsigned char
     }
 }
 
+// min over a u64 array (RoutingInfo::get_smallest_latency_ns, mod.rs:474-476: all n^2 entries,
+// diagonal included)
+__global__ void k_min_u64(const uint64_t* __restrict__ a, size_t count, unsigned long long* out) {
+    unsigned long long m = ~0ull;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+        m = a[i] < m ? a[i] : m;
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_down(m, off, 64);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(out, m);
+}
+
 __global__ void k_positions(const uint32_t* __restrict__ nodes, uint32_t n, int32_t* __restrict__ pos) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         pos[nodes[i]] = (int32_t)i;
@@ -1699,6 +1712,13 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
         else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr);
         auto t1 = std::chrono::steady_clock::now();
+        unsigned long long hmin = ~0ull;
+        if (nn && stats) {  // smallest latency over the table (feeds the runahead, manager.rs:238-243)
+            unsigned long long* dmin = (unsigned long long*)c->b_multi.get(8);
+            HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 8, st));
+            k_min_u64<<<grid_for(nn, 1024), kThreads, 0, st>>>(dol, nn, dmin);
+            HIP_CHECK(hipMemcpyAsync(&hmin, dmin, 8, hipMemcpyDeviceToHost, st));
+        }
         if (nn && !sink.lat_sent) HIP_CHECK(hipMemcpyAsync(out_lat, dol, nn * 8, hipMemcpyDeviceToHost, st));
         if (nn && !sink.loss_sent) HIP_CHECK(hipMemcpyAsync(out_loss, dos, nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
@@ -1709,6 +1729,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             stats->ms_total = ms_since(t0);
             stats->ms_host_register = reg.join() ? reg.ms : -1.0;
             stats->d2h_overlapped_bytes = sink.early_bytes;
+            stats->min_latency_ns = hmin;
             if (direct) stats->path_kind = SRG_PATH_DIRECT;
         }
     });

@@ -1,0 +1,199 @@
+// routing_info.cpp — dense-backed RoutingInfo behind the C ABI.
+//
+// Replaces, on Shadow's side of the boundary:
+//   generate_routing_info   src/main/core/sim_config.rs:425-462  (GML ids -> NodeIndex, shortest or
+//                           direct paths, results keyed back by GML id)
+//   RoutingInfo<u32>        src/main/network/graph/mod.rs:428-477 (path lookup, packet counters,
+//                           get_smallest_latency_ns)
+// The reference materialises two HashMaps of n^2 entries (mod.rs:190-208 and sim_config.rs:448-450:
+// 2 x 10^8 inserts at C3).  Here the table stays the dense n x n SoA the GPU wrote (row-major by
+// position of the id in the caller's list) plus a GML-id -> position index, so the build is the
+// host entry (H2D + kernels + overlapped D2H) and nothing else.  Host-only C++: no HIP calls here.
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/shadow_routing.h"
+
+namespace {
+
+constexpr uint32_t NO_POS = 0xFFFFFFFFu;
+
+void put_err(char* buf, size_t len, const std::string& m) {
+    if (buf && len) std::snprintf(buf, len, "%s", m.c_str());
+}
+
+// per-path packet counters (mod.rs:432, 449-456): RwLock<HashMap> in the reference, here 64
+// lock-striped maps so that concurrent senders on different paths rarely share a lock
+struct Counters {
+    static constexpr int SHARDS = 64;
+    struct Shard {
+        std::mutex mu;
+        std::unordered_map<uint64_t, uint64_t> m;
+    } shard[SHARDS];
+    static uint64_t key(uint32_t a, uint32_t b) { return (uint64_t)a << 32 | b; }
+    Shard& of(uint64_t k) { return shard[(k * 0x9E3779B97F4A7C15ull) >> 58]; }
+};
+
+}  // namespace
+
+struct srg_routing_info {
+    uint32_t n = 0;
+    std::vector<uint32_t> ids;       // GML id per position
+    // [n x n] tables, left uninitialised (every entry is written by the build; no 1.2 GB memset)
+    std::unique_ptr<uint64_t[]> lat;
+    std::unique_ptr<float[]> loss;
+    uint64_t min_lat = UINT64_MAX;
+    // GML id -> position: a direct table when the ids are dense enough, else a hash map
+    std::vector<uint32_t> pos_direct;
+    std::unordered_map<uint32_t, uint32_t> pos_hash;
+    Counters counters;
+
+    uint32_t pos(uint32_t id) const {
+        if (!pos_direct.empty()) return id < pos_direct.size() ? pos_direct[id] : NO_POS;
+        auto f = pos_hash.find(id);
+        return f == pos_hash.end() ? NO_POS : f->second;
+    }
+};
+
+extern "C" {
+
+int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
+                           int use_shortest_paths, srg_routing_info** out, srg_stats* stats, char* errbuf,
+                           size_t errlen) {
+    if (!ctx || !graph || !out || (num_ids && !gml_ids)) {
+        put_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    *out = nullptr;
+    try {
+        // node_id_to_index (mod.rs:126-128): GML id -> NodeIndex, later duplicate ids win (:161)
+        const uint32_t V = graph->num_vertices;
+        std::unordered_map<uint32_t, uint32_t> id_to_index;
+        id_to_index.reserve(V);
+        for (uint32_t v = 0; v < V; ++v) id_to_index[graph->node_ids ? graph->node_ids[v] : v] = v;
+        std::vector<uint32_t> nodes(num_ids);
+        for (uint32_t i = 0; i < num_ids; ++i) {
+            auto f = id_to_index.find(gml_ids[i]);
+            if (f == id_to_index.end()) {  // graph.node_id_to_index(*x).unwrap() panics (sim_config.rs:433)
+                put_err(errbuf, errlen,
+                        "called `Option::unwrap()` on a `None` value (GML node id " + std::to_string(gml_ids[i]) +
+                            " is not in the graph)");
+                return SRG_ERR_ARG;
+            }
+            nodes[i] = f->second;
+        }
+        auto* ri = new srg_routing_info();
+        ri->n = num_ids;
+        ri->ids.assign(gml_ids, gml_ids + num_ids);
+        const size_t nn = (size_t)num_ids * num_ids;
+        ri->lat.reset(new uint64_t[std::max<size_t>(nn, 1)]);
+        ri->loss.reset(new float[std::max<size_t>(nn, 1)]);
+        srg_stats local{};
+        srg_stats* st = stats ? stats : &local;
+        const int rc = use_shortest_paths
+                           ? srg_compute_shortest_paths(ctx, graph, nodes.data(), num_ids, ri->lat.get(),
+                                                        ri->loss.get(), st, errbuf, errlen)
+                           : srg_get_direct_paths(ctx, graph, nodes.data(), num_ids, ri->lat.get(),
+                                                  ri->loss.get(), st, errbuf, errlen);
+        if (rc != SRG_OK) {
+            delete ri;
+            // .context("Failed to compute shortest paths between graph nodes") (sim_config.rs:446-447)
+            if (errbuf && errlen) {
+                const std::string inner = errbuf;
+                put_err(errbuf, errlen,
+                        std::string(use_shortest_paths ? "Failed to compute shortest paths between graph nodes: "
+                                                       : "Failed to get the direct paths between graph nodes: ") +
+                            inner);
+            }
+            return rc;
+        }
+        ri->min_lat = st->min_latency_ns;
+        if (!use_shortest_paths) ri->min_lat = nn ? *std::min_element(ri->lat.get(), ri->lat.get() + nn) : UINT64_MAX;
+        uint32_t max_id = 0;
+        for (uint32_t id : ri->ids) max_id = std::max(max_id, id);
+        if (num_ids && (uint64_t)max_id < std::max<uint64_t>(1u << 20, 16ull * num_ids)) {
+            ri->pos_direct.assign((size_t)max_id + 1, NO_POS);
+            for (uint32_t i = 0; i < num_ids; ++i) {
+                if (ri->pos_direct[ri->ids[i]] != NO_POS) {
+                    delete ri;
+                    put_err(errbuf, errlen, "duplicate GML id in the node list");
+                    return SRG_ERR_ARG;
+                }
+                ri->pos_direct[ri->ids[i]] = i;
+            }
+        } else {
+            for (uint32_t i = 0; i < num_ids; ++i)
+                if (!ri->pos_hash.emplace(ri->ids[i], i).second) {
+                    delete ri;
+                    put_err(errbuf, errlen, "duplicate GML id in the node list");
+                    return SRG_ERR_ARG;
+                }
+        }
+        *out = ri;
+        return SRG_OK;
+    } catch (const std::bad_alloc&) {
+        put_err(errbuf, errlen, "out of host memory");
+        return SRG_ERR_OOM;
+    } catch (...) {
+        put_err(errbuf, errlen, "internal error");
+        return SRG_ERR_INTERNAL;
+    }
+}
+
+void srg_routing_info_free(srg_routing_info* ri) { delete ri; }
+
+uint32_t srg_routing_info_num_nodes(const srg_routing_info* ri) { return ri ? ri->n : 0; }
+
+int srg_routing_info_path(const srg_routing_info* ri, uint32_t start, uint32_t end, uint64_t* latency_ns,
+                          float* packet_loss) {
+    if (!ri) return 0;
+    const uint32_t a = ri->pos(start), b = ri->pos(end);
+    if (a == NO_POS || b == NO_POS) return 0;  // paths.get(&(start, end)) == None
+    const size_t k = (size_t)a * ri->n + b;
+    if (latency_ns) *latency_ns = ri->lat[k];
+    if (packet_loss) *packet_loss = ri->loss[k];
+    return 1;
+}
+
+void srg_routing_info_increment_packet_count(srg_routing_info* ri, uint32_t start, uint32_t end) {
+    if (!ri) return;
+    const uint64_t k = Counters::key(start, end);
+    auto& s = ri->counters.of(k);
+    std::lock_guard<std::mutex> lk(s.mu);
+    uint64_t& c = s.m[k];
+    if (c != UINT64_MAX) ++c;  // saturating_add(1)
+}
+
+uint64_t srg_routing_info_packet_count(srg_routing_info* ri, uint32_t start, uint32_t end) {
+    if (!ri) return 0;
+    const uint64_t k = Counters::key(start, end);
+    auto& s = ri->counters.of(k);
+    std::lock_guard<std::mutex> lk(s.mu);
+    auto f = s.m.find(k);
+    return f == s.m.end() ? 0 : f->second;
+}
+
+int srg_routing_info_smallest_latency_ns(const srg_routing_info* ri, uint64_t* out) {
+    if (!ri || ri->n == 0) return 0;  // an empty map: None
+    if (out) *out = ri->min_lat;
+    return 1;
+}
+
+void srg_routing_info_tables(const srg_routing_info* ri, const uint64_t** latency_ns, const float** packet_loss,
+                             const uint32_t** gml_ids, uint32_t* n) {
+    if (latency_ns) *latency_ns = ri ? ri->lat.get() : nullptr;
+    if (packet_loss) *packet_loss = ri ? ri->loss.get() : nullptr;
+    if (gml_ids) *gml_ids = ri ? ri->ids.data() : nullptr;
+    if (n) *n = ri ? ri->n : 0;
+}
+
+}  // extern "C"

@@ -7,8 +7,8 @@ Same names, argument meaning and error behaviour as the reference:
   NetworkGraph.node_index_to_id  mod.rs:130-132
   NetworkGraph.compute_shortest_paths   mod.rs:183-228  (HIP, gfx950 — no CPU fallback)
   NetworkGraph.get_direct_paths  mod.rs:230-252  (HIP)
-  RoutingInfo                    mod.rs:428-477
-  generate_routing_info          src/main/core/sim_config.rs:425-462
+  RoutingInfo                    mod.rs:428-477            (native dense table, srg_routing_info)
+  generate_routing_info          src/main/core/sim_config.rs:425-462  (srg_routing_info_build)
 
 The reference returns HashMap<(NodeIndex, NodeIndex), PathProperties>; here the result is a
 dense PathTable (row-major by position in `nodes`) that behaves like that map
@@ -351,49 +351,72 @@ class NetworkGraph:
 
 
 class RoutingInfo:
-    """Routing information keyed by GML node ids (mod.rs:428-477), dense-backed."""
+    """RoutingInfo<u32> (mod.rs:428-477) backed by the native dense table (srg_routing_info):
+    path(start, end) by GML id, packet counters with saturating_add, get_smallest_latency_ns."""
 
-    def __init__(self, table, ids):
-        self._table = table
-        self._ids = np.asarray(ids, dtype=np.uint32)
-        self._pos = {int(g): i for i, g in enumerate(self._ids)}
-        self._counters = {}
-        self._lock = threading.Lock()
+    def __init__(self, handle, stats=None):
+        self._h = handle
+        self.stats = stats
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().srg_routing_info_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def path(self, start, end):
-        i, j = self._pos.get(start), self._pos.get(end)
-        if i is None or j is None:
+        lat, loss = ctypes.c_uint64(), ctypes.c_float()
+        if not N.lib().srg_routing_info_path(self._h, int(start), int(end), ctypes.byref(lat), ctypes.byref(loss)):
             return None
-        return PathProperties(int(self._table.latency_ns[i, j]), self._table.packet_loss[i, j])
+        return PathProperties(lat.value, loss.value)
 
     def increment_packet_count(self, start, end):
-        with self._lock:
-            k = (start, end)
-            self._counters[k] = min(self._counters.get(k, 0) + 1, 0xFFFFFFFFFFFFFFFF)
+        N.lib().srg_routing_info_increment_packet_count(self._h, int(start), int(end))
 
     def packet_count(self, start, end):
-        return self._counters.get((start, end), 0)
+        return int(N.lib().srg_routing_info_packet_count(self._h, int(start), int(end)))
 
     def get_smallest_latency_ns(self):
-        if len(self._ids) == 0:
+        v = ctypes.c_uint64()
+        if not N.lib().srg_routing_info_smallest_latency_ns(self._h, ctypes.byref(v)):
             return None
-        return int(self._table.latency_ns.min())
+        return int(v.value)
+
+    def tables(self):
+        """(latency_ns u64 [n, n], packet_loss f32 [n, n], gml_ids u32 [n]) -- zero-copy views."""
+        lp, fp, ip, n = N._u64p(), N._f32p(), N._u32p(), ctypes.c_uint32()
+        N.lib().srg_routing_info_tables(self._h, ctypes.byref(lp), ctypes.byref(fp), ctypes.byref(ip), ctypes.byref(n))
+        n = n.value
+        if n == 0:
+            return (np.zeros((0, 0), np.uint64), np.zeros((0, 0), np.float32), np.zeros(0, np.uint32))
+        return (np.ctypeslib.as_array(lp, shape=(n, n)), np.ctypeslib.as_array(fp, shape=(n, n)),
+                np.ctypeslib.as_array(ip, shape=(n,)))
 
     def __len__(self):
-        return len(self._ids) ** 2
+        return int(N.lib().srg_routing_info_num_nodes(self._h)) ** 2
 
 
 def generate_routing_info(graph, nodes, use_shortest_paths=True, router=None):
-    """sim_config.rs:425-462: GML ids -> NodeIndex, shortest or direct paths, keyed by GML id."""
-    idx = [graph.node_id_to_index(x) for x in nodes]
-    if any(i is None for i in idx):
-        raise NetGraphError(N.SRG_ERR_ARG, "node id not in graph")
-    try:
-        if use_shortest_paths:
-            table = graph.compute_shortest_paths(idx, router)
-        else:
-            table = graph.get_direct_paths(idx, router)
-    except NetGraphError as e:
-        what = "compute shortest paths" if use_shortest_paths else "get the direct paths"
-        raise type(e)(e.code, f"Failed to {what} between graph nodes: {e.message}") from e
-    return RoutingInfo(table, [graph.node_index_to_id(i) for i in idx])
+    """sim_config.rs:425-462 through srg_routing_info_build: GML ids -> NodeIndex, shortest or
+    direct paths on the GPU, a dense RoutingInfo keyed by GML id (no n^2 HashMap)."""
+    router = router or Router.default()
+    ids = np.ascontiguousarray(list(nodes), dtype=np.uint32)
+    edges = graph.edges if isinstance(graph, NetworkGraph) else graph
+    if edges.node_ids is None and isinstance(graph, NetworkGraph):
+        edges = Edges(edges.num_vertices, edges.src, edges.dst, edges.latency_ns, edges.packet_loss, edges.directed,
+                      graph._ids)
+    el = edges.as_struct()
+    h = ctypes.c_void_p()
+    st = N.Stats()
+    err = ctypes.create_string_buffer(2048)
+    rc = N.lib().srg_routing_info_build(router._h, ctypes.byref(el), ids.ctypes.data, len(ids),
+                                        1 if use_shortest_paths else 0, ctypes.byref(h), ctypes.byref(st), err,
+                                        len(err))
+    if rc != N.SRG_OK:
+        _raise(rc, err.value.decode(errors="replace"))
+    return RoutingInfo(h, st.as_dict())

@@ -173,6 +173,21 @@ def test_unused_isolated_vertex_keeps_u32(router):
         router.compute_shortest_paths(iso2, list(range(101)))
 
 
+def test_latency_range_is_an_error(router):
+    """Documented divergence: when a path sum could reach 2^62 ns the library
+    returns SRG_ERR_LATENCY_RANGE, where the release build of the reference would wrap u64
+    silently (mod.rs:327 `+` on u64, overflow checks off in src/Cargo.toml:56-61).  The Rust
+    binding panics on it, like the `.unwrap()` of an overflowing unit conversion (mod.rs:336)."""
+    big = 2 ** 61
+    e = Edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [1, 1, 1, big, big], [0.0] * 5, False)
+    with pytest.raises(NetGraphError) as ei:
+        router.compute_shortest_paths(e, [0, 1, 2])
+    assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
+    ok = Edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [1, 1, 1, 2 ** 40, 2 ** 40], [0.0] * 5, False)
+    t = router.compute_shortest_paths(ok, [0, 1, 2])
+    assert t[(0, 2)].latency_ns == 2 ** 41 and t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+
+
 def test_deterministic_bytes(router):
     g = synth.random_graph(150, 0.2, 9, lat_hi=4, parallel=0.2)
     a = router.compute_shortest_paths(g, list(range(150)))
@@ -210,17 +225,39 @@ def test_direct_paths_vs_oracle(router):
 
 
 def test_generate_routing_info_ids(router):
+    """f1: generate_routing_info (sim_config.rs:425-462) through srg_routing_info_build -- a dense
+    RoutingInfo keyed by GML id: path() by id (None for unknown ids), get_smallest_latency_ns over
+    all entries incl. the diagonal (mod.rs:474-476), saturating packet counters (mod.rs:449-456),
+    direct paths, and the reference's error context."""
     txt = synth.to_gml(synth.random_graph(20, 0.4, 3, lat_hi=9), node_ids=[100 + 3 * i for i in range(20)])
     g = NetworkGraph.parse(txt)
-    ids = {100, 103, 130, 157}
-    ri = generate_routing_info(g, ids, True, router)
+    ids = [157, 100, 130, 103]
+    ri = generate_routing_info(g, set(ids), True, router)
     idx = [g.node_id_to_index(x) for x in ids]
     lat, loss = oracle.compute_shortest_paths(g.edges.as_tuple(), idx)
     for i, a in enumerate(ids):
         for j, b in enumerate(ids):
             p = ri.path(a, b)
             assert p.latency_ns == int(lat[i, j]) and np.float32(p.packet_loss) == loss[i, j]
+    assert ri.path(100, 101) is None and ri.path(999, 100) is None
     assert ri.get_smallest_latency_ns() == int(lat.min())
+    assert len(ri) == 16
+    for _ in range(3):
+        ri.increment_packet_count(100, 157)
+    assert ri.packet_count(100, 157) == 3 and ri.packet_count(157, 100) == 0
+    tl, tf, tid = ri.tables()
+    assert sorted(tid.tolist()) == sorted(ids) and tl.shape == (4, 4)
+    # use_shortest_path = false: direct edges; the KAT graph lacks 1->2 (mod.rs:266-268)
+    kg = NetworkGraph.parse(kat_gml(True))
+    with pytest.raises(NetGraphError, match="Failed to get the direct paths between graph nodes: No edge connecting"):
+        generate_routing_info(kg, {0, 1, 2}, False, router)
+    d = generate_routing_info(kg, {0, 1}, False, router)
+    assert d.path(0, 1).latency_ns == 3 and d.path(1, 0).latency_ns == 5
+    assert d.get_smallest_latency_ns() == 3
+    with pytest.raises(NetGraphError, match="unwrap"):
+        generate_routing_info(g, {100, 5}, True, router)  # id 5 is not a node (sim_config.rs:433)
+    empty = generate_routing_info(g, set(), True, router)
+    assert empty.get_smallest_latency_ns() is None and len(empty) == 0
 
 
 def test_device_entry_matches_host(router):

@@ -92,7 +92,13 @@ def test_bf_global_bitmaps(bf_router, kw):
     V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
     g = synth.random_graph(V, dens, seed, **kw)
     nodes = list(range(V))
-    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    try:
+        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    except oracle.OracleError as e:
+        with pytest.raises(NetGraphError) as ei:
+            bf_router.compute_shortest_paths(g, nodes)
+        assert ei.value.code == e.code
+        return
     t = bf_router.compute_shortest_paths(g, nodes)
     assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
