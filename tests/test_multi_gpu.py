@@ -123,3 +123,30 @@ def test_rccl_single_rank():
     lat, loss = oracle.compute_shortest_paths(e.as_tuple(), list(range(200)))
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
     r.close()
+
+
+@pytest.fixture(scope="module")
+def c3_single():
+    """Config C3 (atlas_like(10000, seed=10000)) built by one rank: the reference table."""
+    e = synth.atlas_like(10000, seed=10000)
+    r = Router(0)
+    t = r.compute_shortest_paths(e, list(range(10000)))
+    r.close()
+    assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
+    return e, t
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("G", [2, 8])
+def test_c3_full_size_ranks_match_single_gpu(c3_single, G):
+    """The multi-rank build at full C3 size (10 000 vertices, 5e7 edges): G in-process ranks on one
+    GPU (row-block FW with per-pivot panel broadcasts, essential-mask exchange, output row
+    exchange) -- every rank ends with the single-GPU table bit for bit."""
+    e, ref = c3_single
+    out, errs = run_ranks(G, e, list(range(10000)))
+    assert errs == [None] * G, errs
+    for r, t in enumerate(out):
+        assert t.stats["nranks"] == G and t.stats["rank"] == r
+        assert np.array_equal(t.latency_ns, ref.latency_ns), f"rank {r} latency"
+        assert bits_equal(t.packet_loss, ref.packet_loss), f"rank {r} loss"
+    assert sum(t.stats["local_sources"] for t in out) == 10000
