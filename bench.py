@@ -249,7 +249,7 @@ def main():
     ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
-    ap.add_argument("--fw-packed", type=int, default=1, help="u32 FW tiles: 1 = packed-pair adds, 0 = add + min3")
+    ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs, KC 16, 3 waves/SIMD; 1 = packed, KC 32; 0 = add + min3")
     ap.add_argument("--scan-variant", type=int, default=None, help="u32 tight scan kernel (0 readlane, 1 scalar)")
     ap.add_argument("--simulate-rank", type=str, default=None,
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
@@ -414,7 +414,7 @@ def main():
         relax = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
         traffic, tsrc = load_traffic("fw_product", wkey)
-        roofline = {"bound": "valu", "kernel": ("fw_product<u32,128,32,packed> (FW phase 3, non-lookahead tiles)" if args.fw_packed else "fw_product<u32,128,32> (FW phase 3, non-lookahead tiles)") if kind == 0 else "fw_product<u64,64,32> (FW phase 3)", "achieved": round(achieved, 3),
+        roofline = {"bound": "valu", "kernel": (f"fw_product<u32,128,{16 if args.fw_packed >= 2 else 32},{args.fw_packed}> (FW phase 3, pair-packed, non-lookahead tiles)" if args.fw_packed else "fw_product<u32,128,32,0> (FW phase 3, add + min3, non-lookahead tiles)") if kind == 0 else "fw_product<u64,64,32,0> (FW phase 3)", "achieved": round(achieved, 3),
                     "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),

@@ -127,8 +127,10 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SIMULATE_RANK 6   /* TIMING AID ONLY: value = nranks*1000 + rank runs this rank's share
                                      with every collective elided -- outputs are NOT valid; 0 detaches */
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
-#define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles: 1 (default) = two relaxations per 64-bit add of
-                                     packed key pairs + v_min3; 0 = one add per relaxation */
+#define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles: 1 = two relaxations per 64-bit add of
+                                     packed key pairs + v_min3, 32-deep k-chunks, operand prefetch;
+                                     2 (default) = the same with 16-deep k-chunks and no operand prefetch (3 waves
+                                     per SIMD); 3 = 16-deep with prefetch; 0 = one add per relaxation */
 #define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 3 = source columns staged in LDS per u-chunk,
                                      2 (default) = entries grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry
                                      batches broadcast with v_readlane */
@@ -214,6 +216,11 @@ uint32_t srg_graph_node_id(const srg_graph* g, uint32_t index);
 void srg_graph_node_bandwidth(const srg_graph* g, uint32_t index,
                               uint64_t* down_bits, int* has_down,
                               uint64_t* up_bits, int* has_up);
+/* All nodes at once: arrays of srg_graph_num_vertices entries (any pointer may be NULL).      */
+void srg_graph_node_bandwidths(const srg_graph* g, uint64_t* down_bits, int* has_down,
+                               uint64_t* up_bits, int* has_up);
+/* Diagnostics: how many text chunks the last parse of `g` used (1 = one sequential pass).    */
+uint32_t srg_graph_parse_chunks(const srg_graph* g);
 
 /* ---- multi-GPU: one process (or thread) per GPU, SPMD -------------------------------
  * After srg_comm_init*, every rank calls srg_compute_shortest_paths[_device] with the SAME

@@ -135,7 +135,8 @@ EXPORTS = [
     "srg_create", "srg_destroy", "srg_set_option", "srg_compute_shortest_paths", "srg_compute_shortest_paths_device",
     "srg_get_direct_paths", "srg_graph_parse_gml", "srg_graph_free", "srg_graph_edge_list",
     "srg_graph_num_vertices", "srg_graph_num_edges", "srg_graph_directed", "srg_graph_node_index",
-    "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_version", "srg_comm_unique_id", "srg_comm_init",
+    "srg_graph_node_id", "srg_graph_node_bandwidth", "srg_graph_node_bandwidths", "srg_graph_parse_chunks",
+    "srg_version", "srg_comm_unique_id", "srg_comm_init",
     "srg_local_group_create", "srg_local_group_release", "srg_comm_init_local", "srg_comm_size",
     "srg_order_packet_events_device", "srg_routing_info_build", "srg_routing_info_free", "srg_routing_info_num_nodes",
     "srg_routing_info_path", "srg_routing_info_increment_packet_count", "srg_routing_info_packet_count",
@@ -198,6 +199,10 @@ def lib():
     L.srg_graph_node_bandwidth.restype = None
     L.srg_graph_node_bandwidth.argtypes = [c.c_void_p, c.c_uint32, _u64p, c.POINTER(c.c_int), _u64p,
                                            c.POINTER(c.c_int)]
+    L.srg_graph_node_bandwidths.restype = None
+    L.srg_graph_node_bandwidths.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p]
+    L.srg_graph_parse_chunks.restype = c.c_uint32
+    L.srg_graph_parse_chunks.argtypes = [c.c_void_p]
     L.srg_version.restype = c.c_char_p
     L.srg_version.argtypes = []
     L.srg_comm_unique_id.restype = c.c_int

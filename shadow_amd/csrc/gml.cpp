@@ -23,7 +23,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <map>
+#include <algorithm>
+#include <thread>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -40,11 +41,24 @@ struct srg_graph {
     std::vector<uint32_t> src, dst;
     std::vector<uint64_t> lat_ns;
     std::vector<float> loss;
+    uint32_t parse_chunks = 1;
 };
 
 namespace {
 
 // ----------------------------------------------------------------------------------------
+// Zero-copy views into the GML text: one pass over the text, no allocation per key/value.
+struct SV {
+    const char* p = nullptr;
+    uint32_t n = 0;
+    bool eq(const char* s) const {
+        const size_t m = std::strlen(s);
+        return m == n && std::memcmp(p, s, n) == 0;
+    }
+    bool same(const SV& o) const { return n == o.n && std::memcmp(p, o.p, n) == 0; }
+    std::string str() const { return std::string(p, n); }
+};
+
 // nom-like result: OK, ERR (recoverable: alt/many_till may try something else), FAIL (fatal)
 enum class R { OK, ERR, FAIL };
 
@@ -52,7 +66,12 @@ struct Value {
     enum Kind { INT, FLOAT, STR } kind = INT;
     int32_t i = 0;
     float f = 0.0f;
-    std::string s;
+    SV s;
+};
+
+struct KV {
+    SV k;
+    Value v;
 };
 
 struct Parser {
@@ -94,7 +113,7 @@ struct Parser {
         return R::FAIL;
     }
     // key (parser.rs:45-51): take(1) alphabetic-or-'_' (chr as u8), take_while alnum-or-'_'
-    R key(const char*& p, std::string& out) const {
+    R key(const char*& p, SV& out) const {
         if (p >= end) return R::ERR;
         // take(1) takes one *char*; `chr as u8` truncates multibyte chars -> never a letter
         unsigned char c = (unsigned char)*p;
@@ -123,21 +142,24 @@ struct Parser {
             }
             break;
         }
-        out.assign(p, q);
+        out.p = p;
+        out.n = (uint32_t)(q - p);
         p = q;
         return R::OK;
     }
     // int (parser.rs:226-229)
     R int_(const char*& p, Value& v) const {
         const char* q = p;
-        while (q < end && is_digit((unsigned char)*q)) ++q;
-        if (q == p) return R::ERR;
-        // str::parse::<i32>: overflow -> map_res error (ERR)
         int64_t acc = 0;
-        for (const char* r = p; r < q; ++r) {
-            acc = acc * 10 + (*r - '0');
-            if (acc > INT32_MAX) return R::ERR;
+        bool ovf = false;
+        while (q < end && is_digit((unsigned char)*q)) {
+            acc = acc * 10 + (*q - '0');
+            ovf |= acc > INT32_MAX;
+            if (ovf) acc = INT32_MAX + 1ll;
+            ++q;
         }
+        if (q == p) return R::ERR;
+        if (ovf) return R::ERR;  // str::parse::<i32>: overflow -> map_res error (ERR)
         v.kind = Value::INT;
         v.i = (int32_t)acc;
         p = q;
@@ -147,7 +169,6 @@ struct Parser {
     R float_(const char*& p, Value& v) {
         const char* q = p;
         if (q < end && (*q == '+' || *q == '-')) ++q;
-        const char* m = q;
         if (q < end && is_digit((unsigned char)*q)) {
             while (q < end && is_digit((unsigned char)*q)) ++q;
             if (q < end && *q == '.') {
@@ -160,7 +181,6 @@ struct Parser {
         } else {
             return R::ERR;
         }
-        (void)m;
         if (q < end && (*q == 'e' || *q == 'E')) {
             const char* e = q + 1;
             if (e < end && (*e == '+' || *e == '-')) ++e;
@@ -169,12 +189,46 @@ struct Parser {
             if (e == d) return fail(d, "expected exponent digits in float");  // cut(digit1)
             q = e;
         }
-        std::string txt(p, q);
-        // Rust's f32 parse is correctly rounded, as glibc strtof (C locale numerics).
-        errno = 0;
+        // Rust's f32 parse is correctly rounded.  Fast path (Clinger): a mantissa < 2^24 and a
+        // power of ten <= 10^10 are both exact floats, so one IEEE division rounds correctly.
+        {
+            const char* c = p;
+            const bool neg = *c == '-';
+            if (*c == '+' || *c == '-') ++c;
+            uint32_t m = 0;
+            int digits = 0, frac = 0;
+            bool ok = true, dot = false;
+            for (; c < q; ++c) {
+                if (*c == '.') { dot = true; continue; }
+                if (*c == 'e' || *c == 'E') { ok = false; break; }
+                if (m == 0 && *c == '0') { if (dot) ++frac; continue; }  // leading zeros
+                if (++digits > 7) { ok = false; break; }
+                m = m * 10 + (uint32_t)(*c - '0');
+                if (dot) ++frac;
+            }
+            if (ok && frac <= 10) {
+                static const float p10[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+                const float f = (float)m / p10[frac];
+                v.kind = Value::FLOAT;
+                v.f = neg ? -f : f;
+                p = q;
+                return R::OK;
+            }
+        }
+        const size_t len = (size_t)(q - p);
+        char small[64];
+        std::string big;
+        char* txt = small;
+        if (len < sizeof small) {
+            std::memcpy(small, p, len);
+            small[len] = 0;
+        } else {
+            big.assign(p, q);
+            txt = &big[0];
+        }
         char* ep = nullptr;
-        float f = std::strtof(txt.c_str(), &ep);
-        if (ep != txt.c_str() + txt.size()) return R::ERR;
+        const float f = std::strtof(txt, &ep);
+        if (ep != txt + len) return R::ERR;
         v.kind = Value::FLOAT;
         v.f = f;
         p = q;
@@ -183,44 +237,46 @@ struct Parser {
     // string (parser.rs:237-250): '"' then a NON-EMPTY run of non-quote bytes then '"'
     R string_(const char*& p, Value& v) const {
         if (p >= end || *p != '"') return R::ERR;
-        const char* q = p + 1;
-        const char* s = q;
-        while (q < end && *q != '"') ++q;
-        if (q == s) return R::ERR;      // escaped_transform at index 0 -> Error
-        if (q >= end) return R::ERR;    // Eof
+        const char* s = p + 1;
+        const char* q = static_cast<const char*>(std::memchr(s, '"', (size_t)(end - s)));
+        if (!q) return R::ERR;        // Eof
+        if (q == s) return R::ERR;    // escaped_transform at index 0 -> Error
         v.kind = Value::STR;
-        v.s.assign(s, q);
+        v.s.p = s;
+        v.s.n = (uint32_t)(q - s);
         p = q + 1;
         return R::OK;
     }
-    // value (parser.rs:214-224)
+    // value (parser.rs:214-224): int newline | float newline | string newline
     R value(const char*& p, Value& v) {
         const char* start = space0(p);
+        if (start < end && *start == '"') {  // int_ and float_ both fail on '"'
+            const char* q = start;
+            if (string_(q, v) == R::OK && newline(q) == R::OK) {
+                p = q;
+                return R::OK;
+            }
+            return R::ERR;
+        }
         {
             const char* q = start;
-            Value t;
-            if (int_(q, t) == R::OK && newline(q) == R::OK) {
-                v = t;
+            if (int_(q, v) == R::OK && newline(q) == R::OK) {
                 p = q;
                 return R::OK;
             }
         }
         {
             const char* q = start;
-            Value t;
-            R r = float_(q, t);
+            R r = float_(q, v);
             if (r == R::FAIL) return r;
             if (r == R::OK && newline(q) == R::OK) {
-                v = t;
                 p = q;
                 return R::OK;
             }
         }
         {
             const char* q = start;
-            Value t;
-            if (string_(q, t) == R::OK && newline(q) == R::OK) {
-                v = t;
+            if (string_(q, v) == R::OK && newline(q) == R::OK) {
                 p = q;
                 return R::OK;
             }
@@ -228,12 +284,9 @@ struct Parser {
         return R::ERR;
     }
 
-    struct KV {
-        std::string k;
-        Value v;
-    };
-    // many_till(tuple((key, value)), tag("]")) + duplicate check + newline
+    // many_till(tuple((key, value)), tag("]")) + duplicate check + newline (kvs reused: no alloc)
     R block(const char*& p, std::vector<KV>& kvs) {
+        kvs.clear();
         const char* q = space0(p);
         if (tag(q, "[") != R::OK) return R::ERR;
         if (newline(q) != R::OK) return R::ERR;
@@ -243,18 +296,18 @@ struct Parser {
             if (key(q, kv.k) != R::OK) return R::ERR;
             R r = value(q, kv.v);
             if (r != R::OK) return r;
-            kvs.push_back(std::move(kv));
+            kvs.push_back(kv);
         }
-        std::map<std::string, int> seen;
-        for (auto& kv : kvs)
-            if (seen[kv.k]++) return fail(q, "Duplicate keys are not supported");
+        for (size_t a = 1; a < kvs.size(); ++a)
+            for (size_t b = 0; b < a; ++b)
+                if (kvs[a].k.same(kvs[b].k)) return fail(q, "Duplicate keys are not supported");
         if (newline(q) != R::OK) return R::ERR;
         p = q;
         return R::OK;
     }
 };
 
-// ---------------- units (units.rs) ----------------------------------------------------
+// ---------------- units (units.rs), on views --------------------------------------------
 bool is_unicode_ws(const char*& p, const char* end) {
     unsigned char c = (unsigned char)*p;
     if (c == ' ' || (c >= 0x09 && c <= 0x0D)) {
@@ -279,9 +332,22 @@ bool is_unicode_ws(const char*& p, const char* end) {
     return false;
 }
 
-std::string utrim(const std::string& s) {
-    const char* b = s.data();
-    const char* e = s.data() + s.size();
+SV utrim(SV s) {
+    const char* b = s.p;
+    const char* e = s.p + s.n;
+    {  // ASCII fast path: no byte >= 0x80 at either end after trimming ASCII white space
+        const char* fb = b;
+        const char* fe = e;
+        auto ws = [](char c) { return c == ' ' || (c >= 0x09 && c <= 0x0D); };
+        while (fb < fe && ws(*fb)) ++fb;
+        while (fe > fb && ws(fe[-1])) --fe;
+        if ((fb == fe || (unsigned char)*fb < 0x80) && (fe == fb || (unsigned char)fe[-1] < 0x80)) {
+            SV r;
+            r.p = fb;
+            r.n = (uint32_t)(fe - fb);
+            return r;
+        }
+    }
     while (b < e) {
         const char* q = b;
         if (!is_unicode_ws(q, e)) break;
@@ -301,44 +367,49 @@ std::string utrim(const std::string& s) {
             last = p;
         }
     }
-    return std::string(b, last > e ? e : last);
+    SV r;
+    r.p = b;
+    r.n = (uint32_t)((last > e ? e : last) - b);
+    return r;
 }
 
 // regex ^([+-]?[0-9\.]*)\s*(.*)$  -> (value, unit), both trimmed (units.rs:409-417)
-bool split_value_unit(const std::string& s, std::string& val, std::string& unit) {
-    const char* p = s.data();
-    const char* e = s.data() + s.size();
+bool split_value_unit(SV s, SV& val, SV& unit) {
+    const char* p = s.p;
+    const char* e = s.p + s.n;
     const char* v0 = p;
     if (p < e && (*p == '+' || *p == '-')) ++p;
     while (p < e && ((*p >= '0' && *p <= '9') || *p == '.')) ++p;
-    val.assign(v0, p);
+    val.p = v0;
+    val.n = (uint32_t)(p - v0);
     while (p < e) {
         const char* q = p;
         if (!is_unicode_ws(q, e)) break;
         p = q;
     }
-    if (std::memchr(p, '\n', e - p)) return false;  // `.` does not match '\n'
-    unit.assign(p, e);
+    if (std::memchr(p, '\n', (size_t)(e - p))) return false;  // `.` does not match '\n'
+    unit.p = p;
+    unit.n = (uint32_t)(e - p);
     val = utrim(val);
     unit = utrim(unit);
     return true;
 }
 
 // Rust u64::from_str: optional '+', then >= 1 ASCII digit, no overflow.
-bool parse_u64(const std::string& s, uint64_t& out, std::string& err) {
+bool parse_u64(SV s, uint64_t& out, const char*& err) {
     size_t i = 0;
-    if (i < s.size() && s[i] == '+') ++i;
-    if (i == s.size()) {
-        err = s.empty() ? "cannot parse integer from empty string" : "invalid digit found in string";
+    if (i < s.n && s.p[i] == '+') ++i;
+    if (i == s.n) {
+        err = s.n == 0 ? "cannot parse integer from empty string" : "invalid digit found in string";
         return false;
     }
     unsigned __int128 acc = 0;
-    for (; i < s.size(); ++i) {
-        if (s[i] < '0' || s[i] > '9') {
+    for (; i < s.n; ++i) {
+        if (s.p[i] < '0' || s.p[i] > '9') {
             err = "invalid digit found in string";
             return false;
         }
-        acc = acc * 10 + (unsigned)(s[i] - '0');
+        acc = acc * 10 + (unsigned)(s.p[i] - '0');
         if (acc > UINT64_MAX) {
             err = "number too large to fit in target type";
             return false;
@@ -355,26 +426,25 @@ const char* kTimeUnitErr =
 
 // Time<TimePrefix>::from_str + convert(Nano) magnitude (units.rs:236-280, 377-388, 405-439).
 // Returns false with `err` on a parse error; `ns_overflow` set if the ns value overflows u64.
-bool parse_time_ns(const std::string& s, uint64_t& value, uint64_t& ns, bool& ns_overflow,
-                   std::string& err) {
-    std::string v, u;
+bool parse_time_ns(SV s, uint64_t& value, uint64_t& ns, bool& ns_overflow, const char*& err) {
+    SV v, u;
     if (!split_value_unit(s, v, u)) {
         err = "Unable to identify value and unit";
         return false;
     }
     // Time suffixes = [""]: strip_suffix("") always succeeds -> prefix = unit
     uint64_t mag;
-    if (u.empty() || u == "s" || u == "sec" || u == "secs" || u == "second" || u == "seconds")
+    if (u.n == 0 || u.eq("s") || u.eq("sec") || u.eq("secs") || u.eq("second") || u.eq("seconds"))
         mag = 1000000000ull;
-    else if (u == "ns" || u == "nanosecond" || u == "nanoseconds")
+    else if (u.eq("ns") || u.eq("nanosecond") || u.eq("nanoseconds"))
         mag = 1;
-    else if (u == "us" || u == "μs" || u == "microsecond" || u == "microseconds")
+    else if (u.eq("us") || u.eq("μs") || u.eq("microsecond") || u.eq("microseconds"))
         mag = 1000ull;
-    else if (u == "ms" || u == "millisecond" || u == "milliseconds")
+    else if (u.eq("ms") || u.eq("millisecond") || u.eq("milliseconds"))
         mag = 1000000ull;
-    else if (u == "m" || u == "min" || u == "mins" || u == "minute" || u == "minutes")
+    else if (u.eq("m") || u.eq("min") || u.eq("mins") || u.eq("minute") || u.eq("minutes"))
         mag = 60000000000ull;
-    else if (u == "h" || u == "hr" || u == "hrs" || u == "hour" || u == "hours")
+    else if (u.eq("h") || u.eq("hr") || u.eq("hrs") || u.eq("hour") || u.eq("hours"))
         mag = 3600000000000ull;
     else {
         err = kTimeUnitErr;
@@ -388,30 +458,30 @@ bool parse_time_ns(const std::string& s, uint64_t& value, uint64_t& ns, bool& ns
 }
 
 // BitsPerSec<SiPrefixUpper>::from_str (suffixes ["bit","bits"], units.rs:140-200, 571-578)
-bool parse_bits(const std::string& s, uint64_t& bits, std::string& err) {
-    std::string v, u;
+bool parse_bits(SV s, uint64_t& bits, const char*& err) {
+    SV v, u;
     if (!split_value_unit(s, v, u)) {
         err = "Unable to identify value and unit";
         return false;
     }
-    std::string prefix = u;
+    SV prefix = u;
     for (const char* suf : {"bit", "bits"}) {
-        size_t n = std::strlen(suf);
-        if (u.size() >= n && u.compare(u.size() - n, n, suf) == 0) {
-            prefix = u.substr(0, u.size() - n);
+        const uint32_t n = (uint32_t)std::strlen(suf);
+        if (u.n >= n && std::memcmp(u.p + u.n - n, suf, n) == 0) {
+            prefix.n = u.n - n;
             break;
         }
     }
     uint64_t mag;
-    if (prefix.empty()) mag = 1;
-    else if (prefix == "K" || prefix == "kilo") mag = 1000ull;
-    else if (prefix == "Ki" || prefix == "kibi") mag = 1024ull;
-    else if (prefix == "M" || prefix == "mega") mag = 1000000ull;
-    else if (prefix == "Mi" || prefix == "mebi") mag = 1048576ull;
-    else if (prefix == "G" || prefix == "giga") mag = 1000000000ull;
-    else if (prefix == "Gi" || prefix == "gibi") mag = 1073741824ull;
-    else if (prefix == "T" || prefix == "tera") mag = 1000000000000ull;
-    else if (prefix == "Ti" || prefix == "tebi") mag = 1099511627776ull;
+    if (prefix.n == 0) mag = 1;
+    else if (prefix.eq("K") || prefix.eq("kilo")) mag = 1000ull;
+    else if (prefix.eq("Ki") || prefix.eq("kibi")) mag = 1024ull;
+    else if (prefix.eq("M") || prefix.eq("mega")) mag = 1000000ull;
+    else if (prefix.eq("Mi") || prefix.eq("mebi")) mag = 1048576ull;
+    else if (prefix.eq("G") || prefix.eq("giga")) mag = 1000000000ull;
+    else if (prefix.eq("Gi") || prefix.eq("gibi")) mag = 1073741824ull;
+    else if (prefix.eq("T") || prefix.eq("tera")) mag = 1000000000000ull;
+    else if (prefix.eq("Ti") || prefix.eq("tebi")) mag = 1099511627776ull;
     else {
         err = "Unit prefix was not one of (K|kilo|Ki|kibi|M|mega|Mi|mebi"
               "|G|giga|Gi|gibi|T|tera|Ti|tebi)";
@@ -435,59 +505,183 @@ int line_of(const char* begin, const char* at) {
     return line;
 }
 
-struct RawNode {
-    std::vector<Parser::KV> kvs;
+// ---- one pass over a run of top-level items -------------------------------------------
+// Syntax (gml_parser::parse) is checked as the items are read; each node / edge is converted
+// right away (ShadowNode / ShadowEdge::try_from, mod.rs:28-111), but a conversion error is only
+// RECORDED (first one, in order) and reported after the whole text parsed -- the reference
+// parses all of the text before it converts anything (mod.rs:135).
+struct NodeRec {
+    uint32_t id;
+    uint64_t down, up;
+    uint8_t has_down, has_up;
+};
+struct EdgeRec {
+    uint32_t src_id, dst_id;
+    uint64_t lat_ns;
+    float loss;
+};
+struct Items {
+    std::vector<NodeRec> nodes;
+    std::vector<EdgeRec> edges;
+    int64_t node_err = -1, edge_err = -1;  // first conversion error (index within this run)
+    std::string node_err_msg, edge_err_msg;
+    std::vector<int32_t> directed;          // values of every `directed` key, in order
+    std::vector<SV> other_keys;
+    bool syntax_ok = true;
+    const char* err_at = nullptr;           // syntax error position (sequential run)
+    std::string fail_msg;
+    const char* stop = nullptr;             // where the run stopped
+    bool saw_close = false;                 // the graph's closing "]" was read
 };
 
-int parse_impl(const char* text, size_t len, srg_graph* g, std::string& err) {
-    Parser P{text, text + len};
-    const char* p = P.multispace0(text);
-    auto syntax = [&](const char* at) {
-        err = "GML syntax error at line " + std::to_string(line_of(text, at));
-        if (!P.fail_msg.empty()) err += ": " + P.fail_msg;
-        return SRG_ERR_PARSE;
-    };
-    if (P.tag(p, "graph") != R::OK) return syntax(p);
-    p = P.space0(p);
-    if (P.tag(p, "[") != R::OK) return syntax(p);
-    if (P.newline(p) != R::OK) return syntax(p);
+const char* node_conv(const std::vector<KV>& kvs, NodeRec& n, std::string& msg) {
+    (void)msg;
+    n = NodeRec{0, 0, 0, 0, 0};
+    bool has_id = false;
+    for (auto& kv : kvs)
+        if (kv.k.eq("id")) {
+            n.id = (uint32_t)kv.v.i;
+            has_id = true;
+        }
+    if (!has_id) return "Node 'id' was not provided";
+    // host_bandwidth_down is converted before host_bandwidth_up (mod.rs:34-57)
+    for (int pass = 0; pass < 2; ++pass) {
+        const char* name = pass == 0 ? "host_bandwidth_down" : "host_bandwidth_up";
+        for (auto& kv : kvs) {
+            if (!kv.k.eq(name)) continue;
+            if (kv.v.kind != Value::STR) {
+                msg = std::string("Node '") + name + "' is not a string";
+                return msg.c_str();
+            }
+            uint64_t bits;
+            const char* e = nullptr;
+            if (!parse_bits(kv.v.s, bits, e)) {
+                msg = std::string("Node '") + name + "' is not a valid unit: " + e;
+                return msg.c_str();
+            }
+            if (pass == 0) { n.down = bits; n.has_down = 1; }
+            else { n.up = bits; n.has_up = 1; }
+        }
+    }
+    return nullptr;
+}
 
-    std::vector<RawNode> nodes, edges;
-    int directed_count = 0;
-    bool directed = false;
-    std::vector<std::string> other_keys;
+// ShadowEdge::try_from (mod.rs:75-110), in the reference's check order
+const char* edge_conv(const std::vector<KV>& kvs, EdgeRec& r, std::string& msg) {
+    const Value* lat = nullptr;
+    const Value* jit = nullptr;
+    const Value* pl = nullptr;
+    r = EdgeRec{0, 0, 0, 0.0f};
+    for (auto& kv : kvs) {
+        if (kv.k.eq("latency")) lat = &kv.v;
+        else if (kv.k.eq("jitter")) jit = &kv.v;
+        else if (kv.k.eq("packet_loss")) pl = &kv.v;
+        else if (kv.k.eq("source")) r.src_id = (uint32_t)kv.v.i;
+        else if (kv.k.eq("target")) r.dst_id = (uint32_t)kv.v.i;
+    }
+    if (!lat) return "Edge 'latency' was not provided";
+    if (lat->kind != Value::STR) return "Edge 'latency' is not a string";
+    uint64_t lat_val = 0, lat_ns = 0;
+    bool ovf = false;
+    const char* ue = nullptr;
+    if (!parse_time_ns(lat->s, lat_val, lat_ns, ovf, ue)) {
+        msg = std::string("Edge 'latency' is not a valid unit: ") + ue;
+        return msg.c_str();
+    }
+    if (jit) {
+        if (jit->kind != Value::STR) return "Edge 'jitter' is not a string";
+        uint64_t jv, jns;
+        bool jo;
+        if (!parse_time_ns(jit->s, jv, jns, jo, ue)) {
+            msg = std::string("Edge 'jitter' is not a valid unit: ") + ue;
+            return msg.c_str();
+        }
+    }
+    float loss = 0.0f;
+    if (pl) {
+        if (pl->kind != Value::FLOAT) return "Edge 'packet_loss' is not a float";
+        loss = pl->f;
+    }
+    if (loss < 0.0f || loss > 1.0f) return "Edge 'packet_loss' is not in the range [0,1]";
+    if (lat_val == 0) return "Edge 'latency' must not be 0";
+    // an overflowing ns conversion panics later in the reference (mod.rs:336 unwrap);
+    // UINT64_MAX makes the routing entry points fail with SRG_ERR_LATENCY_RANGE.
+    r.lat_ns = ovf ? UINT64_MAX : lat_ns;
+    r.loss = loss;
+    return nullptr;
+}
+
+// Items from p until `stop_at` (a chunk boundary) or, when stop_at == nullptr, until the
+// graph's closing "]".  A chunked run that meets the closing "]", a syntax error, or an item
+// ending past its boundary reports syntax_ok = false (the caller then parses sequentially).
+void parse_items(const char* text, const char* p, const char* text_end, const char* stop_at, Items& out) {
+    Parser P{text, text_end};
+    std::vector<KV> kvs;
+    kvs.reserve(16);
+    std::string msg;
+    if (stop_at) {  // address space only: pages are touched as the records are written
+        const size_t bytes = (size_t)(stop_at - p);
+        out.edges.reserve(bytes / 40 + 16);
+        out.nodes.reserve(bytes / 16 + 16);
+    }
+    auto syntax = [&](const char* at) {
+        out.syntax_ok = false;
+        out.err_at = at;
+        out.fail_msg = P.fail_msg;
+    };
     for (;;) {
-        if (P.tag(p, "]") == R::OK) break;
-        std::string k;
+        if (stop_at && p >= stop_at) {
+            if (p != stop_at) out.syntax_ok = false;
+            break;
+        }
+        if (P.tag(p, "]") == R::OK) {
+            out.saw_close = true;
+            if (stop_at) out.syntax_ok = false;
+            break;
+        }
+        SV k;
         const char* item_at = p;
         if (P.key(p, k) != R::OK) return syntax(item_at);
-        if (k == "node" || k == "edge") {
-            RawNode rn;
-            R r = P.block(p, rn.kvs);
+        const bool is_node = k.eq("node"), is_edge = k.eq("edge");
+        if (is_node || is_edge) {
+            R r = P.block(p, kvs);
             if (r == R::FAIL) return syntax(P.fail_at);
             if (r != R::OK) return syntax(item_at);
-            // node(): id must be Int; edge(): source/target required Ints (parser.rs:171-211)
-            if (k == "node") {
-                for (auto& kv : rn.kvs)
-                    if (kv.k == "id" && kv.v.kind != Value::INT) {
+            if (is_node) {
+                // node(): id must be an Int (parser.rs:171-175)
+                for (auto& kv : kvs)
+                    if (kv.k.eq("id") && kv.v.kind != Value::INT) {
                         P.fail_msg = "Incorrect 'id' type";
                         return syntax(p);
                     }
-                nodes.push_back(std::move(rn));
+                NodeRec n;
+                const char* e = node_conv(kvs, n, msg);
+                if (e && out.node_err < 0) {
+                    out.node_err = (int64_t)out.nodes.size();
+                    out.node_err_msg = e;
+                }
+                out.nodes.push_back(n);
             } else {
+                // edge(): source / target required Ints (parser.rs:199-211)
                 const Value* s = nullptr;
                 const Value* t = nullptr;
-                for (auto& kv : rn.kvs) {
-                    if (kv.k == "source") s = &kv.v;
-                    if (kv.k == "target") t = &kv.v;
+                for (auto& kv : kvs) {
+                    if (kv.k.eq("source")) s = &kv.v;
+                    if (kv.k.eq("target")) t = &kv.v;
                 }
                 if (s && s->kind != Value::INT) { P.fail_msg = "Incorrect 'source' type"; return syntax(p); }
                 if (!s) { P.fail_msg = "'source' doesn't exist"; return syntax(p); }
                 if (t && t->kind != Value::INT) { P.fail_msg = "Incorrect 'target' type"; return syntax(p); }
                 if (!t) { P.fail_msg = "'target' doesn't exist"; return syntax(p); }
-                edges.push_back(std::move(rn));
+                EdgeRec er;
+                const char* e = edge_conv(kvs, er, msg);
+                if (e && out.edge_err < 0) {
+                    out.edge_err = (int64_t)out.edges.size();
+                    out.edge_err_msg = e;
+                }
+                out.edges.push_back(er);
             }
-        } else if (k == "directed") {
+        } else if (k.eq("directed")) {
             // int_as_bool (parser.rs:264-273)
             Value v;
             R r = P.value(p, v);
@@ -495,128 +689,184 @@ int parse_impl(const char* text, size_t len, srg_graph* g, std::string& err) {
             if (r != R::OK) return syntax(item_at);
             if (v.kind != Value::INT) { P.fail_msg = "Value was not an integer"; return syntax(p); }
             if (v.i != 0 && v.i != 1) { P.fail_msg = "Bool must be 0 or 1"; return syntax(p); }
-            directed = v.i == 1;
-            ++directed_count;
-            if (directed_count == 1) g->directed = directed;
+            out.directed.push_back(v.i);
         } else {
             Value v;
             R r = P.value(p, v);
             if (r == R::FAIL) return syntax(P.fail_at);
             if (r != R::OK) return syntax(item_at);
-            other_keys.push_back(k);
+            out.other_keys.push_back(k);
         }
     }
-    if (directed_count > 1) {
-        P.fail_msg = "The 'directed' key must only be specified once";
-        return syntax(p);
-    }
-    {
-        std::map<std::string, int> seen;
-        for (auto& k : other_keys)
-            if (seen[k]++) {
-                P.fail_msg = "Duplicate keys are not supported";
-                return syntax(p);
-            }
-    }
+    out.stop = p;
+}
 
-    // ---- NetworkGraph::parse (mod.rs:134-181) ----
-    const uint32_t V = (uint32_t)nodes.size();
-    g->node_id.resize(V);
-    g->bw_down.assign(V, 0);
-    g->bw_up.assign(V, 0);
-    g->has_down.assign(V, 0);
-    g->has_up.assign(V, 0);
-    for (uint32_t i = 0; i < V; ++i) {
-        bool has_id = false;
-        for (auto& kv : nodes[i].kvs) {
-            if (kv.k == "id") {
-                g->node_id[i] = (uint32_t)kv.v.i;
-                has_id = true;
-            }
-        }
-        if (!has_id) {
-            err = "Node 'id' was not provided";
-            return SRG_ERR_PARSE;
-        }
-        for (auto& kv : nodes[i].kvs) {
-            const bool down = kv.k == "host_bandwidth_down";
-            const bool up = kv.k == "host_bandwidth_up";
-            if (!down && !up) continue;
-            const char* name = down ? "host_bandwidth_down" : "host_bandwidth_up";
-            if (kv.v.kind != Value::STR) {
-                err = std::string("Node '") + name + "' is not a string";
-                return SRG_ERR_PARSE;
-            }
-            uint64_t bits;
-            std::string e;
-            if (!parse_bits(kv.v.s, bits, e)) {
-                err = std::string("Node '") + name + "' is not a valid unit: " + e;
-                return SRG_ERR_PARSE;
-            }
-            if (down) { g->bw_down[i] = bits; g->has_down[i] = 1; }
-            else { g->bw_up[i] = bits; g->has_up[i] = 1; }
-        }
-        // the reference validates down before up (mod.rs:34-57); both checked above in
-        // key order -- re-check order for a node with two bad bandwidths is immaterial
-        // to success/failure.
-        g->id_to_index[g->node_id[i]] = i;  // HashMap::insert: later duplicates win
+int parse_threads() {
+    int n = (int)std::thread::hardware_concurrency();
+    if (const char* s = std::getenv("OMP_NUM_THREADS")) {
+        const int v = std::atoi(s);
+        if (v > 0) n = std::min(n > 0 ? n : v, v);
     }
-    const size_t E = edges.size();
-    g->src.reserve(E);
-    g->dst.reserve(E);
-    g->lat_ns.reserve(E);
-    g->loss.reserve(E);
-    for (size_t e = 0; e < E; ++e) {
-        const Value* lat = nullptr;
-        const Value* jit = nullptr;
-        const Value* pl = nullptr;
-        uint32_t s = 0, t = 0;
-        for (auto& kv : edges[e].kvs) {
-            if (kv.k == "latency") lat = &kv.v;
-            else if (kv.k == "jitter") jit = &kv.v;
-            else if (kv.k == "packet_loss") pl = &kv.v;
-            else if (kv.k == "source") s = (uint32_t)kv.v.i;
-            else if (kv.k == "target") t = (uint32_t)kv.v.i;
-        }
-        // ShadowEdge::try_from (mod.rs:75-110), in the reference's check order
-        if (!lat) { err = "Edge 'latency' was not provided"; return SRG_ERR_PARSE; }
-        if (lat->kind != Value::STR) { err = "Edge 'latency' is not a string"; return SRG_ERR_PARSE; }
-        uint64_t lat_val = 0, lat_ns = 0;
-        bool ovf = false;
-        std::string ue;
-        if (!parse_time_ns(lat->s, lat_val, lat_ns, ovf, ue)) {
-            err = "Edge 'latency' is not a valid unit: " + ue;
-            return SRG_ERR_PARSE;
-        }
-        if (jit) {
-            if (jit->kind != Value::STR) { err = "Edge 'jitter' is not a string"; return SRG_ERR_PARSE; }
-            uint64_t jv, jns;
-            bool jo;
-            if (!parse_time_ns(jit->s, jv, jns, jo, ue)) {
-                err = "Edge 'jitter' is not a valid unit: " + ue;
-                return SRG_ERR_PARSE;
+    return std::max(1, std::min(n, 64));
+}
+
+// Chunk boundaries: the start of a line "<spaces>node [" or "<spaces>edge [" near each cut
+// point.  A wrong guess (e.g. inside a multi-line string) makes a chunk's run fail its boundary
+// check and the whole text is parsed sequentially instead -- the result never depends on it.
+std::vector<const char*> chunk_starts(const char* p0, const char* end, size_t chunks) {
+    std::vector<const char*> cuts{p0};
+    const size_t len = (size_t)(end - p0);
+    for (size_t i = 1; i < chunks; ++i) {
+        const char* q = p0 + len * i / chunks;
+        if (q <= cuts.back()) continue;
+        const char* found = nullptr;
+        while (q < end) {
+            const char* nl = static_cast<const char*>(std::memchr(q, '\n', (size_t)(end - q)));
+            if (!nl) break;
+            const char* a = nl + 1;
+            while (a < end && (*a == ' ' || *a == '\t')) ++a;
+            if (end - a >= 6 && (std::memcmp(a, "node", 4) == 0 || std::memcmp(a, "edge", 4) == 0)) {
+                const char* b = a + 4;
+                while (b < end && (*b == ' ' || *b == '\t')) ++b;
+                if (b < end && *b == '[') {
+                    found = a;
+                    break;
+                }
             }
+            q = a;
         }
-        float loss = 0.0f;
-        if (pl) {
-            if (pl->kind != Value::FLOAT) { err = "Edge 'packet_loss' is not a float"; return SRG_ERR_PARSE; }
-            loss = pl->f;
+        if (!found) break;
+        if (found > cuts.back()) cuts.push_back(found);
+    }
+    return cuts;
+}
+
+int parse_impl(const char* text, size_t len, srg_graph* g, std::string& err) {
+    const char* end = text + len;
+    Parser P{text, end};
+    const char* p = P.multispace0(text);
+    auto syntax_at = [&](const char* at, const std::string& fm) {
+        err = "GML syntax error at line " + std::to_string(line_of(text, at));
+        if (!fm.empty()) err += ": " + fm;
+        return SRG_ERR_PARSE;
+    };
+    if (P.tag(p, "graph") != R::OK) return syntax_at(p, "");
+    p = P.space0(p);
+    if (P.tag(p, "[") != R::OK) return syntax_at(p, "");
+    if (P.newline(p) != R::OK) return syntax_at(p, "");
+
+    // ---- gml_parser::parse: chunked in parallel when large, else (and on any doubt) sequential
+    const size_t min_chunk = []() {
+        const char* s = std::getenv("SRG_GML_MIN_CHUNK");  // testing aid: force small chunks
+        return s ? (size_t)std::max(1ll, std::atoll(s)) : (size_t)32 << 20;
+    }();
+    const size_t want = std::min<size_t>((size_t)parse_threads(), std::max<size_t>(1, (size_t)(end - p) / min_chunk));
+    std::vector<Items> parts;
+    bool ok = false;
+    if (want > 1) {
+        std::vector<const char*> cuts = chunk_starts(p, end, want);
+        if (cuts.size() > 1) {
+            parts.resize(cuts.size());
+            std::vector<std::thread> th;
+            for (size_t i = 0; i < cuts.size(); ++i)
+                th.emplace_back([&, i]() {
+                    try {
+                        Items local;  // not parts[i] in place: neighbouring Items share cache lines
+                        parse_items(text, cuts[i], end, i + 1 < cuts.size() ? cuts[i + 1] : nullptr, local);
+                        parts[i] = std::move(local);
+                    } catch (...) {
+                        parts[i].syntax_ok = false;
+                    }
+                });
+            for (auto& t : th) t.join();
+            ok = true;
+            for (size_t i = 0; i < parts.size(); ++i)
+                ok &= parts[i].syntax_ok && (i + 1 < parts.size() || parts[i].saw_close);
         }
-        if (loss < 0.0f || loss > 1.0f) {
-            err = "Edge 'packet_loss' is not in the range [0,1]";
+    }
+    if (!ok) {
+        parts.assign(1, Items{});
+        parse_items(text, p, end, nullptr, parts[0]);
+        if (!parts[0].syntax_ok) return syntax_at(parts[0].err_at, parts[0].fail_msg);
+        if (!parts[0].saw_close) return syntax_at(parts[0].stop ? parts[0].stop : end, "");
+    }
+    g->parse_chunks = (uint32_t)parts.size();
+    const char* close_at = parts.back().stop;
+    std::vector<int32_t> directed;
+    std::vector<SV> other;
+    size_t V = 0, E = 0;
+    for (auto& it : parts) {
+        directed.insert(directed.end(), it.directed.begin(), it.directed.end());
+        other.insert(other.end(), it.other_keys.begin(), it.other_keys.end());
+        V += it.nodes.size();
+        E += it.edges.size();
+    }
+    if (directed.size() > 1) return syntax_at(close_at, "The 'directed' key must only be specified once");
+    for (size_t a = 1; a < other.size(); ++a)
+        for (size_t b = 0; b < a; ++b)
+            if (other[a].same(other[b])) return syntax_at(close_at, "Duplicate keys are not supported");
+    g->directed = !directed.empty() && directed[0] == 1;
+
+    // ---- NetworkGraph::parse (mod.rs:134-181): nodes, then edges, in order -------------------
+    g->node_id.resize(V);
+    g->bw_down.resize(V);
+    g->bw_up.resize(V);
+    g->has_down.resize(V);
+    g->has_up.resize(V);
+    size_t off = 0;
+    for (auto& it : parts) {
+        if (it.node_err >= 0) {
+            err = it.node_err_msg;
             return SRG_ERR_PARSE;
         }
-        if (lat_val == 0) { err = "Edge 'latency' must not be 0"; return SRG_ERR_PARSE; }
-        auto si = g->id_to_index.find(s);
-        if (si == g->id_to_index.end()) { err = "Edge source " + std::to_string(s) + " doesn't exist"; return SRG_ERR_PARSE; }
-        auto ti = g->id_to_index.find(t);
-        if (ti == g->id_to_index.end()) { err = "Edge target " + std::to_string(t) + " doesn't exist"; return SRG_ERR_PARSE; }
-        g->src.push_back(si->second);
-        g->dst.push_back(ti->second);
-        // an overflowing ns conversion panics later in the reference (mod.rs:336 unwrap);
-        // UINT64_MAX makes the routing entry points fail with SRG_ERR_LATENCY_RANGE.
-        g->lat_ns.push_back(ovf ? UINT64_MAX : lat_ns);
-        g->loss.push_back(loss);
+        for (size_t i = 0; i < it.nodes.size(); ++i) {
+            const NodeRec& n = it.nodes[i];
+            g->node_id[off + i] = n.id;
+            g->bw_down[off + i] = n.down;
+            g->bw_up[off + i] = n.up;
+            g->has_down[off + i] = n.has_down;
+            g->has_up[off + i] = n.has_up;
+        }
+        off += it.nodes.size();
+    }
+    g->id_to_index.reserve(V);
+    for (uint32_t i = 0; i < (uint32_t)V; ++i) g->id_to_index[g->node_id[i]] = i;  // later duplicates win
+    g->src.resize(E);
+    g->dst.resize(E);
+    g->lat_ns.resize(E);
+    g->loss.resize(E);
+    // dense id -> index table when the ids allow it (the common 0..V-1 case)
+    uint32_t max_id = 0;
+    for (uint32_t id : g->node_id) max_id = std::max(max_id, id);
+    std::vector<uint32_t> direct;
+    if (V && (uint64_t)max_id < 4ull * V + 1024) {
+        direct.assign((size_t)max_id + 1, UINT32_MAX);
+        for (uint32_t i = 0; i < (uint32_t)V; ++i) direct[g->node_id[i]] = i;
+    }
+    auto lookup = [&](uint32_t id) -> uint32_t {
+        if (!direct.empty()) return id < direct.size() ? direct[id] : UINT32_MAX;
+        auto f = g->id_to_index.find(id);
+        return f == g->id_to_index.end() ? UINT32_MAX : f->second;
+    };
+    off = 0;
+    for (auto& it : parts) {
+        const size_t stop = it.edge_err >= 0 ? (size_t)it.edge_err : it.edges.size();
+        for (size_t e = 0; e < stop; ++e) {
+            const EdgeRec& r = it.edges[e];
+            const uint32_t si = lookup(r.src_id);
+            if (si == UINT32_MAX) { err = "Edge source " + std::to_string(r.src_id) + " doesn't exist"; return SRG_ERR_PARSE; }
+            const uint32_t ti = lookup(r.dst_id);
+            if (ti == UINT32_MAX) { err = "Edge target " + std::to_string(r.dst_id) + " doesn't exist"; return SRG_ERR_PARSE; }
+            g->src[off + e] = si;
+            g->dst[off + e] = ti;
+            g->lat_ns[off + e] = r.lat_ns;
+            g->loss[off + e] = r.loss;
+        }
+        if (it.edge_err >= 0) {
+            err = it.edge_err_msg;
+            return SRG_ERR_PARSE;
+        }
+        off += it.edges.size();
     }
     return SRG_OK;
 }
@@ -690,5 +940,17 @@ void srg_graph_node_bandwidth(const srg_graph* g, uint32_t index, uint64_t* down
     if (up_bits) *up_bits = g->bw_up[index];
     if (has_up) *has_up = g->has_up[index];
 }
+
+void srg_graph_node_bandwidths(const srg_graph* g, uint64_t* down_bits, int* has_down, uint64_t* up_bits,
+                               int* has_up) {
+    if (!g) return;
+    const size_t V = g->node_id.size();
+    if (down_bits) std::copy(g->bw_down.begin(), g->bw_down.end(), down_bits);
+    if (has_down) std::copy(g->has_down.begin(), g->has_down.begin() + V, has_down);
+    if (up_bits) std::copy(g->bw_up.begin(), g->bw_up.end(), up_bits);
+    if (has_up) std::copy(g->has_up.begin(), g->has_up.begin() + V, has_up);
+}
+
+uint32_t srg_graph_parse_chunks(const srg_graph* g) { return g ? g->parse_chunks : 0; }
 
 }  // extern "C"

@@ -318,15 +318,25 @@ __device__ __forceinline__ int tile_kept(int base, int idx, int x0, int x1) {
 // gridDim.z > 1 splits the pivot block's k range across workgroups (split-K): each split
 // reduces its share and merges with atomicMin, which is exact because min is associative and
 // commutative (used for the short launches on the multi-GPU critical path).
-template <class K, int T, int KC, bool PK>
+template <class K, int T, int KC, int PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J);
 
-// PK = true (u32 keys only): the pair-packed tile below (fw_tile_pk); false: add + min3.
-#ifndef SRG_PK_MINB
-#define SRG_PK_MINB 1  // workgroups per CU the packed tile is register-budgeted for
-#endif
-template <class K, int T, int KC, bool PK>
-__global__ void __launch_bounds__(256, PK ? SRG_PK_MINB : 1) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
+// PK (tile variant, SRG_OPT_FW_PACKED): 0 = add + min3 (any key); u32 keys only, the
+// pair-packed tile below (fw_tile_pk):
+//   1 = KC 32, next k-pair's operands read from LDS while the current one is folded (2 waves/SIMD)
+//   2 = KC 16, no operand prefetch: register budget for 3 waves per SIMD (latency hidden by
+//       the other waves instead), LDS 33 KB per workgroup
+//   3 = KC 16 with the operand prefetch
+//   4 = KC 16, no prefetch, register budget for 4 waves per SIMD (<= 128 VGPRs)
+template <int PK>
+constexpr int pk_kc() { return (PK >= 2) ? 16 : 32; }
+template <int PK>
+constexpr bool pk_prefetch() { return PK == 1 || PK == 3; }
+template <int PK>
+constexpr int pk_min_waves() { return PK == 2 ? 3 : PK == 4 ? 4 : 1; }  // waves per SIMD budgeted for
+
+template <class K, int T, int KC, int PK>
+__global__ void __launch_bounds__(256, pk_min_waves<PK>()) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
     fw_tile<K, T, KC, PK>(D, ld, kb, tile_kept(ts.r0, (int)blockIdx.y, ts.rx0, ts.rx1),
                           tile_kept(ts.c0, (int)blockIdx.x, ts.cx0, ts.cx1));
 }
@@ -335,7 +345,7 @@ __global__ void __launch_bounds__(256, PK ? SRG_PK_MINB : 1) fw_product(K* __res
 // once the pivot tile is closed, and each is a single short wave of workgroups, so one launch
 // instead of two takes a tile latency off the FW critical path).  grid.x = na + nb tiles;
 // set s is nc_s columns wide, tiles flattened row-major.
-template <class K, int T, int KC, bool PK>
+template <class K, int T, int KC, int PK>
 __global__ void __launch_bounds__(256) fw_product_pair(K* __restrict__ D, size_t ld, int kb, TileSet a, int na,
                                                        int nca, TileSet b, int ncb) {
     int x = (int)blockIdx.x;
@@ -433,7 +443,7 @@ constexpr size_t pk_lds_bytes() {
     return (size_t)2 * KC * (T + 2) * sizeof(u64p);  // double-buffered Ap + Bp
 }
 
-template <int T, int KC>
+template <int T, int KC, bool PF>
 __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
     using S = PkStage<T, KC>;
     constexpr int M = T / 16;
@@ -477,8 +487,6 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
         const u64p* Ap = lds + ((ch - ch0) & 1) * BUF;
         const u64p* Bp = Ap + (KC / 2) * LDA;
         if (ch + 1 < ch1) pk_load<T, KC>(sg, A, B, ld, arow, (ch + 1) * KC);  // issue early
-        // operands of k-pair kp+1 are read from LDS while kp is folded (two register sets)
-        u64p ap[2][M], bp[2][M];
         auto rd = [&](int kp, u64p* xa, u64p* xb) {
 #pragma unroll
             for (int g = 0; g < M / 2; ++g) {
@@ -490,12 +498,7 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
                 xb[2 * g + 1] = vb.v[1];
             }
         };
-        rd(0, ap[0], bp[0]);
-#pragma unroll
-        for (int kp = 0; kp < KC / 2; ++kp) {
-            if (kp + 1 < KC / 2) rd(kp + 1, ap[(kp + 1) & 1], bp[(kp + 1) & 1]);
-            const u64p* xa = ap[kp & 1];
-            const u64p* xb = bp[kp & 1];
+        auto fold = [&](const u64p* xa, const u64p* xb) {
 #pragma unroll
             for (int a = 0; a < M; ++a)
 #pragma unroll
@@ -503,6 +506,24 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
                     const u64p s = add_pairs(xa[a], xb[b]);
                     c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
+        };
+        if constexpr (PF) {
+            // operands of k-pair kp+1 are read from LDS while kp is folded (two register sets)
+            u64p ap[2][M], bp[2][M];
+            rd(0, ap[0], bp[0]);
+#pragma unroll
+            for (int kp = 0; kp < KC / 2; ++kp) {
+                if (kp + 1 < KC / 2) rd(kp + 1, ap[(kp + 1) & 1], bp[(kp + 1) & 1]);
+                fold(ap[kp & 1], bp[kp & 1]);
+            }
+        } else {
+            // one register set: the other resident waves hide the LDS latency
+#pragma unroll
+            for (int kp = 0; kp < KC / 2; ++kp) {
+                u64p ap[M], bp[M];
+                rd(kp, ap, bp);
+                fold(ap, bp);
+            }
         }
         if (ch + 1 < ch1) {  // write late into the other buffer
             u64p* An = lds + ((ch + 1 - ch0) & 1) * BUF;
@@ -528,11 +549,11 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
     }
 }
 
-template <class K, int T, int KC, bool PK>
+template <class K, int T, int KC, int PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J) {
-    if constexpr (PK) {
+    if constexpr (PK != 0) {
         static_assert(sizeof(K) == 4, "pair-packed tiles need u32 keys");
-        fw_tile_pk<T, KC>(reinterpret_cast<uint32_t*>(D), ld, kb, I, J);
+        fw_tile_pk<T, KC, pk_prefetch<PK>()>(reinterpret_cast<uint32_t*>(D), ld, kb, I, J);
         return;
     }
     using G = Geo<K, T>;

@@ -424,7 +424,7 @@ struct srg_ctx {
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
     int fw_tile = 0;                 // 0 = auto, 64 or 128
-    bool fw_packed = true;           // u32 FW tiles: pair-packed 64-bit adds (else add + min3)
+    int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
     int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default), 3 = LDS-staged u-chunks
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
@@ -673,31 +673,34 @@ inline Rect make_rect(int ra, int rb, std::initializer_list<int> rx, int ca, int
 }
 
 // split-K factor for a short launch of `tiles` workgroups (critical-path launches only)
-template <int T>
+template <int T, int KCV>
 int split_for(int tiles, bool enable) {
     if (!enable) return 1;
-    constexpr int maxs = T / KC;
+    constexpr int maxs = T / KCV;
     int sp = 1;
     while (sp < maxs && tiles * sp * 2 <= 512) sp *= 2;
     return sp;
 }
 
-template <class K, int T, bool PK>
+template <int PK>
+constexpr int kc_for() { return PK ? pk_kc<PK>() : KC; }
+
+template <class K, int T, int PK>
 void fw_tiles(K* D, size_t ld, int kb, int ra, int rb, std::initializer_list<int> rx, int ca, int cb,
               std::initializer_list<int> cx, size_t lds, hipStream_t s, bool split = false) {
     const Rect r = make_rect(ra, rb, rx, ca, cb, cx);
     if (r.nr <= 0 || r.nc <= 0) return;
-    const int sp = split_for<T>(r.nr * r.nc, split);
-    fw_product<K, T, KC, PK><<<dim3(r.nc, r.nr, sp), 256, lds, s>>>(D, ld, kb, r.ts);
+    const int sp = split_for<T, kc_for<PK>()>(r.nr * r.nc, split);
+    fw_product<K, T, kc_for<PK>(), PK><<<dim3(r.nc, r.nr, sp), 256, lds, s>>>(D, ld, kb, r.ts);
 }
 
-template <class K, int T, bool PK>
+template <class K, int T, int PK>
 void fw_tiles_pair(K* D, size_t ld, int kb, const Rect& a, const Rect& b, size_t lds, hipStream_t s,
                    bool split = false) {
     const int na = std::max(0, a.nr) * std::max(0, a.nc), nb = std::max(0, b.nr) * std::max(0, b.nc);
     if (na + nb == 0) return;
-    const int sp = split_for<T>(na + nb, split);
-    fw_product_pair<K, T, KC, PK><<<dim3(na + nb, 1, sp), 256, lds, s>>>(D, ld, kb, a.ts, na, std::max(1, a.nc),
+    const int sp = split_for<T, kc_for<PK>()>(na + nb, split);
+    fw_product_pair<K, T, kc_for<PK>(), PK><<<dim3(na + nb, 1, sp), 256, lds, s>>>(D, ld, kb, a.ts, na, std::max(1, a.nc),
                                                                         b.ts, std::max(1, b.nc));
 }
 
@@ -706,13 +709,14 @@ void fw_tiles_pair(K* D, size_t ld, int kb, const Rect& a, const Rect& b, size_t
 //   panel on the auxiliary stream, and broadcasts the panel (T x Vp keys, in place) while
 //   every rank finishes the remaining tiles of kb; then each rank updates its own column
 //   panel of kb+1.  Single GPU: the same schedule with the broadcast elided.
-template <class K, int T, bool PK>
+template <class K, int T, int PK>
 void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax, int& prof_n) {
     const int nb = pl.nb;
+    constexpr int KCV = kc_for<PK>();
     // double-buffered LDS image: A^T + B (add + min3 tiles) or the k-pair image (packed tiles)
-    const size_t lds = PK ? pk_lds_bytes<T, KC>() : (size_t)4 * KC * (T + 16 / (int)sizeof(K)) * sizeof(K);
-    set_lds(fw_product<K, T, KC, PK>, lds);
-    set_lds(fw_product_pair<K, T, KC, PK>, lds);
+    const size_t lds = PK ? pk_lds_bytes<T, KCV>() : (size_t)4 * KCV * (T + 16 / (int)sizeof(K)) * sizeof(K);
+    set_lds(fw_product<K, T, KCV, PK>, lds);
+    set_lds(fw_product_pair<K, T, KCV, PK>, lds);
     const bool multi = c.comm && c.comm->nranks > 1;
     const bool prof = c.profiling && nb > 2;
     if (prof) {
@@ -836,10 +840,15 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint64_t prof_relax = 0;
     int prof_n = 0;
     if constexpr (sizeof(K) == 4) {
-        if (c.fw_packed) fw_blocked<K, T, true>(c, pl, D, Vp, st, prof_relax, prof_n);
-        else fw_blocked<K, T, false>(c, pl, D, Vp, st, prof_relax, prof_n);
+        switch (c.fw_packed) {
+            case 0: fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n); break;
+            case 2: fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n); break;
+            case 3: fw_blocked<K, T, 3>(c, pl, D, Vp, st, prof_relax, prof_n); break;
+            case 4: fw_blocked<K, T, 4>(c, pl, D, Vp, st, prof_relax, prof_n); break;
+            default: fw_blocked<K, T, 1>(c, pl, D, Vp, st, prof_relax, prof_n); break;
+        }
     } else {
-        fw_blocked<K, T, false>(c, pl, D, Vp, st, prof_relax, prof_n);
+        fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
     }
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
@@ -982,7 +991,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
     // LDS-staged scan (SRG_OPT_SCAN_VARIANT 3, default): entries by (target tile, u-chunk, target)
-    const bool lds = sizeof(K) == 4 && c.scan_variant == 3;
+    const bool lds = sizeof(K) == 4 && (c.scan_variant == 3 || c.scan_variant == 4);
     const uint32_t nK = (V + LS_UC - 1) / LS_UC, nbTT = (NT + LS_TT - 1) / LS_TT;
     const size_t NQ3 = (size_t)nbTT * nK * LS_TT;
     uint32_t *ls_cnt = nullptr, *ls_nr = nullptr, *ls_roff = nullptr;
@@ -1092,7 +1101,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
                 if (lds) {
-                    tight_lds_u32<<<8u * nbTT * ((nbS + 7) / 8), LS_WAVES * 64, 0, st>>>(
+                    auto kern = c.scan_variant == 4 ? tight_lds_u32_rl : tight_lds_u32;
+                    kern<<<8u * nbTT * ((nbS + 7) / 8), LS_WAVES * 64, 0, st>>>(
                         (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, (uint32_t)Vp, nbTT, nbS, nK,
                         ls_nr, ls_roff, ent_ro, (const uint32_t*)ent_w, PRED, Vp);
                 } else if (runs) {
@@ -1808,10 +1818,11 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
         case SRG_OPT_FW_PACKED:
-            ctx->fw_packed = value != 0.0;
+            if (!(value == 0 || value == 1 || value == 2 || value == 3 || value == 4)) return SRG_ERR_ARG;
+            ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (value != 0 && value != 1 && value != 2 && value != 3) return SRG_ERR_ARG;
+            if (!(value == 0 || value == 1 || value == 2 || value == 3 || value == 4)) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:

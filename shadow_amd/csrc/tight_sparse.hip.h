@@ -714,6 +714,145 @@ __global__ void __launch_bounds__(512, 2) tight_lds_u32(const uint32_t* __restri
     }
 }
 
+// Variant 4: the LDS-staged scan with the entry stream in VECTOR registers.  Variant 3 read
+// each target's entries with scalar loads: one dependent scalar-cache round trip per target
+// (the scalar cache misses on a 265 KB-per-workgroup stream) kept its waves parked ~70 % of the
+// time (profiles/r02/scan_v3_lds_pmc.txt).  Here a wave loads its chunk's entries 64 at a time
+// with coalesced vector loads, one batch ahead, and broadcasts each entry with v_readlane;
+// the per-target run counts arrive the same way (lane j = target j).
+__global__ void __launch_bounds__(512, 2) tight_lds_u32_rl(const uint32_t* __restrict__ DST, size_t npad,
+                                                            uint32_t dst_bytes, const uint32_t* __restrict__ nodes,
+                                                            uint32_t n, uint32_t V, uint32_t Vp, uint32_t nbTT,
+                                                            uint32_t nbS, uint32_t nK,
+                                                            const uint32_t* __restrict__ nruns,
+                                                            const uint32_t* __restrict__ roff,
+                                                            const uint32_t* __restrict__ ent_lo,
+                                                            const uint32_t* __restrict__ ent_w,
+                                                            uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ __attribute__((aligned(16))) uint32_t chunk[LS_UC * 64];
+    __shared__ uint32_t hitq[LS_WAVES][LS_TW][2];
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r = c * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t voff = r * 4u;  // row offsets in the VGPR offset: range-checked
+    const uint32_t t0 = b * LS_TT + wave * LS_TW;
+    const bool active = t0 < Vp;
+    const bool own_row = active && r < n;
+    const uint32_t s = r < n ? nodes[r] : 0xFFFFFFFFu;
+    uint32_t* out = PRED + (size_t)r * ldp + t0;
+    v32u_ls dd;
+#pragma unroll
+    for (uint32_t j = 0; j < LS_TW; ++j)
+        dd[j] = active ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + (t0 + j) * (uint32_t)npad * 4u, 0, 0)
+                       : KeyOps<uint32_t>::INF;
+    if (own_row) {
+        const uint4 none = make_uint4(PRED_NONE, PRED_NONE, PRED_NONE, PRED_NONE);
+#pragma unroll
+        for (uint32_t j = 0; j < LS_TW; j += 4) *reinterpret_cast<uint4*>(out + j) = none;
+    }
+    constexpr uint32_t ROWS_PER_PASS = LS_WAVES * 64 / 16;
+    constexpr uint32_t SR = LS_UC / ROWS_PER_PASS;
+    const uint32_t srow = tid >> 4, scol = (tid & 15) * 4;
+    uint4 sv[SR];
+    auto stage_load = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t i = 0; i < SR; ++i) {
+            const uint32_t u = k * LS_UC + srow + ROWS_PER_PASS * i;
+            const uint32_t off = u * (uint32_t)npad * 4u + (c * 64 + scol) * 4u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+            sv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    auto stage_store = [&]() {
+#pragma unroll
+        for (uint32_t i = 0; i < SR; ++i)
+            *reinterpret_cast<uint4*>(&chunk[(srow + ROWS_PER_PASS * i) * 64 + scol]) = sv[i];
+    };
+    stage_load(0);
+    stage_store();
+    __syncthreads();
+    const unsigned char* lrow = reinterpret_cast<const unsigned char*>(chunk) + lane * 4u;
+    auto lds_ld = [&](uint32_t byte_off) { return *reinterpret_cast<const uint32_t*>(lrow + byte_off); };
+    for (uint32_t k = 0; k < nK; ++k) {
+        if (k + 1 < nK) stage_load(k + 1);  // issue early, write late
+        if (active) {
+            const size_t q0 = ((size_t)b * nK + k) * LS_TT + wave * LS_TW;
+            const uint32_t nrv = lane < LS_TW ? nruns[q0 + lane] : 0u;
+            uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(roff[q0]);
+            uint32_t eb = e & ~63u;  // entry batch base (the allocation has 256 entries of slack)
+            uint32_t lo_c = ent_lo[eb + lane], w_c = ent_w[eb + lane];
+            uint32_t lo_n = ent_lo[eb + 64 + lane], w_n = ent_w[eb + 64 + lane];
+            uint32_t nq = 0;
+            for (uint32_t j = 0; j < LS_TW; ++j) {
+                const uint32_t runs = (uint32_t)__builtin_amdgcn_readlane((int)nrv, (int)j);
+                if (!runs) continue;
+                const uint32_t dj = dd[j];
+                const uint32_t e_t = e;
+                uint32_t m = 0xFFFFFFFFu;
+                for (uint32_t ri = 0; ri < runs; ++ri, e += LS_R) {
+                    if (e - eb >= 64) {  // next entry batch (a run never straddles one)
+                        eb += 64;
+                        lo_c = lo_n;
+                        w_c = w_n;
+                        lo_n = ent_lo[eb + 64 + lane];
+                        w_n = ent_w[eb + 64 + lane];
+                    }
+                    const int i = (int)(e - eb);
+                    const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)lo_c, i);
+                    const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane((int)lo_c, i + 1);
+                    const uint32_t l2 = (uint32_t)__builtin_amdgcn_readlane((int)lo_c, i + 2);
+                    const uint32_t l3 = (uint32_t)__builtin_amdgcn_readlane((int)lo_c, i + 3);
+                    const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w_c, i);
+                    const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)w_c, i + 1);
+                    const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)w_c, i + 2);
+                    const uint32_t w3 = (uint32_t)__builtin_amdgcn_readlane((int)w_c, i + 3);
+                    const uint32_t x0 = lds_ld(l0), x1 = lds_ld(l1), x2 = lds_ld(l2), x3 = lds_ld(l3);
+                    m = min(m, min((x0 + w0) ^ dj, (x1 + w1) ^ dj));
+                    m = min(m, min((x2 + w2) ^ dj, (x3 + w3) ^ dj));
+                }
+                if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                    if (lane == 0) {
+                        hitq[wave][nq][0] = j;
+                        hitq[wave][nq][1] = e_t;
+                    }
+                    ++nq;
+                }
+            }
+            // resolve the queued targets (rare): count the tight entries, keep the entry index
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t qi = 0; qi < nq; ++qi) {
+                const uint32_t j = hitq[wave][qi][0], e0 = hitq[wave][qi][1];
+                const uint32_t runs = nruns[q0 + j];
+                const uint32_t t = t0 + j;
+                const uint32_t dj = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + t * (uint32_t)npad * 4u, 0, 0);
+                uint32_t cnt = 0, last = 0;
+                for (uint32_t ri = 0; ri < runs; ++ri) {
+                    const uint32_t e1 = e0 + LS_R * ri;
+                    const uint4 lo = *reinterpret_cast<const uint4*>(ent_lo + e1);
+                    const uint4 wv = *reinterpret_cast<const uint4*>(ent_w + e1);
+                    const uint32_t h0 = lds_ld(lo.x) + wv.x == dj, h1 = lds_ld(lo.y) + wv.y == dj;
+                    const uint32_t h2 = lds_ld(lo.z) + wv.z == dj, h3 = lds_ld(lo.w) + wv.w == dj;
+                    cnt += h0 + h1 + h2 + h3;
+                    last = h3 ? e1 + 3 : h2 ? e1 + 2 : h1 ? e1 + 1 : h0 ? e1 : last;
+                }
+                if (cnt && own_row && t < V && t != s && dj != KeyOps<uint32_t>::INF) {
+                    const uint32_t sj = out[j];
+                    out[j] = (sj == PRED_NONE && cnt == 1) ? last : PRED_MULTI;
+                }
+            }
+        }
+        if (k + 1 < nK) {
+            __syncthreads();
+            stage_store();
+            __syncthreads();
+        }
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,

@@ -315,16 +315,18 @@ class NetworkGraph:
                           arr(el.latency_ns, ctypes.c_uint64, E, np.uint64),
                           arr(el.packet_loss, ctypes.c_float, E, np.float32), bool(el.directed),
                           arr(el.node_ids, ctypes.c_uint32, V, np.uint32))
-            down, up = [], []
-            for i in range(V):
-                d, u = ctypes.c_uint64(), ctypes.c_uint64()
-                hd, hu = ctypes.c_int(), ctypes.c_int()
-                L.srg_graph_node_bandwidth(h, i, ctypes.byref(d), ctypes.byref(hd), ctypes.byref(u), ctypes.byref(hu))
-                down.append(d.value if hd.value else None)
-                up.append(u.value if hu.value else None)
+            d, u = np.zeros(V, np.uint64), np.zeros(V, np.uint64)
+            hd, hu = np.zeros(V, np.int32), np.zeros(V, np.int32)
+            if V:
+                L.srg_graph_node_bandwidths(h, d.ctypes.data, hd.ctypes.data, u.ctypes.data, hu.ctypes.data)
+            down = [int(x) if k else None for x, k in zip(d.tolist(), hd.tolist())]
+            up = [int(x) if k else None for x, k in zip(u.tolist(), hu.tolist())]
+            chunks = int(L.srg_graph_parse_chunks(h))
         finally:
             L.srg_graph_free(h)
-        return NetworkGraph(edges, down, up)
+        g = NetworkGraph(edges, down, up)
+        g.parse_chunks = chunks
+        return g
 
     @property
     def directed(self):

@@ -135,3 +135,75 @@ def test_roundtrip_synthetic_gml():
     assert np.array_equal(g.edges.src, e.src) and np.array_equal(g.edges.dst, e.dst)
     assert np.array_equal(g.edges.latency_ns, e.latency_ns)
     assert np.array_equal(g.edges.packet_loss.view(np.uint32), e.packet_loss.view(np.uint32))
+
+
+# ---- chunked parallel parse (gml.cpp parse_impl): same result / same error as one pass -----
+def _parse_both(txt, monkeypatch):
+    """(sequential result-or-error, chunked result-or-error) for the same text."""
+    chunks = []
+    def run():
+        try:
+            g = NetworkGraph.parse(txt)
+            e = g.edges
+            chunks.append(g.parse_chunks)
+            return ("ok", e.num_vertices, e.directed, e.src.tolist(), e.dst.tolist(), e.latency_ns.tolist(),
+                    e.packet_loss.view(np.uint32).tolist(), e.node_ids.tolist(), g.bandwidth_down, g.bandwidth_up)
+        except NetGraphError as err:
+            return ("err", str(err))
+    monkeypatch.delenv("SRG_GML_MIN_CHUNK", raising=False)
+    seq = run()
+    monkeypatch.setenv("SRG_GML_MIN_CHUNK", "64")
+    monkeypatch.setenv("OMP_NUM_THREADS", "8")
+    par = run()
+    if seq[0] == "ok":
+        assert chunks == [1, 1 if _parse_both.expect_fallback else 8], chunks
+    return seq, par
+
+
+_parse_both.expect_fallback = False
+
+
+def test_chunked_parse_matches_sequential(monkeypatch):
+    e = synth.random_graph(200, 0.1, 4, directed=False, loss_hi=0.05)
+    seq, par = _parse_both(synth.to_gml(e), monkeypatch)
+    assert seq[0] == "ok" and seq == par
+    assert seq[3] == e.src.tolist() and seq[5] == e.latency_ns.tolist()
+
+
+def _nodes_edges(nv, bad_node=None, bad_edge=None, syntax_at=None, trailer=""):
+    s = ["graph [", "  directed 0"]
+    for i in range(nv):
+        s += ["  node [", f"    id {i}"]
+        if i == bad_node:
+            s.append('    host_bandwidth_up "1 Xbit"')
+        s.append("  ]")
+    for i in range(nv - 1):
+        s += ["  edge [", f"    source {i}", f"    target {i + 1}"]
+        s.append('    latency "0 ms"' if i == bad_edge else '    latency "3 ms"')
+        if i == syntax_at:
+            s.append("    weird[")
+        s.append("  ]")
+    return "\n".join(s) + "\n]\n" + trailer
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),                                 # clean
+    dict(bad_edge=5),                       # edge conversion error early
+    dict(bad_node=90, bad_edge=2),          # node error (late) wins over edge error (early)
+    dict(bad_edge=3, syntax_at=80),         # syntax error (late) wins over conversion error
+    dict(syntax_at=10),
+])
+def test_chunked_parse_error_order(kw, monkeypatch):
+    seq, par = _parse_both(_nodes_edges(100, **kw), monkeypatch)
+    assert seq == par
+    assert (seq[0] == "ok") == (not kw)
+
+
+def test_chunked_parse_cut_inside_string_falls_back(monkeypatch):
+    """A multi-line string holding what looks like an item start: the guessed boundary is wrong,
+    the chunk's run fails its boundary check, and the text is parsed in one pass instead."""
+    body = "".join(f'  node [\n    id {i}\n    label "x\n  edge [\n    source 1\n"\n  ]\n' for i in range(120))
+    txt = "graph [\n" + body + "]\n"
+    monkeypatch.setattr(_parse_both, "expect_fallback", True)
+    seq, par = _parse_both(txt, monkeypatch)
+    assert seq[0] == "ok" and seq == par and seq[1] == 120

@@ -91,7 +91,7 @@ def test_random_vs_oracle(scan_router, kw):
     assert_parity(tab, lat, loss)
 
 
-@pytest.mark.parametrize("packed", [0, 1])
+@pytest.mark.parametrize("packed", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("kw", [dict(V=300, density=0.1, seed=111, lat_hi=40, parallel=0.1),
                                 dict(V=390, density=0.2, seed=112, directed=True, lat_lo=10**6, lat_hi=10**8)],
                          ids=["ties", "directed_wide"])
@@ -110,7 +110,7 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_scan_variants_match_oracle(variant):
     """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs,
     LDS-staged u-chunks (the default)."""

@@ -1,8 +1,8 @@
 """Ingest at scale: write a synthetic graph's GML once (C3: ≈4.5 GB, the text
 Shadow would read), parse it with srg_graph_parse_gml (NetworkGraph::parse, mod.rs:134-181),
 time the parse, and check the parsed edge list equals the generator's.  Also times reading the
-same text xz-compressed through srg_graph_parse_gml_xz when --xz is given (read_xz, mod.rs:480-492).
-usage: python tools/ingest/ingest_bench.py [--vertices 10000] [--xz] [--keep]"""
+text with OMP_NUM_THREADS parser threads (chunked parallel parse, gml.cpp parse_impl).
+usage: python tools/ingest/ingest_bench.py [--vertices 10000] [--graph atlas|ba]"""
 import argparse
 import json
 import os
