@@ -131,9 +131,11 @@ void srg_destroy(srg_ctx* ctx);
                                      packed key pairs + v_min3, 32-deep k-chunks, operand prefetch;
                                      2 (default) = the same with 16-deep k-chunks and no operand prefetch (3 waves
                                      per SIMD); 3 = 16-deep with prefetch; 0 = one add per relaxation */
-#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 3 = source columns staged in LDS per u-chunk,
-                                     2 (default) = entries grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry
-                                     batches broadcast with v_readlane */
+#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 5 = two sources per lane over LDS-staged rows
+                                     (ds_read_b64) with a 4-pair scalar record stream; 4 / 3 = one source per lane
+                                     over LDS-staged rows (v_readlane / s_load entry reads); 2 (default) = entries
+                                     grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches
+                                     broadcast with v_readlane */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
@@ -142,6 +144,8 @@ void srg_destroy(srg_ctx* ctx);
                                         below the bucket bound, 0 (default) = when any is */
 #define SRG_OPT_SPARSE_GLOBAL_BITMAPS 14 /* sparse: 1 = keep the per-batch vertex bitmaps in global memory
                                         (automatic when 5V/8 bytes do not fit the LDS budget) */
+#define SRG_OPT_SPARSE_LANE_MASKS 15 /* sparse: 1 = pull only the lanes whose label of the arc's source
+                                        changed since its last push (per-vertex 64-bit lane masks) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

@@ -423,6 +423,8 @@ struct srg_ctx {
     bool sparse_delta_all = false;   // sparse: bucket test over every dropped lane (else any lane)
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
+    bool sparse_lane_masks = false;      // sparse: lane-masked pulls (SRG_OPT_SPARSE_LANE_MASKS)
+    DevBuf b_lmask;
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
     int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default), 3 = LDS-staged u-chunks
@@ -450,7 +452,7 @@ struct srg_ctx {
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
                           &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst,
-                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
+                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered, &b_lmask})
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
@@ -987,7 +989,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    const size_t npad = ((size_t)nloc + 63) / 64 * 64;
+    const bool v5 = sizeof(K) == 4 && c.scan_variant == 5;  // pair-lane LDS scan: 128-source blocks
+    const size_t npad = v5 ? ((size_t)nloc + 127) / 128 * 128 : ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
     // LDS-staged scan (SRG_OPT_SCAN_VARIANT 3, default): entries by (target tile, u-chunk, target)
@@ -1001,7 +1004,32 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const size_t NQ = (size_t)nbT * V;
     uint64_t E_ess = 0, E_layout = 0;
     size_t tbytes = 0;
-    if (lds) {
+    const uint32_t nK5 = (V + V5_UC - 1) / V5_UC, nbTT5 = (NT + V5_TT - 1) / V5_TT;
+    const size_t NG5 = (size_t)nbTT5 * nK5 * V5_WAVES;
+    uint32_t *v5_cnt = nullptr, *v5_goff = nullptr;
+    if (v5) {
+        v5_cnt = (uint32_t*)c.b_ecnt.get((size_t)nbTT5 * nK5 * V5_TT * 4);
+        uint32_t* v5_glen = (uint32_t*)c.b_rlen.get((NG5 + 1) * 4);
+        v5_goff = (uint32_t*)c.b_eoff.get((NG5 + 1) * 4);
+        HIP_CHECK(hipMemsetAsync(v5_cnt, 0, (size_t)nbTT5 * nK5 * V5_TT * 4, st));
+        HIP_CHECK(hipMemsetAsync(v5_glen, 0, (NG5 + 1) * 4, st));
+        const size_t nwaves = (size_t)nw64 * nK5;
+        k_v5_count<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, V, nw64, nK5, v5_cnt, v5_glen, indeg);
+        HIP_CHECK(hipGetLastError());
+        size_t ta = 0, tc = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, v5_glen, v5_goff, (int)(NG5 + 1), st));
+        tbytes = std::max(ta, tc);
+        void* tmp = c.b_scantmp.get(tbytes);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(NT + 1), st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, v5_glen, v5_goff, (int)(NG5 + 1), st));
+        uint32_t tail[2];
+        HIP_CHECK(hipMemcpyAsync(&tail[0], cscoff + NT, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tail[1], v5_goff + NG5, 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        E_ess = tail[0];
+        E_layout = 2ull * tail[1];
+    } else if (lds) {
         ls_cnt = (uint32_t*)c.b_ecnt.get(NQ3 * 4);
         ls_nr = (uint32_t*)c.b_gblk.get(NQ3 * 4);
         uint32_t* ls_rlen = (uint32_t*)c.b_rlen.get((NQ3 + 1) * 4);
@@ -1069,13 +1097,22 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         scan_kind = SRG_SCAN_SPARSE;
         const size_t Eb = E_layout + 256;
         uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
-        uint32_t* ent_ro = (uint32_t*)c.b_entkey.get(Eb * 4);
+        uint32_t* ent_ro = v5 ? nullptr : (uint32_t*)c.b_entkey.get(Eb * 4);  // v5: pair records instead
         K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
         uint32_t* ent_tl = (uint32_t*)c.b_grpu.get(Eb * 4);
         uint32_t* ent_u = (uint32_t*)c.b_grpe.get(Eb * 4);
         float* ent_b = (float*)c.b_entb.get(Eb * 4);
         uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
-        if (lds) {
+        if (v5) {
+            if constexpr (sizeof(K) == 4) {
+                HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+                uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
+                const size_t nwaves = (size_t)nw64 * nK5;
+                k_v5_fill<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK5, v5_cnt,
+                                                                                   v5_goff, cscoff, cscfill, rec, ent_w,
+                                                                                   ent_u, ent_b, cscent);
+            }
+        } else if (lds) {
             if constexpr (sizeof(K) == 4) {
                 const size_t nwaves = (size_t)nw64 * nK;
                 k_ls_fill<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK, ls_cnt,
@@ -1100,7 +1137,12 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             if constexpr (sizeof(K) == 4) {
-                if (lds) {
+                if (v5) {
+                    const uint32_t nbS5 = (uint32_t)(npad / V5_SB);
+                    tight_v5<<<8u * nbTT5 * ((nbS5 + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                        (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, nbS5, nK5, v5_goff,
+                        (const uint32_t*)c.b_entkey.get(0), PRED, Vp);
+                } else if (lds) {
                     auto kern = c.scan_variant == 4 ? tight_lds_u32_rl : tight_lds_u32;
                     kern<<<8u * nbTT * ((nbS + 7) / 8), LS_WAVES * 64, 0, st>>>(
                         (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, (uint32_t)Vp, nbTT, nbS, nK,
@@ -1361,7 +1403,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     // label slots (V x 64 x 8 B per resident batch) within about half of the free HBM
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t slot_bytes = (size_t)V * 64 * 8;
+    const size_t slot_bytes = (size_t)V * 64 * 8 + (c.sparse_lane_masks ? (size_t)V * 3 * 8 : 0);
     grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
     const uint32_t nwv = (V + 63) / 64;
     const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
@@ -1370,7 +1412,9 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                        bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / c.sparse_wgs_per_cu;
     const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
     if (nbatch) {
-        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * slot_bytes);
+        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
+        unsigned long long* lm =
+            c.sparse_lane_masks ? (unsigned long long*)c.b_lmask.get((size_t)grid * V * 3 * 8) : nullptr;
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
@@ -1378,7 +1422,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                           : (c.sparse_group == 4 ? k_sparse_bf<4, false> : k_sparse_bf<SP_G, false>);
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
-                     P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb};
+                     P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb, lm};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.es.max_lat / (unsigned long long)c.sparse_delta_div);
@@ -1400,9 +1444,15 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         c.comm->allreduce_max_u32(fl, 2, st);
         c.comm->allreduce_max_u32(fl + 5, 1, st);
     }
-    uint32_t hfl[6] = {0, 0, 0, 0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(hfl, fl, 24, hipMemcpyDeviceToHost, st));
+    uint32_t hfl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(hfl, fl, 32, hipMemcpyDeviceToHost, st));
     const double ms_sssp = tm.lap();
+    if (std::getenv("SRG_DEBUG_SPARSE")) {
+        const unsigned long long ev = (unsigned long long)hfl[2] | (unsigned long long)hfl[3] << 32;
+        const unsigned long long ll = (unsigned long long)hfl[6] | (unsigned long long)hfl[7] << 32;
+        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu, arc lanes loaded %llu\n",
+                     nbatch, grid, hfl[1], ev, ll);
+    }
     if (hfl[0]) {
         // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
         // finite (>= 2^32-1 ns) path; otherwise the pair is unreachable -- the reference's panic
@@ -1822,7 +1872,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (!(value == 0 || value == 1 || value == 2 || value == 3 || value == 4)) return SRG_ERR_ARG;
+            if (!(value >= 0 && value <= 5 && value == (int)value)) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
@@ -1842,6 +1892,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_SPARSE_GLOBAL_BITMAPS:
             ctx->sparse_global_bitmaps = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_LANE_MASKS:
+            ctx->sparse_lane_masks = value != 0.0;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

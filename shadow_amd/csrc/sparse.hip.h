@@ -36,9 +36,10 @@ constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_CAP = 128;            // active-arc list entries per wave
 constexpr int SP_G = 8;                // label rows in flight per wave (default; SRG_OPT_SPARSE_GROUP)
 constexpr size_t sp_scratch_bytes() {
-    return (size_t)SP_WAVES * (128 + 4 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 4 * SP_CAP) * 4
+    return (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4
                                                                    : (size_t)64 * 65 * 8;
 }
+constexpr uint32_t SP_OWN = 0xFFFFFFFFu;  // w_b tag of a list entry that is a vertex's own row (b is never NaN)
 
 __device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, uint32_t w, float b) {
     const uint32_t lat = (uint32_t)(lu >> 32);
@@ -124,6 +125,9 @@ struct SparseArgs {
     uint32_t delta;              // bucket width in ns (0xFFFFFFFF = one bucket: plain Bellman-Ford)
     uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
+    unsigned long long* lmask;   // [gridDim.x][3][V] per-vertex lane masks (null = whole-row pulls): two
+                                 // sweep-parity buffers of "lanes changed since the last push" and the
+                                 // accumulator of lanes dropped but not yet pushed
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
@@ -137,6 +141,11 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
     return __builtin_nontemporal_load(p);
 }
 
+// Lane masks (a.lmask): a pull of arc (u, t) only needs the lanes whose label of u changed since
+// u was last pushed -- the other lanes already relaxed (u, t) with their current label of u when
+// it last changed (same argument as the vertex-level fprev skip, per lane).  The masked lanes
+// issue no memory request, so a row pull reads only the 128-B lines that hold changed lanes.
+//
 // Vertex bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
 // pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
 // sweep (the out-neighbours of changed vertices, pushed when a vertex changes).  A sweep
@@ -162,9 +171,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     uint32_t* w_st = scratch + wave * (128 + 4 * SP_CAP);
     uint32_t* w_lo = w_st + 64;
     uint32_t* w_u = w_lo + 64;
-    uint32_t* w_w = w_u + SP_CAP;
-    uint32_t* w_b = w_w + SP_CAP;
-    uint32_t* w_vi = w_b + SP_CAP;
+    uint32_t* w_w = w_u + SP_CAP;   // arc weight, or the window index of an own-row entry
+    uint32_t* w_b = w_w + SP_CAP;   // 1 - arc loss, or SP_OWN
+    uint32_t* w_ml = w_b + SP_CAP;  // lane mask of the arc's source vertex (lanes 0-31 / 32-63)
+    uint32_t* w_mh = w_ml + SP_CAP;
+    const bool LM = a.lmask != nullptr;
+    unsigned long long* cmX = LM ? a.lmask + (size_t)blockIdx.x * 3 * V : nullptr;  // [2][V] by sweep parity
+    unsigned long long* cmP = LM ? cmX + 2 * (size_t)V : nullptr;                  // dropped, not yet pushed
+    unsigned long long lanes_loaded = 0;
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
     unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
     uint32_t max_sweeps = 0;
@@ -197,6 +211,15 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
             pend[w] = 0;
         }
         if (threadIdx.x == 0) s_pend = 0;
+        uint32_t par = 0;  // sweep parity: pulls read cmX[par], pushes write cmX[par ^ 1]
+        if (LM) {
+            for (uint32_t v = threadIdx.x; v < V; v += SP_THREADS) cmP[v] = 0;
+            for (uint32_t q = wave; q < 64; q += SP_WAVES) {
+                const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)my_src, q);
+                const unsigned long long m = __ballot(my_src == sv);
+                if (lane == 0) cmX[sv] = m;
+            }
+        }
         // bucket bound (delta-stepping): a changed vertex is pushed to its out-neighbours only
         // once some lane's new latency is below the bound; the others wait in `pend` until the
         // bucket is exhausted and the bound moves on.  Any push order reaches the same unique
@@ -256,37 +279,51 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                         unsigned long long row[G];
 #pragma unroll
                         for (int q = 0; q < G; ++q)
-                            if (j0 + q < cnt) row[q] = ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]);
+                            if (j0 + q < cnt) {
+                                bool need = true;
+                                if (LM && w_b[j0 + q] != SP_OWN)
+                                    need = ((lane < 32 ? w_ml[j0 + q] : w_mh[j0 + q]) >> (lane & 31)) & 1u;
+                                if (LM) lanes_loaded += need ? 1u : 0u;
+                                row[q] = need ? ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]) : LBL_INF;
+                            }
 #pragma unroll
                         for (int q = 0; q < G; ++q) {
                             const uint32_t e = j0 + q;
                             if (e >= cnt) break;
-                            const uint32_t tag = w_vi[e];
-                            if (tag & 0x80000000u) {  // a new vertex: its current label
-                                if (cur >= 0 && __ballot(best < old)) {
-                                    if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
-                                    if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
-                                        changed |= 1ull << cur;
-                                    else
-                                        deferred |= 1ull << cur;
+                            const uint32_t tagb = w_b[e];
+                            if (tagb == SP_OWN) {  // a new vertex: its current label
+                                if (cur >= 0) {
+                                    const unsigned long long dm = __ballot(best < old);
+                                    if (dm) {
+                                        if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
+                                        if (LM && lane == 0) atomicOr(&cmP[w * 64 + cur], dm);
+                                        if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
+                                            changed |= 1ull << cur;
+                                        else
+                                            deferred |= 1ull << cur;
+                                    }
                                 }
-                                cur = (int)(tag & 63u);
+                                cur = (int)(w_w[e] & 63u);
                                 old = best = row[q];
                             } else {
                                 const unsigned long long c =
-                                    row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(w_b[e]));
+                                    row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(tagb));
                                 saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
                                 best = c < best ? c : best;
                                 ++evals;
                             }
                         }
                     }
-                    if (cur >= 0 && __ballot(best < old)) {
-                        if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
-                        if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
-                            changed |= 1ull << cur;
-                        else
-                            deferred |= 1ull << cur;
+                    if (cur >= 0) {
+                        const unsigned long long dm = __ballot(best < old);
+                        if (dm) {
+                            if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
+                            if (LM && lane == 0) atomicOr(&cmP[w * 64 + cur], dm);
+                            if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
+                                changed |= 1ull << cur;
+                            else
+                                deferred |= 1ull << cur;
+                        }
                     }
                 };
                 for (uint32_t f0 = 0; f0 < total; f0 += 64) {
@@ -303,6 +340,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                             u = w * 64 + i;
                             vi = 0x80000000u | i;
                             act = true;
+                            k = i;
                         } else {
                             k = w_lo[i] + slot - 1;
                             u = a.in_src[k];
@@ -318,8 +356,15 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                         if (!(vi & 0x80000000u)) {
                             w_w[pos] = a.in_w[k];
                             w_b[pos] = __float_as_uint(a.in_b[k]);
+                            if (LM) {
+                                const unsigned long long mk = __builtin_nontemporal_load(&cmX[par * (size_t)V + u]);
+                                w_ml[pos] = (uint32_t)mk;
+                                w_mh[pos] = (uint32_t)(mk >> 32);
+                            }
+                        } else {
+                            w_w[pos] = k;  // window index of the vertex
+                            w_b[pos] = SP_OWN;
                         }
-                        w_vi[pos] = vi;
                     }
                     __builtin_amdgcn_wave_barrier();
                     n += (uint32_t)__popcll(m);
@@ -337,7 +382,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                 if (lane == 0) {
                                     w_u[0] = w * 64 + i;
-                                    w_vi[0] = 0x80000000u | i;
+                                    w_w[0] = i;
+                                    w_b[0] = SP_OWN;
                                 }
                                 __builtin_amdgcn_wave_barrier();
                                 n = 1;
@@ -355,6 +401,11 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                 // (4) mark the out-neighbours of the changed vertices for the next sweep
                 if (changed) {
                     if (lane == 0) atomicOr(&fcur[w], changed);
+                    if (LM) {  // their lanes changed since the last push -> the next sweep's pull masks
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if ((changed >> lane) & 1ull)
+                            cmX[(par ^ 1u) * (size_t)V + vl] = atomicExch(&cmP[vl], 0ull);
+                    }
                     chg = 1;
                     const bool ch = (changed >> lane) & 1ull;
                     uint32_t olo = lo, ohi = hi;
@@ -394,6 +445,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
             __syncthreads();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             ++sweeps;
+            par ^= 1u;
             const bool more = s_changed != 0;
             for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
                 fprev[w] = fcur[w];
@@ -421,6 +473,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                         const uint32_t b = (uint32_t)__builtin_ctzll(mk);
                         mk &= mk - 1;
                         push_out(w * 64 + b);
+                        if (LM && lane == 0) cmX[par * (size_t)V + w * 64 + b] = atomicExch(&cmP[w * 64 + b], 0ull);
                     }
                 }
                 __syncthreads();
@@ -467,6 +520,11 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     if (threadIdx.x == 0) atomicMax(&a.flags[1], max_sweeps);
     if (__ballot(saturated) && lane == 0) atomicOr(&a.flags[5], 1u);
     if (lane == 0 && evals) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[2]), evals);
+    if (LM) {  // lanes actually loaded by arc pulls (diagnostics: flags[6..7])
+        unsigned long long tot = lanes_loaded;
+        for (int o = 32; o; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[6]), tot);
+    }
 }
 
 }  // namespace srg

@@ -853,6 +853,223 @@ __global__ void __launch_bounds__(512, 2) tight_lds_u32_rl(const uint32_t* __res
     }
 }
 
+// ---- pair-lane LDS scan (SRG_OPT_SCAN_VARIANT 5) ------------------------------------------
+// A workgroup owns 128 sources x V5_TT targets; lane l holds sources 2l and 2l+1, so ONE
+// conflict-free ds_read_b64 (64 lanes x 8 B = the 512-B staged row) feeds two checks per lane:
+// half the LDS cycles per check of a b32 row (§LDS table: b64 = 256 B/clk/CU).  Rows of a
+// V5_UC-row u-chunk are staged into a double-buffered LDS ring (2 x 32 KB), one barrier per chunk.
+// With D the exact closure, a + w >= d for every edge (u, t), so x = a + w - d (mod 2^32, with
+// -d held per lane) is the true nonnegative slack and tight <=> x == 0: two v_add3 + a min per
+// entry pair and source pair, one compare per pair of entries.  The entry stream of a
+// (tile, chunk, wave) is a flat run of 16-B pair records {lo0 | tl << 16, w0, lo1, w1} (both
+// entries of a pair share the target tl; odd runs end with a sentinel w = INF), read as 4-pair
+// s_load_dwordx16 groups one group ahead, so the loop has no per-target trip counts; -d and the
+// per-target state are 16-element register vectors read with the pair's uniform tl.  A hit
+// (x == 0 in some lane: ~1 pair in 4) updates St[tl] = entry, or MULTI on a second hit.
+constexpr uint32_t V5_WAVES = 8;                 // waves per workgroup
+constexpr uint32_t V5_TW = 16;                   // targets per wave
+constexpr uint32_t V5_TT = V5_WAVES * V5_TW;     // targets per workgroup tile (128)
+constexpr uint32_t V5_UC = 64;                   // u rows per chunk: 64 x 512 B = 32 KB per buffer
+constexpr uint32_t V5_SB = 128;                  // sources per workgroup (2 per lane)
+constexpr uint32_t V5_SLACK = 32;                // entries past the end (the scan reads one group ahead)
+
+// one wave per (64-target window, chunk), lane = target: entries per (tile b, chunk k, target),
+// pairs per (b, k, wave) rounded up to whole 4-pair groups, and indeg[t] for the CSC lists
+__global__ void __launch_bounds__(256) k_v5_count(const unsigned long long* __restrict__ ess, uint32_t V,
+                                                   uint32_t nw64, uint32_t nK, uint32_t* __restrict__ cnt,
+                                                   uint32_t* __restrict__ glen, uint32_t* __restrict__ indeg) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wv = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    if (wv >= (size_t)nw64 * nK) return;  // whole wave
+    const uint32_t w64 = (uint32_t)(wv / nK), k = (uint32_t)(wv % nK);
+    const uint32_t t = w64 * 64 + lane, b = t / V5_TT, tt = t % V5_TT;
+    const uint32_t u0 = k * V5_UC, u1 = min(V, u0 + V5_UC);
+    uint32_t c = 0;
+    for (uint32_t u = u0; u < u1; ++u) c += (uint32_t)((ess[(size_t)u * nw64 + w64] >> lane) & 1ull);
+    cnt[((size_t)b * nK + k) * V5_TT + tt] = c;
+    if (c) atomicAdd(&indeg[t], c);
+    uint32_t p = (c + 1) / 2;
+#pragma unroll
+    for (int off = 1; off < (int)V5_TW; off <<= 1) p += __shfl_xor(p, off, V5_TW);
+    if ((lane % V5_TW) == 0) glen[((size_t)b * nK + k) * V5_WAVES + tt / V5_TW] = (p + 3) / 4 * 4;
+}
+
+// records rec[e] = (lo | tl << 16, w) for entry e = 2 * pair + slot, plus ent_w / ent_u / ent_b
+// (k_loss_rows) and the CSC lists (any order: the MULTI fold is a min)
+__global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __restrict__ ess,
+                                                  const uint32_t* __restrict__ W, const uint32_t* __restrict__ WL,
+                                                  size_t ld, uint32_t V, uint32_t nw64, uint32_t nK,
+                                                  const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ goff,
+                                                  const uint32_t* __restrict__ csc_off, uint32_t* __restrict__ csc_fill,
+                                                  uint2* __restrict__ rec, uint32_t* __restrict__ ent_w,
+                                                  uint32_t* __restrict__ ent_u, float* __restrict__ ent_b,
+                                                  uint32_t* __restrict__ csc_ent) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wv = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    if (wv >= (size_t)nw64 * nK) return;
+    const uint32_t w64 = (uint32_t)(wv / nK), k = (uint32_t)(wv % nK);
+    const uint32_t t = w64 * 64 + lane, b = t / V5_TT, tt = t % V5_TT, j = tt % V5_TW;
+    const uint32_t c = cnt[((size_t)b * nK + k) * V5_TT + tt];
+    const uint32_t p = (c + 1) / 2;
+    uint32_t incl = p;
+#pragma unroll
+    for (int off = 1; off < (int)V5_TW; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, V5_TW);
+        if ((int)j >= off) incl += y;
+    }
+    const size_t g = ((size_t)b * nK + k) * V5_WAVES + tt / V5_TW;
+    const uint32_t pbase = goff[g];
+    size_t e = 2 * ((size_t)pbase + incl - p);
+    const uint32_t u0 = k * V5_UC, u1 = min(V, u0 + V5_UC);
+    const uint32_t cbase = t < V ? csc_off[t] : 0u;
+    for (uint32_t u = u0; u < u1; ++u) {
+        if (!((ess[(size_t)u * nw64 + w64] >> lane) & 1ull)) continue;
+        const uint32_t w = W[(size_t)u * ld + t];
+        rec[e] = make_uint2(((u - u0) * 512u) | (j << 16), w);
+        ent_w[e] = w;
+        ent_u[e] = u;
+        ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));
+        csc_ent[cbase + atomicAdd(&csc_fill[t], 1u)] = (uint32_t)e;
+        ++e;
+    }
+    if (c & 1u) {  // odd run: a sentinel second slot (w = INF is never tight on a reachable target)
+        rec[e] = make_uint2(0u, KeyOps<uint32_t>::INF);
+        ent_w[e] = KeyOps<uint32_t>::INF;
+        ent_u[e] = 0;
+        ent_b[e] = 1.0f;
+    }
+    if (j == V5_TW - 1) {  // the slice's group padding
+        const uint32_t total = incl;
+        for (size_t q = 2 * ((size_t)pbase + total); q < 2 * (size_t)goff[g + 1]; ++q) {
+            rec[q] = make_uint2(0u, KeyOps<uint32_t>::INF);
+            ent_w[q] = KeyOps<uint32_t>::INF;
+            ent_u[q] = 0;
+            ent_b[q] = 1.0f;
+        }
+    }
+}
+
+typedef uint32_t v16u_v5 __attribute__((ext_vector_type(16)));
+struct alignas(64) V5Grp {
+    uint32_t v[16];
+};
+
+// grid: 8 * nbTT * ceil(nbS / 8) workgroups of 512 (XCD-aware: the workgroups of one XCD share
+// the 128-source block, whose staged rows then come out of that XCD's L2)
+__global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK,
+                                                    const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
+                                                    uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r0 = c * V5_SB + 2 * lane;  // this lane's two sources (columns of DST)
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t t0 = b * V5_TT + wave * V5_TW;
+    const bool active = t0 < NT;  // a wave past the targets still stages and syncs
+    v16u_v5 ndl, ndh, stl, sth;
+#pragma unroll
+    for (uint32_t j = 0; j < V5_TW; ++j) {
+        uint32_t dl = 0, dh = 0;
+        if (active) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ((t0 + j) * (uint32_t)npad + r0) * 4u, 0, 0);
+            dl = v[0];
+            dh = v[1];
+        }
+        ndl[j] = 0u - dl;
+        ndh[j] = 0u - dh;
+        stl[j] = PRED_NONE;
+        sth[j] = PRED_NONE;
+    }
+    // staging: 512 threads x 16 B = 16 rows per pass, 4 passes per 64-row chunk
+    const uint32_t srow = tid >> 5, scol = (tid & 31) * 4;
+    uint4 sv[4];
+    auto stage_load = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t u = k * V5_UC + srow + 16 * i;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (u * (uint32_t)npad + c * V5_SB + scol) * 4u, 0, 0);
+            sv[i] = make_uint4(v[0], v[1], v[2], v[3]);  // rows past DST read 0 (range-checked)
+        }
+    };
+    auto stage_store = [&](uint32_t buf) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4*>(&rows[buf * (V5_UC * V5_SB) + (srow + 16 * i) * V5_SB + scol]) = sv[i];
+    };
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows);
+    for (uint32_t k = 0; k < nK; ++k) {
+        if (k + 1 < nK) stage_load(k + 1);  // issue early, write after the chunk
+        if (active) {
+            const size_t q = ((size_t)b * nK + k) * V5_WAVES + wave;
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q]);
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q + 1]);
+            const uint32_t vb = (k & 1u) * (V5_UC * V5_SB * 4u) + lane * 8u;
+            if (p0 < p1) {
+                V5Grp cur = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)p0);
+                for (uint32_t p = p0; p < p1; p += 4) {
+                    const V5Grp nxt = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p + 4));
+                    uint2 A[8];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        A[2 * i] = *reinterpret_cast<const uint2*>(lds + vb + (cur.v[4 * i] & 0xFFFFu));
+                        A[2 * i + 1] = *reinterpret_cast<const uint2*>(lds + vb + cur.v[4 * i + 2]);
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        const uint32_t tl = cur.v[4 * i] >> 16;
+                        const uint32_t dl = ndl[tl], dh = ndh[tl];
+                        const uint32_t w0 = cur.v[4 * i + 1], w1 = cur.v[4 * i + 3];
+                        const uint32_t x0l = A[2 * i].x + w0 + dl, x0h = A[2 * i].y + w0 + dh;
+                        const uint32_t x1l = A[2 * i + 1].x + w1 + dl, x1h = A[2 * i + 1].y + w1 + dh;
+                        const uint32_t m = min(min(x0l, x0h), min(x1l, x1h));
+                        if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                            const uint32_t e0 = 2 * (p + i);
+                            uint32_t sl = stl[tl], sh = sth[tl];
+                            if (x0l == 0) sl = (sl == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (x1l == 0) sl = (sl == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            if (x0h == 0) sh = (sh == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (x1h == 0) sh = (sh == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            stl[tl] = sl;
+                            sth[tl] = sh;
+                        }
+                    }
+                    cur = nxt;
+                }
+            }
+        }
+        if (k + 1 < nK) {
+            stage_store((k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
+            __syncthreads();
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t r = r0 + h;
+        if (r >= n) continue;
+        const uint32_t s = nodes[r];
+        uint32_t o[V5_TW];
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; ++j) {
+            const uint32_t t = t0 + j;
+            const uint32_t nd = h ? ndh[j] : ndl[j];
+            const uint32_t st = h ? sth[j] : stl[j];
+            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+        }
+        uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; j += 4) out[j / 4] = make_uint4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,

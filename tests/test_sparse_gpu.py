@@ -84,6 +84,48 @@ def test_bf_delta_buckets(bf_router, kw, div, all_lanes):
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
 
 
+@pytest.mark.parametrize("div", [0, 1, 4])
+@pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], dict(V=1000, density=0.01, seed=207, lat_hi=100, parallel=0.1)],
+                         ids=lambda k: f"V{k['V']}_s{k['seed']}")
+def test_bf_lane_masks(bf_router, kw, div):
+    """Lane-masked pulls (only the lanes whose label of the arc's source changed since its last
+    push are loaded) reach the same fixpoint bit for bit, with and without delta buckets."""
+    bf_router.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, 1)
+    bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, div)
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    nodes = list(range(V))
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
+def test_bf_lane_masks_c4_equal():
+    """C4 at full size: the lane-masked and whole-row pulls give identical 2.5e9-pair tables."""
+    import torch
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+    V = 50000
+    dev = torch.device("cuda", 0)
+    e = synth.barabasi_albert(V, 4, seed=V)
+    dg = DeviceGraph(e)
+    nodes_t = torch.arange(V, dtype=torch.int32, device=dev)
+    outs = []
+    for lm in (0, 1):
+        r = Router(0)
+        r.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, lm)
+        ol = torch.empty((V, V), dtype=torch.int64, device=dev)
+        os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
+        st = compute_shortest_paths_device(r, dg, nodes_t, ol, os_)
+        assert st["path_kind"] == N.SRG_PATH_SPARSE_U32
+        outs.append((ol, os_))
+        r.close()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
+
+
 @pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], CASES[5]], ids=lambda k: f"V{k['V']}_s{k['seed']}")
 def test_bf_global_bitmaps(bf_router, kw):
     """Vertex bitmaps in global memory (the layout for V beyond the LDS budget) are bit-exact."""

@@ -6,6 +6,7 @@ dense-matrix Dijkstra (mode 2).  Prints one JSON line per config."""
 import json
 import os
 import sys
+import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -16,7 +17,15 @@ from bench import cpu_info  # noqa: E402
 from shadow_amd import synth  # noqa: E402
 
 
+def _heartbeat():
+    t0 = time.perf_counter()
+    while True:
+        time.sleep(30)
+        print(f"... {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+
 def main():
+    threading.Thread(target=_heartbeat, daemon=True).start()
     info = cpu_info()
     th = info["threads"]
     cfgs = [("C1", lambda: synth.complete_random(1000, seed=1001)), ("C2", lambda: synth.atlas_like(4096, seed=4096))]
