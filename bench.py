@@ -229,6 +229,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--vertices", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--lat-scale", type=int, default=1,
+                    help="multiply every edge latency by this factor (e.g. 1000 puts C3's used paths past "
+                         "2^31 ns, so the u64-key FW runs: the u64 path benchmark)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -300,6 +303,10 @@ def main():
     else:
         edges = synth.barabasi_albert(V, 4, seed=seed)
         gdesc = f"C4 barabasi_albert({V}, m=4, seed={seed}): sparse undirected graph"
+    if args.lat_scale != 1:
+        import numpy as np
+        edges.latency_ns = edges.latency_ns * np.uint64(args.lat_scale)
+        gdesc += f", latencies x{args.lat_scale}"
     log(f"[rank {rank}] generated {gdesc}: {edges.num_edges} edges in {time.time()-t0:.1f}s")
     dg = DeviceGraph(edges, dev)
     nodes = torch.arange(V, dtype=torch.int32, device=dev)
@@ -393,7 +400,7 @@ def main():
             compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
         torch.cuda.synchronize(dev)
         dev_ms = (time.perf_counter() - t1) * 1e3 / 2
-    wkey = (f"{args.graph}:{V}:{seed}:packed{args.fw_packed}:tile{args.fw_tile or 128}:"
+    wkey = (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "") + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
             f"w{args.sparse_wgs or 2}" + (f":lm{args.sparse_lane_masks}" if args.sparse_lane_masks else ""))
     roofline = None
