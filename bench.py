@@ -251,6 +251,7 @@ def main():
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
     ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--sparse-lane-masks", type=int, default=None, help="sparse: 1 = lane-masked pulls")
+    ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs, KC 16, 3 waves/SIMD; 1 = packed, KC 32; 0 = add + min3")
@@ -336,6 +337,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, args.sparse_delta_div)
     if args.sparse_lane_masks is not None:
         router.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, args.sparse_lane_masks)
+    if args.sparse_split_labels is not None:
+        router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
     if args.scan_variant is not None:
@@ -402,7 +405,8 @@ def main():
         dev_ms = (time.perf_counter() - t1) * 1e3 / 2
     wkey = (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "") + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
-            f"w{args.sparse_wgs or 2}" + (f":lm{args.sparse_lane_masks}" if args.sparse_lane_masks else ""))
+            f"w{args.sparse_wgs or 2}" + (f":lm{args.sparse_lane_masks}" if args.sparse_lane_masks else "")
+            + (f":sl{args.sparse_split_labels}" if args.sparse_split_labels else ""))
     roofline = None
     if agg.get("prof_launches") and kind == 3:
         # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row

@@ -424,6 +424,7 @@ struct srg_ctx {
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
     bool sparse_lane_masks = false;      // sparse: lane-masked pulls (SRG_OPT_SPARSE_LANE_MASKS)
+    bool sparse_split_labels = false;    // sparse: u32 latency + u32 loss label arrays (SRG_OPT_SPARSE_SPLIT_LABELS)
     DevBuf b_lmask;
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
@@ -1418,8 +1419,11 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
-        auto kern = gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true> : k_sparse_bf<SP_G, true>)
-                          : (c.sparse_group == 4 ? k_sparse_bf<4, false> : k_sparse_bf<SP_G, false>);
+        auto kern = c.sparse_split_labels
+                        ? (gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true, true> : k_sparse_bf<SP_G, true, true>)
+                                 : (c.sparse_group == 4 ? k_sparse_bf<4, false, true> : k_sparse_bf<SP_G, false, true>))
+                        : (gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true, false> : k_sparse_bf<SP_G, true, false>)
+                                 : (c.sparse_group == 4 ? k_sparse_bf<4, false, false> : k_sparse_bf<SP_G, false, false>));
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
                      P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb, lm};
@@ -1895,6 +1899,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_SPARSE_LANE_MASKS:
             ctx->sparse_lane_masks = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_SPARSE_SPLIT_LABELS:
+            ctx->sparse_split_labels = value != 0.0;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

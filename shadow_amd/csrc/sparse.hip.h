@@ -152,7 +152,12 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
 // only visits marked vertices, 64 per wave step (one bitmap word pair).  The five bitmaps take
 // 5 V / 8 bytes: in LDS up to V ~ 190k (GB = false), beyond that in a per-workgroup global
 // slice (GB = true; the same accesses, separated by the same barriers, L2-resident).
-template <int G, bool GB>
+// Split labels (SPL): the slot holds a u32 latency array and a u32 loss-bits array instead of
+// packed u64 labels.  A pull reads the 256-B latency row; the source's loss is loaded (lane-
+// masked) only in lanes whose candidate latency does not exceed the target's latency at the
+// start of its group -- every other candidate loses the lexicographic min on latency alone.
+// The fold itself is unchanged (u64 keys rebuilt in registers), so the fixpoint is the same.
+template <int G, bool GB, bool SPL>
 __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
@@ -181,6 +186,21 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     unsigned long long lanes_loaded = 0;
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
     unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
+    uint32_t* Llat = reinterpret_cast<uint32_t*>(L);  // SPL: [V][64] latency, then [V][64] loss bits
+    uint32_t* Lls = Llat + (size_t)V * 64;
+    auto ld32 = [](const uint32_t* p) { return __builtin_nontemporal_load(p); };
+    auto st_label = [&](size_t idx, unsigned long long v) {
+        if constexpr (SPL) {
+            Llat[idx] = (uint32_t)(v >> 32);
+            Lls[idx] = (uint32_t)v;
+        } else {
+            L[idx] = v;
+        }
+    };
+    auto ld_full = [&](size_t idx) -> unsigned long long {
+        if constexpr (SPL) return ((unsigned long long)ld32(&Llat[idx]) << 32) | ld32(&Lls[idx]);
+        else return ld_label(&L[idx]);
+    };
     uint32_t max_sweeps = 0;
     unsigned long long evals = 0;
     uint32_t saturated = 0;  // a finite label + arc reached 2^32-1: INF may then mean "too long", not unreachable
@@ -202,7 +222,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
         const uint32_t my_src = a.batch_src[bt * 64 + lane];
         // init: labels INF except the sources; changed = the sources; marks = their out-neighbours
         for (uint32_t v = wave; v < V; v += SP_WAVES)
-            L[(size_t)v * 64 + lane] = (v == my_src) ? 0ull : LBL_INF;
+            st_label((size_t)v * 64 + lane, (v == my_src) ? 0ull : LBL_INF);
         for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
             fprev[w] = 0;
             fcur[w] = 0;
@@ -277,15 +297,52 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                     unsigned long long best = 0, old = 0;
                     for (uint32_t j0 = 0; j0 < cnt; j0 += G) {
                         unsigned long long row[G];
+                        if constexpr (SPL) {
+                            uint32_t rl[G], rs[G];
 #pragma unroll
-                        for (int q = 0; q < G; ++q)
-                            if (j0 + q < cnt) {
-                                bool need = true;
-                                if (LM && w_b[j0 + q] != SP_OWN)
-                                    need = ((lane < 32 ? w_ml[j0 + q] : w_mh[j0 + q]) >> (lane & 31)) & 1u;
-                                if (LM) lanes_loaded += need ? 1u : 0u;
-                                row[q] = need ? ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]) : LBL_INF;
-                            }
+                            for (int q = 0; q < G; ++q)
+                                if (j0 + q < cnt) {
+                                    const uint32_t e = j0 + q;
+                                    const bool own = w_b[e] == SP_OWN;
+                                    bool need = true;
+                                    if (LM && !own) need = ((lane < 32 ? w_ml[e] : w_mh[e]) >> (lane & 31)) & 1u;
+                                    if (LM) lanes_loaded += need ? 1u : 0u;
+                                    const size_t idx = (size_t)w_u[e] * 64 + lane;
+                                    rl[q] = need ? ld32(&Llat[idx]) : 0xFFFFFFFFu;
+                                    rs[q] = own ? ld32(&Lls[idx]) : 0u;
+                                }
+                            // a candidate can only win if its latency is <= the target's latency at
+                            // the start of its group (best <= old): load the source's loss there only
+                            uint32_t olat = (uint32_t)(old >> 32);
+#pragma unroll
+                            for (int q = 0; q < G; ++q)
+                                if (j0 + q < cnt) {
+                                    const uint32_t e = j0 + q;
+                                    if (w_b[e] == SP_OWN) {
+                                        olat = rl[q];
+                                    } else if (rl[q] != 0xFFFFFFFFu) {
+                                        const uint32_t cl = __builtin_elementwise_add_sat(rl[q], w_w[e]);
+                                        saturated |= cl == 0xFFFFFFFFu;
+                                        if (cl != 0xFFFFFFFFu && cl <= olat)
+                                            rs[q] = ld32(&Lls[(size_t)w_u[e] * 64 + lane]);
+                                        else
+                                            rl[q] = 0xFFFFFFFFu;  // cannot win: an INF row in the fold
+                                    }
+                                }
+#pragma unroll
+                            for (int q = 0; q < G; ++q)
+                                row[q] = rl[q] == 0xFFFFFFFFu ? LBL_INF : ((unsigned long long)rl[q] << 32) | rs[q];
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < G; ++q)
+                                if (j0 + q < cnt) {
+                                    bool need = true;
+                                    if (LM && w_b[j0 + q] != SP_OWN)
+                                        need = ((lane < 32 ? w_ml[j0 + q] : w_mh[j0 + q]) >> (lane & 31)) & 1u;
+                                    if (LM) lanes_loaded += need ? 1u : 0u;
+                                    row[q] = need ? ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]) : LBL_INF;
+                                }
+                        }
 #pragma unroll
                         for (int q = 0; q < G; ++q) {
                             const uint32_t e = j0 + q;
@@ -295,7 +352,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                                 if (cur >= 0) {
                                     const unsigned long long dm = __ballot(best < old);
                                     if (dm) {
-                                        if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
+                                        if (best < old) st_label((size_t)(w * 64 + cur) * 64 + lane, best);
                                         if (LM && lane == 0) atomicOr(&cmP[w * 64 + cur], dm);
                                         if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
                                             changed |= 1ull << cur;
@@ -308,7 +365,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                             } else {
                                 const unsigned long long c =
                                     row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(tagb));
-                                saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
+                                if constexpr (!SPL) saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
                                 best = c < best ? c : best;
                                 ++evals;
                             }
@@ -317,7 +374,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
                     if (cur >= 0) {
                         const unsigned long long dm = __ballot(best < old);
                         if (dm) {
-                            if (best < old) L[(size_t)(w * 64 + cur) * 64 + lane] = best;
+                            if (best < old) st_label((size_t)(w * 64 + cur) * 64 + lane, best);
                             if (LM && lane == 0) atomicOr(&cmP[w * 64 + cur], dm);
                             if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
                                 changed |= 1ull << cur;
@@ -490,7 +547,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
         for (uint32_t j0 = 0; j0 < a.ncols; j0 += 64) {
             for (uint32_t i = wave; i < 64; i += SP_WAVES) {
                 const uint32_t j = j0 + i;
-                tile[i * 65 + lane] = j < a.ncols ? ld_label(&L[(size_t)a.cols[j] * 64 + lane]) : 0ull;
+                tile[i * 65 + lane] = j < a.ncols ? ld_full((size_t)a.cols[j] * 64 + lane) : 0ull;
             }
             __syncthreads();
             for (uint32_t sl = wave; sl < 64; sl += SP_WAVES) {
