@@ -251,6 +251,7 @@ def main():
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
     ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--sparse-lane-masks", type=int, default=None, help="sparse: 1 = lane-masked pulls")
+    ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
@@ -337,6 +338,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, args.sparse_delta_div)
     if args.sparse_lane_masks is not None:
         router.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, args.sparse_lane_masks)
+    if args.fw_symmetric is not None:
+        router.set_option(N.SRG_OPT_FW_SYMMETRIC, args.fw_symmetric)
     if args.sparse_split_labels is not None:
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
@@ -406,7 +409,8 @@ def main():
     wkey = (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "") + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
             f"w{args.sparse_wgs or 2}" + (f":lm{args.sparse_lane_masks}" if args.sparse_lane_masks else "")
-            + (f":sl{args.sparse_split_labels}" if args.sparse_split_labels else ""))
+            + (f":sl{args.sparse_split_labels}" if args.sparse_split_labels else "")
+            + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else ""))
     roofline = None
     if agg.get("prof_launches") and kind == 3:
         # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
@@ -428,7 +432,17 @@ def main():
         relax = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
         traffic, tsrc = load_traffic("fw_product", wkey)
-        roofline = {"bound": "valu", "kernel": (f"fw_product<u32,128,{16 if args.fw_packed >= 2 else 32},{args.fw_packed}> (FW phase 3, pair-packed, non-lookahead tiles)" if args.fw_packed else "fw_product<u32,128,32,0> (FW phase 3, add + min3, non-lookahead tiles)") if kind == 0 else "fw_product<u64,64,32,0> (FW phase 3)", "achieved": round(achieved, 3),
+        sym = (kind == 0 and args.fw_packed and args.fw_symmetric != 0 and not edges.directed and world == 1
+               and not args.simulate_rank)
+        if sym:
+            kname = "fw_product_sym<128,16> (FW phase 3 over the stored tiles I <= J of the symmetric D, pair-packed)"
+        elif kind == 0:
+            kname = (f"fw_product<u32,128,{16 if args.fw_packed >= 2 else 32},{args.fw_packed}> (FW phase 3, pair-packed, "
+                     "non-lookahead tiles)" if args.fw_packed else
+                     "fw_product<u32,128,32,0> (FW phase 3, add + min3, non-lookahead tiles)")
+        else:
+            kname = "fw_product<u64,64,32,0> (FW phase 3)"
+        roofline = {"bound": "valu", "kernel": kname, "achieved": round(achieved, 3),
                     "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),

@@ -549,6 +549,196 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Symmetric FW (undirected graph, one rank).  W is symmetric, and so is D after every FW step
+// (D[i][j] = min(D[i][j], D[i][k] + D[k][j]) maps symmetric to symmetric), so only the tiles
+// (I <= J) are updated; the lower triangle is mirrored once after the last pivot.  Operands:
+//     A = D[I][kb] = tile (I, kb) if I <= kb, else tile (kb, I) read transposed
+//     B = D[kb][J] = tile (kb, J) if kb <= J, else tile (J, kb) read transposed
+// An operand is staged from either layout into the same k-pair LDS image:
+//   row form  (element (x, k) at base + x*ld + k, 16 B along k)      = A plain / B transposed
+//   col form  (element (x, k) at base + k*ld + x, two k-rows paired)  = A transposed / B plain
+// Tile sets (SymSet): mode 0 = every kept tile I <= J with rows/cols x0, x1 excluded
+// (grid.x = nb(nb+1)/2), mode 1 = the tiles of line L, i.e. (min(L,x), max(L,x)) for x != x0, x1
+// (grid.x = nb).
+struct SymSet {
+    int mode, L, x0, x1, nb;
+};
+
+__device__ __forceinline__ bool sym_tile(const SymSet& s, int idx, int& I, int& J) {
+    if (s.mode == 1) {
+        if (idx == s.x0 || idx == s.x1) return false;
+        I = min(idx, s.L);
+        J = max(idx, s.L);
+        return true;
+    }
+    // idx -> (I, J), I <= J, row I holding nb - I tiles
+    const int m = s.nb;
+    const double b = 2.0 * m + 1.0;
+    int i = (int)((b - sqrt(b * b - 8.0 * (double)idx)) * 0.5);
+    auto off = [&](int r) { return r * m - r * (r - 1) / 2; };
+    while (i > 0 && off(i) > idx) --i;
+    while (i + 1 < m && off(i + 1) <= idx) ++i;
+    I = i;
+    J = i + (idx - off(i));
+    if (I == s.x0 || I == s.x1 || J == s.x0 || J == s.x1) return false;
+    return true;
+}
+
+template <int T, int KC>
+struct SymOp {
+    static constexpr int NV = T * KC / 4 / 256;  // 16-B vectors per thread per operand (either form)
+    static_assert(T * KC / 4 % 256 == 0 && (KC / 2) * (T / 4) % 256 == 0, "sym staging");
+    Vec16<uint32_t> r[NV];
+};
+
+template <int T, int KC>
+__device__ __forceinline__ void sym_load(SymOp<T, KC>& o, const uint32_t* __restrict__ base, size_t ld, bool colform,
+                                         int k0) {
+    using S = SymOp<T, KC>;
+    const int tid = threadIdx.x;
+    if (!colform) {
+#pragma unroll
+        for (int q = 0; q < S::NV; ++q) {
+            const int v = tid + 256 * q, x = v / (KC / 4), kq = v % (KC / 4);
+            o.r[q] = ld16(base + (size_t)x * ld + k0 + kq * 4);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < S::NV / 2; ++q) {
+            const int v = tid + 256 * q, p = v / (T / 4), xq = v % (T / 4);
+            const uint32_t* r0 = base + (size_t)(k0 + 2 * p) * ld + xq * 4;
+            o.r[2 * q] = ld16(r0);
+            o.r[2 * q + 1] = ld16(r0 + ld);
+        }
+    }
+}
+
+template <int T, int KC>
+__device__ __forceinline__ void sym_store(const SymOp<T, KC>& o, u64p* __restrict__ Xp, bool colform) {
+    using S = SymOp<T, KC>;
+    constexpr int LDA = T + 2;
+    const int tid = threadIdx.x;
+    if (!colform) {
+#pragma unroll
+        for (int q = 0; q < S::NV; ++q) {
+            const int v = tid + 256 * q, x = v / (KC / 4), kq = v % (KC / 4);
+            const uint32_t* e = o.r[q].v;
+            Xp[(2 * kq) * LDA + x] = (u64p)e[0] | ((u64p)e[1] << 32);
+            Xp[(2 * kq + 1) * LDA + x] = (u64p)e[2] | ((u64p)e[3] << 32);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < S::NV / 2; ++q) {
+            const int v = tid + 256 * q, p = v / (T / 4), xq = v % (T / 4);
+            const uint32_t* a = o.r[2 * q].v;
+            const uint32_t* b = o.r[2 * q + 1].v;
+            VecN<u64p, 2> w0, w1;
+            w0.v[0] = (u64p)a[0] | ((u64p)b[0] << 32);
+            w0.v[1] = (u64p)a[1] | ((u64p)b[1] << 32);
+            w1.v[0] = (u64p)a[2] | ((u64p)b[2] << 32);
+            w1.v[1] = (u64p)a[3] | ((u64p)b[3] << 32);
+            stv<u64p, 2>(Xp + p * LDA + xq * 4, w0);
+            stv<u64p, 2>(Xp + p * LDA + xq * 4 + 2, w1);
+        }
+    }
+}
+
+// one stored tile C = (I, J), I <= J, relaxed through pivot block kb (pair-packed, as fw_tile_pk)
+template <int T, int KC>
+__device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
+    using S = SymOp<T, KC>;
+    constexpr int M = T / 16;
+    constexpr int LDA = T + 2;
+    constexpr int BUF = KC * LDA;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    u64p* lds = reinterpret_cast<u64p*>(smem_raw);
+    uint32_t* C = D + (size_t)I * T * ld + (size_t)J * T;
+    const bool acol = I > kb, bcol = !(J < kb);  // A transposed / B plain read column-form
+    const uint32_t* Ab = acol ? D + (size_t)kb * T * ld + (size_t)I * T : D + (size_t)I * T * ld + (size_t)kb * T;
+    const uint32_t* Bb = bcol ? D + (size_t)kb * T * ld + (size_t)J * T : D + (size_t)J * T * ld + (size_t)kb * T;
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    constexpr int NCH = T / KC;
+    S sa, sb;
+    sym_load<T, KC>(sa, Ab, ld, acol, 0);
+    sym_load<T, KC>(sb, Bb, ld, bcol, 0);
+    uint32_t c[M][M];
+#pragma unroll
+    for (int a = 0; a < M; ++a)
+#pragma unroll
+        for (int g = 0; g < M / 2; ++g) {
+            VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx);
+            c[a][2 * g] = v.v[0];
+            c[a][2 * g + 1] = v.v[1];
+        }
+    sym_store<T, KC>(sa, lds, acol);
+    sym_store<T, KC>(sb, lds + (KC / 2) * LDA, bcol);
+    __syncthreads();
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const u64p* Ap = lds + (ch & 1) * BUF;
+        const u64p* Bp = Ap + (KC / 2) * LDA;
+        if (ch + 1 < NCH) {  // issue early
+            sym_load<T, KC>(sa, Ab, ld, acol, (ch + 1) * KC);
+            sym_load<T, KC>(sb, Bb, ld, bcol, (ch + 1) * KC);
+        }
+#pragma unroll
+        for (int kp = 0; kp < KC / 2; ++kp) {
+            u64p ap[M], bp[M];
+#pragma unroll
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<u64p, 2> va = ldv<u64p, 2>(Ap + kp * LDA + 32 * g + 2 * ty);
+                VecN<u64p, 2> vb = ldv<u64p, 2>(Bp + kp * LDA + 32 * g + 2 * tx);
+                ap[2 * g] = va.v[0];
+                ap[2 * g + 1] = va.v[1];
+                bp[2 * g] = vb.v[0];
+                bp[2 * g + 1] = vb.v[1];
+            }
+#pragma unroll
+            for (int a = 0; a < M; ++a)
+#pragma unroll
+                for (int b = 0; b < M; ++b) {
+                    const u64p s = add_pairs(ap[a], bp[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                }
+        }
+        if (ch + 1 < NCH) {  // write late into the other buffer
+            u64p* An = lds + ((ch + 1) & 1) * BUF;
+            sym_store<T, KC>(sa, An, acol);
+            sym_store<T, KC>(sb, An + (KC / 2) * LDA, bcol);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < M; ++a)
+#pragma unroll
+        for (int g = 0; g < M / 2; ++g) {
+            VecN<uint32_t, 2> v;
+            v.v[0] = c[a][2 * g];
+            v.v[1] = c[a][2 * g + 1];
+            stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx, v);
+        }
+}
+
+template <int T, int KC>
+__global__ void __launch_bounds__(256, 3) fw_product_sym(uint32_t* __restrict__ D, size_t ld, int kb, SymSet s) {
+    int I, J;
+    if (!sym_tile(s, (int)blockIdx.x, I, J)) return;  // whole workgroup
+    fw_tile_sym<T, KC>(D, ld, kb, I, J);
+}
+
+// lower triangle <- transpose of the upper one, 64 x 64 blocks (bi > bj) through LDS
+template <class K>
+__global__ void __launch_bounds__(256) k_sym_mirror(K* __restrict__ D, size_t ld) {
+    const uint32_t bi = blockIdx.y, bj = blockIdx.x;
+    if (bi <= bj) return;
+    __shared__ K tile[64][65];
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (uint32_t r = ty; r < 64; r += 4) tile[r][tx] = D[(size_t)(bj * 64 + r) * ld + bi * 64 + tx];
+    __syncthreads();
+    for (uint32_t r = ty; r < 64; r += 4) D[(size_t)(bi * 64 + r) * ld + bj * 64 + tx] = tile[tx][r];
+}
+
 template <class K, int T, int KC, int PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J) {
     if constexpr (PK != 0) {

@@ -428,6 +428,7 @@ struct srg_ctx {
     DevBuf b_lmask;
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
+    bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
     int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default), 3 = LDS-staged u-chunks
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
@@ -797,6 +798,59 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     }
 }
 
+// Symmetric blocked FW (undirected graph, one rank, u32 pair-packed tiles): the same
+// lookahead schedule as fw_blocked over the stored tiles I <= J only (kernels.hip.h
+// fw_tile_sym), then the lower triangle is mirrored.  The chain of pivot k1 updates line k1
+// (row k1 = column k1^T) w.r.t. kb, closes k1, and updates line k1 w.r.t. k1; the bulk of kb
+// is every stored tile off the lines kb and k1.
+template <int T>
+void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
+                    int& prof_n) {
+    constexpr int KCS = 16;
+    const int nb = pl.nb;
+    const size_t lds = pk_lds_bytes<T, KCS>();
+    set_lds(fw_product_sym<T, KCS>, lds);
+    const bool prof = c.profiling && nb > 2;
+    if (prof) {
+        while (c.prof_events.size() < (size_t)2 * nb) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            c.prof_events.push_back(e);
+        }
+    }
+    hipStream_t aux = c.aux_stream;
+    auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
+        fw_product_sym<T, KCS><<<nb, 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb});
+    };
+    fw_phase1<uint32_t, T><<<1, 512, 0, st>>>(D, Vp, 0);
+    if (nb > 1) line(0, 0, 0, -1, st);
+    for (int kb = 0; kb < nb; ++kb) {
+        const int k1 = kb + 1;
+        if (k1 >= nb) {
+            if (nb > 1) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb});
+            break;
+        }
+        HIP_CHECK(hipEventRecord(c.ev_a, st));
+        HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
+        line(k1, kb, kb, -1, aux);  // line k1 (incl. tile (k1, k1)) w.r.t. kb
+        fw_phase1<uint32_t, T><<<1, 512, 0, aux>>>(D, Vp, k1);
+        line(k1, k1, k1, -1, aux);  // line k1 w.r.t. its own closed pivot
+        HIP_CHECK(hipEventRecord(c.ev_d, aux));
+        const int m = nb - 2;  // lines kb and k1 excluded
+        const bool timed = prof && m > 0;
+        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
+        if (m > 0) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb});
+        if (timed) {
+            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
+            prof_relax += (uint64_t)m * (m + 1) / 2 * T * T * T;
+            ++prof_n;
+        }
+        HIP_CHECK(hipStreamWaitEvent(st, c.ev_d, 0));
+    }
+    const unsigned nb64 = (unsigned)(Vp / 64);
+    k_sym_mirror<uint32_t><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
+}
+
 // Dense path for key type K. Returns false (u32 only) when certification fails.
 template <class K, int T>
 bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
@@ -842,7 +896,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // ---- blocked Floyd-Warshall ----
     uint64_t prof_relax = 0;
     int prof_n = 0;
-    if constexpr (sizeof(K) == 4) {
+    const bool sym_fw = sizeof(K) == 4 && T == 128 && c.fw_symmetric && !g.directed && !multi && c.fw_packed != 0;
+    if (sym_fw) {
+        if constexpr (sizeof(K) == 4 && T == 128) fw_blocked_sym<T>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
+    } else if constexpr (sizeof(K) == 4) {
         switch (c.fw_packed) {
             case 0: fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n); break;
             case 2: fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n); break;
@@ -1902,6 +1959,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_SPARSE_SPLIT_LABELS:
             ctx->sparse_split_labels = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_FW_SYMMETRIC:
+            ctx->fw_symmetric = value != 0.0;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

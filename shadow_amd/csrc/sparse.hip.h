@@ -39,6 +39,7 @@ constexpr size_t sp_scratch_bytes() {
     return (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4
                                                                    : (size_t)64 * 65 * 8;
 }
+static_assert(sp_scratch_bytes() >= (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4, "per-wave scratch");
 constexpr uint32_t SP_OWN = 0xFFFFFFFFu;  // w_b tag of a list entry that is a vertex's own row (b is never NaN)
 
 __device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, uint32_t w, float b) {
@@ -170,10 +171,10 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
     unsigned long long* pend = mnext + nw;  // changed, but above the bucket bound: not pushed yet
     __shared__ uint32_t s_batch, s_changed, s_pend;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (4 x SP_CAP);
+    // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (5 x SP_CAP);
     // the output transpose tile [64][65] u64 reuses the same region after convergence
     uint32_t* scratch = GB ? reinterpret_cast<uint32_t*>(smem_raw) : reinterpret_cast<uint32_t*>(pend + nw);
-    uint32_t* w_st = scratch + wave * (128 + 4 * SP_CAP);
+    uint32_t* w_st = scratch + wave * (128 + 5 * SP_CAP);  // stride = sp_scratch_bytes() / SP_WAVES
     uint32_t* w_lo = w_st + 64;
     uint32_t* w_u = w_lo + 64;
     uint32_t* w_w = w_u + SP_CAP;   // arc weight, or the window index of an own-row entry

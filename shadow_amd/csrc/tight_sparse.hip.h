@@ -925,7 +925,7 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
     for (uint32_t u = u0; u < u1; ++u) {
         if (!((ess[(size_t)u * nw64 + w64] >> lane) & 1ull)) continue;
         const uint32_t w = W[(size_t)u * ld + t];
-        rec[e] = make_uint2(((u - u0) * 512u) | (j << 16), w);
+        rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), w);  // the pair's target: first slot only
         ent_w[e] = w;
         ent_u[e] = u;
         ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));

@@ -130,6 +130,27 @@ def test_scan_variants_match_oracle(variant):
     r.close()
 
 
+@pytest.mark.parametrize("V", [100, 200, 300, 1000])
+def test_fw_symmetric_matches_general(V):
+    """Undirected graphs: FW over the stored tiles I <= J (+ mirror) equals the general FW
+    table bit for bit, at one, two, three and eight 128-tiles; and the oracle on V <= 300."""
+    g = synth.atlas_like(V, seed=V + 7)
+    nodes = np.random.default_rng(V).permutation(V).tolist()
+    out = []
+    for sym in (0, 1):
+        r = Router(0)
+        r.set_option(N.SRG_OPT_FW_SYMMETRIC, sym)
+        t = r.compute_shortest_paths(g, nodes)
+        assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
+        out.append(t)
+        r.close()
+    assert np.array_equal(out[0].latency_ns, out[1].latency_ns)
+    assert bits_equal(out[0].packet_loss, out[1].packet_loss)
+    if V <= 300:
+        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+        assert_parity(out[1], lat, loss)
+
+
 @pytest.mark.parametrize("variant", [2, 5])
 def test_scan_variants_ragged_sources(variant):
     """Several 128-source blocks, target tiles and u-chunks, with n and V off every block size and
