@@ -252,6 +252,7 @@ def main():
     ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--sparse-lane-masks", type=int, default=None, help="sparse: 1 = lane-masked pulls")
     ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
+    ap.add_argument("--chain-prio", type=int, default=None, help="dense: 0 = FW chain kernels at normal wave priority")
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
@@ -340,6 +341,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, args.sparse_lane_masks)
     if args.fw_symmetric is not None:
         router.set_option(N.SRG_OPT_FW_SYMMETRIC, args.fw_symmetric)
+    if args.chain_prio is not None:
+        router.set_option(N.SRG_OPT_CHAIN_PRIO, args.chain_prio)
     if args.sparse_split_labels is not None:
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:

@@ -148,6 +148,7 @@ void srg_destroy(srg_ctx* ctx);
                                         changed since its last push (per-vertex 64-bit lane masks) */
 #define SRG_OPT_FW_SYMMETRIC 17     /* dense u32: 1 (default) = for an undirected graph on one rank, update only
                                        the FW tiles I <= J (D stays symmetric) and mirror at the end */
+#define SRG_OPT_CHAIN_PRIO 18       /* dense: 1 (default) = the FW lookahead chain kernels raise their wave priority */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */
 int srg_set_option(srg_ctx* ctx, int option, double value);

@@ -119,7 +119,10 @@ struct P1Geo {
 };
 
 template <class K, int T>
-__global__ void __launch_bounds__(512) fw_phase1(K* __restrict__ D, size_t ld, int kb) {
+__global__ void __launch_bounds__(512) fw_phase1(K* __restrict__ D, size_t ld, int kb, int prio) {
+    // prio: the chain runs beside the bulk tiles; a raised wave priority wins the VALU issue
+    // arbitration on the SIMDs it shares with them (MI355X_MICROARCH.md, waves per SIMD)
+    if (prio) __builtin_amdgcn_s_setprio(3);
     using G = P1Geo<K, T>;
     constexpr int MR = G::MR, MC = G::MC, HR = G::HR, HC = G::HC;
     constexpr int R = 4;
@@ -721,9 +724,10 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
 }
 
 template <int T, int KC>
-__global__ void __launch_bounds__(256, 3) fw_product_sym(uint32_t* __restrict__ D, size_t ld, int kb, SymSet s) {
+__global__ void __launch_bounds__(256, 3) fw_product_sym(uint32_t* __restrict__ D, size_t ld, int kb, SymSet s, int prio) {
     int I, J;
     if (!sym_tile(s, (int)blockIdx.x, I, J)) return;  // whole workgroup
+    if (prio) __builtin_amdgcn_s_setprio(3);  // chain (line) launches: see fw_phase1
     fw_tile_sym<T, KC>(D, ld, kb, I, J);
 }
 

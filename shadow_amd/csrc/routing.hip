@@ -428,6 +428,7 @@ struct srg_ctx {
     DevBuf b_lmask;
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
+    int chain_prio = 1;              // FW lookahead chain kernels at raised wave priority (SRG_OPT_CHAIN_PRIO)
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
     int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default), 3 = LDS-staged u-chunks
     srg::Comm* comm = nullptr;       // null = single GPU
@@ -736,7 +737,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     const int r0 = pl.rb0, r1 = pl.rb1;
     // pivot 0
     if (pl.own(0)) {
-        fw_phase1<K, T><<<1, 512, 0, st>>>(D, Vp, 0);
+        fw_phase1<K, T><<<1, 512, 0, st>>>(D, Vp, 0, c.chain_prio);
         fw_tiles<K, T, PK>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st, pl.G > 1);
     }
     if (multi) {
@@ -763,7 +764,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
         fw_tiles_pair<K, T, PK>(D, Vp, kb, rowr, make_rect(r0, r1, {kb, k1}, k1, k1 + 1, {}), lds, aux, sk);
         const Rect colp = make_rect(r0, r1, {k1}, k1, k1 + 1, {});  // own column panel of k1
         if (pl.own(k1)) {
-            fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1);
+            fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1, c.chain_prio);
             // the column panel of k1 rewrites tile (kb, k1) of panel kb: its broadcast (still the
             // last one recorded in ev_c) must have left first
             if (multi) HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
@@ -820,26 +821,26 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
     }
     hipStream_t aux = c.aux_stream;
     auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
-        fw_product_sym<T, KCS><<<nb, 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb});
+        fw_product_sym<T, KCS><<<nb, 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
     };
-    fw_phase1<uint32_t, T><<<1, 512, 0, st>>>(D, Vp, 0);
+    fw_phase1<uint32_t, T><<<1, 512, 0, st>>>(D, Vp, 0, c.chain_prio);
     if (nb > 1) line(0, 0, 0, -1, st);
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
         if (k1 >= nb) {
-            if (nb > 1) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb});
+            if (nb > 1) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
             break;
         }
         HIP_CHECK(hipEventRecord(c.ev_a, st));
         HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
         line(k1, kb, kb, -1, aux);  // line k1 (incl. tile (k1, k1)) w.r.t. kb
-        fw_phase1<uint32_t, T><<<1, 512, 0, aux>>>(D, Vp, k1);
+        fw_phase1<uint32_t, T><<<1, 512, 0, aux>>>(D, Vp, k1, c.chain_prio);
         line(k1, k1, k1, -1, aux);  // line k1 w.r.t. its own closed pivot
         HIP_CHECK(hipEventRecord(c.ev_d, aux));
         const int m = nb - 2;  // lines kb and k1 excluded
         const bool timed = prof && m > 0;
         if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        if (m > 0) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb});
+        if (m > 0) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
         if (timed) {
             HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
             prof_relax += (uint64_t)m * (m + 1) / 2 * T * T * T;
@@ -1047,7 +1048,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    const bool v5 = sizeof(K) == 4 && c.scan_variant == 5;  // pair-lane LDS scan: 128-source blocks
+    const bool v5 = sizeof(K) == 4 && (c.scan_variant == 5 || c.scan_variant == 6);  // pair-lane LDS scans
     const size_t npad = v5 ? ((size_t)nloc + 127) / 128 * 128 : ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
@@ -1197,7 +1198,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             if constexpr (sizeof(K) == 4) {
                 if (v5) {
                     const uint32_t nbS5 = (uint32_t)(npad / V5_SB);
-                    tight_v5<<<8u * nbTT5 * ((nbS5 + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                    auto scan5 = c.scan_variant == 6 ? tight_v6 : tight_v5;
+                    scan5<<<8u * nbTT5 * ((nbS5 + 7) / 8), V5_WAVES * 64, 0, st>>>(
                         (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, nbS5, nK5, v5_goff,
                         (const uint32_t*)c.b_entkey.get(0), PRED, Vp);
                 } else if (lds) {
@@ -1933,7 +1935,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (!(value >= 0 && value <= 5 && value == (int)value)) return SRG_ERR_ARG;
+            if (!(value >= 0 && value <= 6 && value == (int)value)) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
@@ -1962,6 +1964,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_FW_SYMMETRIC:
             ctx->fw_symmetric = value != 0.0;
+            return SRG_OK;
+        case SRG_OPT_CHAIN_PRIO:
+            ctx->chain_prio = value != 0.0 ? 1 : 0;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

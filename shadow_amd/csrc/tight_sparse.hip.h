@@ -871,7 +871,7 @@ constexpr uint32_t V5_TW = 16;                   // targets per wave
 constexpr uint32_t V5_TT = V5_WAVES * V5_TW;     // targets per workgroup tile (128)
 constexpr uint32_t V5_UC = 64;                   // u rows per chunk: 64 x 512 B = 32 KB per buffer
 constexpr uint32_t V5_SB = 128;                  // sources per workgroup (2 per lane)
-constexpr uint32_t V5_SLACK = 32;                // entries past the end (the scan reads one group ahead)
+constexpr uint32_t V5_SLACK = 256;               // entries past the end (v5 reads one group ahead, v6 a 64-pair batch)
 
 // one wave per (64-target window, chunk), lane = target: entries per (tile b, chunk k, target),
 // pairs per (b, k, wave) rounded up to whole 4-pair groups, and indeg[t] for the CSC lists
@@ -1047,6 +1047,157 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
         }
         if (k + 1 < nK) {
             stage_store((k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
+            __syncthreads();
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t r = r0 + h;
+        if (r >= n) continue;
+        const uint32_t s = nodes[r];
+        uint32_t o[V5_TW];
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; ++j) {
+            const uint32_t t = t0 + j;
+            const uint32_t nd = h ? ndh[j] : ndl[j];
+            const uint32_t st = h ? sth[j] : stl[j];
+            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+        }
+        uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; j += 4) out[j / 4] = make_uint4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+}
+
+// Variant 6: variant 5 with the record stream in VECTOR registers.  v5's 4-pair s_load groups
+// cost one scalar-cache round trip per group that no other work covers (the s_waitcnt for a
+// scalar load also drains every LDS read): 58 % of its wave cycles were waits
+// (profiles/r02/pmc_v5).  Here each wave loads its chunk's records 64 pairs at a time with one
+// coalesced 16-B-per-lane load, issued a whole chunk ahead (vmcnt is in order), and broadcasts
+// pair j with four v_readlane; the rest of the pair's work is v5's.
+__global__ void __launch_bounds__(512, 4) tight_v6(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK,
+                                                    const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
+                                                    uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r0 = c * V5_SB + 2 * lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t t0 = b * V5_TT + wave * V5_TW;
+    const bool active = t0 < NT;
+    const uint4* rec4 = reinterpret_cast<const uint4*>(rec);
+    v16u_v5 ndl, ndh, stl, sth;
+#pragma unroll
+    for (uint32_t j = 0; j < V5_TW; ++j) {
+        uint32_t dl = 0, dh = 0;
+        if (active) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ((t0 + j) * (uint32_t)npad + r0) * 4u, 0, 0);
+            dl = v[0];
+            dh = v[1];
+        }
+        ndl[j] = 0u - dl;
+        ndh[j] = 0u - dh;
+        stl[j] = PRED_NONE;
+        sth[j] = PRED_NONE;
+    }
+    const uint32_t srow = tid >> 5, scol = (tid & 31) * 4;
+    uint4 sv[4];
+    auto stage_load = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t u = k * V5_UC + srow + 16 * i;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (u * (uint32_t)npad + c * V5_SB + scol) * 4u, 0, 0);
+            sv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    auto stage_store = [&](uint32_t buf) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4*>(&rows[buf * (V5_UC * V5_SB) + (srow + 16 * i) * V5_SB + scol]) = sv[i];
+    };
+    auto slice = [&](uint32_t k, uint32_t& p0, uint32_t& p1) {
+        const size_t q = ((size_t)b * nK + k) * V5_WAVES + wave;
+        p0 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q]);
+        p1 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q + 1]);
+    };
+    // loads are issued unconditionally (clamped indices) so that every wait is a counted vmcnt:
+    // a load issued under a condition makes the compiler drain all of them
+    stage_load(0);
+    uint32_t p0, p1;
+    slice(0, p0, p1);
+    uint4 rc = rec4[p0 + lane];  // chunk 0's first 64 pairs (the array has slack past the end)
+    stage_store(0);
+    __syncthreads();
+    const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows);
+    struct Pair {
+        uint2 a0, a1;
+        uint32_t h0, w0, w1;
+    };
+    for (uint32_t k = 0; k < nK; ++k) {
+        const uint32_t kn = min(k + 1, nK - 1);
+        stage_load(kn);
+        uint32_t q0, q1;
+        slice(kn, q0, q1);
+        const uint4 rn = rec4[q0 + lane];  // the next chunk's first records, a whole chunk ahead
+        const uint32_t vb = (k & 1u) * (V5_UC * V5_SB * 4u) + lane * 8u;
+        auto fetch = [&](const uint4& r, int j) {
+            Pair P;
+            P.h0 = (uint32_t)__builtin_amdgcn_readlane((int)r.x, j);
+            P.w0 = (uint32_t)__builtin_amdgcn_readlane((int)r.y, j);
+            const uint32_t h1 = (uint32_t)__builtin_amdgcn_readlane((int)r.z, j);
+            P.w1 = (uint32_t)__builtin_amdgcn_readlane((int)r.w, j);
+            P.a0 = *reinterpret_cast<const uint2*>(lds + vb + (P.h0 & 0xFFFFu));
+            P.a1 = *reinterpret_cast<const uint2*>(lds + vb + h1);
+            return P;
+        };
+        auto check = [&](const Pair& P, uint32_t pair) {
+            const uint32_t tl = P.h0 >> 16;
+            const uint32_t dl = ndl[tl], dh = ndh[tl];
+            const uint32_t x0l = P.a0.x + P.w0 + dl, x0h = P.a0.y + P.w0 + dh;
+            const uint32_t x1l = P.a1.x + P.w1 + dl, x1h = P.a1.y + P.w1 + dh;
+            const uint32_t m = min(min(x0l, x0h), min(x1l, x1h));
+            if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                const uint32_t e0 = 2 * pair;
+                uint32_t sl = stl[tl], sh = sth[tl];
+                if (x0l == 0) sl = (sl == PRED_NONE) ? e0 : PRED_MULTI;
+                if (x1l == 0) sl = (sl == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                if (x0h == 0) sh = (sh == PRED_NONE) ? e0 : PRED_MULTI;
+                if (x1h == 0) sh = (sh == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                stl[tl] = sl;
+                sth[tl] = sh;
+            }
+        };
+        if (active && p1 > p0) {
+            // the first 64 pairs: pair j + 1's LDS reads are in flight while pair j is checked
+            const uint32_t np = min(64u, p1 - p0);  // a multiple of 4
+            Pair cur = fetch(rc, 0);
+            for (uint32_t g = 0; g < np; g += 4) {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    const int jn = (int)min(g + i + 1, 63u);
+                    const Pair nxt = fetch(rc, jn);
+                    check(cur, p0 + g + i);
+                    cur = nxt;
+                }
+            }
+            // slices longer than 64 pairs (rare): the rest in line
+            for (uint32_t base = p0 + 64; base < p1; base += 64) {
+                const uint4 rx = rec4[base + lane];
+                const uint32_t nx = min(64u, p1 - base);
+                for (uint32_t j = 0; j < nx; ++j) check(fetch(rx, (int)j), base + j);
+            }
+        }
+        p0 = q0;
+        p1 = q1;
+        rc = rn;
+        if (k + 1 < nK) {
+            stage_store((k + 1) & 1u);
             __syncthreads();
         }
     }
