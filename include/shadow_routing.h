@@ -131,9 +131,10 @@ void srg_destroy(srg_ctx* ctx);
                                      packed key pairs + v_min3, 32-deep k-chunks, operand prefetch;
                                      2 (default) = the same with 16-deep k-chunks and no operand prefetch (3 waves
                                      per SIMD); 3 = 16-deep with prefetch; 0 = one add per relaxation */
-#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 5 = two sources per lane over LDS-staged rows
-                                     (ds_read_b64) with a 4-pair scalar record stream; 4 / 3 = one source per lane
-                                     over LDS-staged rows (v_readlane / s_load entry reads); 2 (default) = entries
+#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 5 (default) = two sources per lane over
+                                     LDS-staged rows (ds_read_b64) with a 4-pair scalar record stream; 6 = the
+                                     same with the records in vector registers (v_readlane); 4 / 3 = one source per
+                                     lane over LDS-staged rows (v_readlane / s_load entry reads); 2 = entries
                                      grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches
                                      broadcast with v_readlane */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
@@ -149,6 +150,7 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_FW_SYMMETRIC 17     /* dense u32: 1 (default) = for an undirected graph on one rank, update only
                                        the FW tiles I <= J (D stays symmetric) and mirror at the end */
 #define SRG_OPT_CHAIN_PRIO 18       /* dense: 1 (default) = the FW lookahead chain kernels raise their wave priority */
+#define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */
 int srg_set_option(srg_ctx* ctx, int option, double value);

@@ -661,27 +661,38 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
     const uint32_t* Ab = acol ? D + (size_t)kb * T * ld + (size_t)I * T : D + (size_t)I * T * ld + (size_t)kb * T;
     const uint32_t* Bb = bcol ? D + (size_t)kb * T * ld + (size_t)J * T : D + (size_t)J * T * ld + (size_t)kb * T;
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    // gridDim.z > 1: split-K over the pivot block's k chunks, merged with atomicMin (exact: min
+    // is associative and commutative) -- the short line launches on the FW critical chain
     constexpr int NCH = T / KC;
+    const int nsplit = (int)gridDim.z;
+    const int ch0 = (int)blockIdx.z * NCH / nsplit, ch1 = ((int)blockIdx.z + 1) * NCH / nsplit;
     S sa, sb;
-    sym_load<T, KC>(sa, Ab, ld, acol, 0);
-    sym_load<T, KC>(sb, Bb, ld, bcol, 0);
+    sym_load<T, KC>(sa, Ab, ld, acol, ch0 * KC);
+    sym_load<T, KC>(sb, Bb, ld, bcol, ch0 * KC);
     uint32_t c[M][M];
+    if (nsplit == 1) {
 #pragma unroll
-    for (int a = 0; a < M; ++a)
+        for (int a = 0; a < M; ++a)
 #pragma unroll
-        for (int g = 0; g < M / 2; ++g) {
-            VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx);
-            c[a][2 * g] = v.v[0];
-            c[a][2 * g + 1] = v.v[1];
-        }
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx);
+                c[a][2 * g] = v.v[0];
+                c[a][2 * g + 1] = v.v[1];
+            }
+    } else {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int b = 0; b < M; ++b) c[a][b] = KeyOps<uint32_t>::INF;
+    }
     sym_store<T, KC>(sa, lds, acol);
     sym_store<T, KC>(sb, lds + (KC / 2) * LDA, bcol);
     __syncthreads();
 #pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
-        const u64p* Ap = lds + (ch & 1) * BUF;
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const u64p* Ap = lds + ((ch - ch0) & 1) * BUF;
         const u64p* Bp = Ap + (KC / 2) * LDA;
-        if (ch + 1 < NCH) {  // issue early
+        if (ch + 1 < ch1) {  // issue early
             sym_load<T, KC>(sa, Ab, ld, acol, (ch + 1) * KC);
             sym_load<T, KC>(sb, Bb, ld, bcol, (ch + 1) * KC);
         }
@@ -705,22 +716,29 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
                     c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         }
-        if (ch + 1 < NCH) {  // write late into the other buffer
-            u64p* An = lds + ((ch + 1) & 1) * BUF;
+        if (ch + 1 < ch1) {  // write late into the other buffer
+            u64p* An = lds + ((ch + 1 - ch0) & 1) * BUF;
             sym_store<T, KC>(sa, An, acol);
             sym_store<T, KC>(sb, An + (KC / 2) * LDA, bcol);
         }
         __syncthreads();
     }
+    if (nsplit == 1) {
 #pragma unroll
-    for (int a = 0; a < M; ++a)
+        for (int a = 0; a < M; ++a)
 #pragma unroll
-        for (int g = 0; g < M / 2; ++g) {
-            VecN<uint32_t, 2> v;
-            v.v[0] = c[a][2 * g];
-            v.v[1] = c[a][2 * g + 1];
-            stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx, v);
-        }
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<uint32_t, 2> v;
+                v.v[0] = c[a][2 * g];
+                v.v[1] = c[a][2 * g + 1];
+                stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx, v);
+            }
+    } else {
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+            for (int b = 0; b < M; ++b) atomicMin(C + (size_t)pk_rc(ty, a) * ld + pk_rc(tx, b), c[a][b]);
+    }
 }
 
 template <int T, int KC>

@@ -428,9 +428,10 @@ struct srg_ctx {
     DevBuf b_lmask;
     int fw_tile = 0;                 // 0 = auto, 64 or 128
     int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
+    int chain_split = 1;             // split-K of the symmetric FW's line launches (SRG_OPT_CHAIN_SPLIT)
     int chain_prio = 1;              // FW lookahead chain kernels at raised wave priority (SRG_OPT_CHAIN_PRIO)
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
-    int scan_variant = 2;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs (default), 3 = LDS-staged u-chunks
+    int scan_variant = 5;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs, 3/4 = LDS u-chunks (one source per lane), 5 (default) / 6 = LDS u-chunks, two sources per lane (scalar / vector record stream)
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -820,8 +821,10 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
         }
     }
     hipStream_t aux = c.aux_stream;
+    // line launches sit on the critical chain: split-K so that ~nb x split workgroups share a tile
+    const int lsplit = std::max(1, std::min(c.chain_split, T / KCS));
     auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
-        fw_product_sym<T, KCS><<<nb, 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
+        fw_product_sym<T, KCS><<<dim3(nb, 1, lsplit), 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
     };
     fw_phase1<uint32_t, T><<<1, 512, 0, st>>>(D, Vp, 0, c.chain_prio);
     if (nb > 1) line(0, 0, 0, -1, st);
@@ -1967,6 +1970,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_CHAIN_SPLIT:
+            if (!(value == 1 || value == 2 || value == 4 || value == 8)) return SRG_ERR_ARG;
+            ctx->chain_split = (int)value;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
