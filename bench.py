@@ -254,6 +254,9 @@ def main():
     ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
     ap.add_argument("--chain-prio", type=int, default=None, help="dense: 0 = FW chain kernels at normal wave priority")
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
+    ap.add_argument("--d2h-mode", type=int, default=None,
+                    help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync, N >= 2 = copy kernel of N workgroups")
+    ap.add_argument("--loss-chunks", type=int, default=None, help="dense: k_loss_rows launches (0 = auto)")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs, KC 16, 3 waves/SIMD; 1 = packed, KC 32; 0 = add + min3")
@@ -347,6 +350,10 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
+    if args.loss_chunks is not None:
+        router.set_option(N.SRG_OPT_LOSS_CHUNKS, args.loss_chunks)
+    if args.d2h_mode is not None:
+        router.set_option(N.SRG_OPT_D2H_MODE, args.d2h_mode)
     if args.scan_variant is not None:
         router.set_option(N.SRG_OPT_SCAN_VARIANT, args.scan_variant)
     if args.simulate_rank:

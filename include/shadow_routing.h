@@ -150,6 +150,11 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_FW_SYMMETRIC 17     /* dense u32: 1 (default) = for an undirected graph on one rank, update only
                                        the FW tiles I <= J (D stays symmetric) and mirror at the end */
 #define SRG_OPT_CHAIN_PRIO 18       /* dense: 1 (default) = the FW lookahead chain kernels raise their wave priority */
+#define SRG_OPT_D2H_MODE 20         /* host entry: how finished rows are shipped into the page-locked caller
+                                     * arrays while kernels run: 1 (default) = an SDMA engine, 0 =
+                                     * hipMemcpyAsync, N >= 2 = a copy kernel of N workgroups */
+#define SRG_OPT_LOSS_CHUNKS 21       /* dense: k_loss_rows launches (row chunks); 0 (default) = 8 when the host
+                                     * entry ships rows early, else 1 */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -41,7 +41,7 @@ def build(force=False, verbose=True):
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-ldl", "-lpthread"]
+    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs + ["-ldl", "-lpthread", "-lhsa-runtime64"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

@@ -12,9 +12,13 @@
 //   6. k_extract         used x used outputs, diagonal <- raw self-loop, unreachable check
 // No CPU fallback: every entry point fails loudly (status code) when HIP is unavailable.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -411,6 +415,53 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 }  // namespace
 
+// The HSA agents of a HIP device (matched by PCI domain / bus / device), for SDMA copies.
+struct SdmaAgents {
+    bool ok = false;
+    hsa_agent_t gpu{}, cpu{};
+    uint32_t engine = 0;  // hsa_amd_sdma_engine_id_t bit of the engine used for D2H
+    void init(int device) {
+        if (hsa_init() != HSA_STATUS_SUCCESS) return;
+        int bus = -1, dev = -1, dom = -1;
+        if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+            hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+            hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess)
+            return;
+        struct Q {
+            int bus, dev, dom;
+            hsa_agent_t gpu{}, cpu{};
+            bool found = false, have_cpu = false;
+        } q{bus, dev, dom};
+        hsa_iterate_agents(
+            [](hsa_agent_t a, void* p) -> hsa_status_t {
+                Q& q = *static_cast<Q*>(p);
+                hsa_device_type_t t;
+                if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+                if (t == HSA_DEVICE_TYPE_CPU && !q.have_cpu) {
+                    q.cpu = a;
+                    q.have_cpu = true;
+                } else if (t == HSA_DEVICE_TYPE_GPU && !q.found) {
+                    uint32_t bdf = 0, dom = 0;
+                    if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
+                        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS &&
+                        (int)(bdf >> 8) == q.bus && (int)((bdf >> 3) & 31) == q.dev && (int)dom == q.dom) {
+                        q.gpu = a;
+                        q.found = true;
+                    }
+                }
+                return HSA_STATUS_SUCCESS;
+            },
+            &q);
+        if (!q.found || !q.have_cpu) return;
+        uint32_t mask = 0;
+        if (hsa_amd_memory_copy_engine_status(q.cpu, q.gpu, &mask) != HSA_STATUS_SUCCESS || !mask) return;
+        gpu = q.gpu;
+        cpu = q.cpu;
+        engine = mask & (~mask + 1);  // lowest available engine
+        ok = true;
+    }
+};
+
 struct srg_ctx {
     int device = 0;
     double sparse_threshold = 0.35;  // essential-edge density above which the dense scan is used
@@ -431,6 +482,9 @@ struct srg_ctx {
     int chain_split = 1;             // split-K of the symmetric FW's line launches (SRG_OPT_CHAIN_SPLIT)
     int chain_prio = 1;              // FW lookahead chain kernels at raised wave priority (SRG_OPT_CHAIN_PRIO)
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
+    int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync, >= 2 = copy kernel of that many workgroups (SRG_OPT_D2H_MODE)
+    SdmaAgents sdma;
+    int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
     int scan_variant = 5;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs, 3/4 = LDS u-chunks (one source per lane), 5 (default) / 6 = LDS u-chunks, two sources per lane (scalar / vector record stream)
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
@@ -568,15 +622,57 @@ struct Timer {
     }
 };
 
+// Device -> host copy by a narrow kernel (SRG_OPT_D2H_MODE >= 2: that many workgroups), kept as
+// a measured alternative: its posted PCIe writes still slowed the streaming kernels it overlapped
+// (profiles/r02c/d2h_probe.txt), so the default ships rows on an SDMA engine instead.
+__global__ void __launch_bounds__(256) k_copy_to_host(const unsigned char* __restrict__ src,
+                                                     unsigned char* __restrict__ dst, size_t bytes) {
+    const size_t nt = (size_t)gridDim.x * blockDim.x, tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    size_t done = 0;
+    if ((((uintptr_t)src ^ (uintptr_t)dst) & 15) == 0) {
+        const size_t head = (16 - ((uintptr_t)src & 15)) & 15;  // bytes before the first 16-B boundary
+        if (head < bytes) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u* s = reinterpret_cast<const v4u*>(src + head);
+            v4u* d = reinterpret_cast<v4u*>(dst + head);
+            const size_t n16 = (bytes - head) / 16;
+            size_t i = tid;
+            for (; i + 3 * nt < n16; i += 4 * nt) {
+                const v4u a = __builtin_nontemporal_load(&s[i]), b = __builtin_nontemporal_load(&s[i + nt]);
+                const v4u c = __builtin_nontemporal_load(&s[i + 2 * nt]), e = __builtin_nontemporal_load(&s[i + 3 * nt]);
+                d[i] = a;
+                d[i + nt] = b;
+                d[i + 2 * nt] = c;
+                d[i + 3 * nt] = e;
+            }
+            for (; i < n16; i += nt) d[i] = s[i];
+            for (size_t k = tid; k < head; k += nt) dst[k] = src[k];
+            done = head + n16 * 16;
+        }
+    }
+    for (size_t k = done + tid; k < bytes; k += nt) dst[k] = src[k];  // unaligned remainder (rare)
+}
+
+
 // Host entry output sink: the caller's n x n host arrays.  Finished output rows are copied
-// on the D2H stream while later kernels run (latency rows right after FW, loss rows per
-// chunk of k_loss_rows), so the 1.2 GB C3 table mostly leaves during the scan and loss pass.
-// The caller's (pageable) buffers are page-locked by a helper thread that runs concurrently
-// with the H2D copy and FW; until `ready()` confirms it, nothing is sent early and the host
-// entry copies everything at the end instead.
+// while later kernels run (latency rows right after FW, loss rows per chunk of k_loss_rows),
+// so the 1.2 GB C3 table mostly leaves during the scan and loss pass.  The caller's (pageable)
+// buffers are page-locked by a helper thread that runs concurrently with the H2D copy and FW;
+// until `ready()` confirms it, nothing is sent early and the host entry copies everything at
+// the end instead.
+// Copy engines (SRG_OPT_D2H_MODE): 1 (default) = an SDMA engine (hsa_amd_memory_async_copy_on_engine),
+// issued by a helper thread once the producing kernels' event has completed -- measured to leave
+// the overlapped kernels at full speed, where hipMemcpyAsync into registered memory (0) runs as a
+// full-chip blit kernel that held k_ess_mask 0.26 -> 12.7 ms and each k_loss_rows chunk
+// 0.48 -> 2.2 ms (profiles/r02c/).
 struct HostSink {
     uint64_t* lat = nullptr;
     float* loss = nullptr;
+    void* lat_view = nullptr;   // device views of the mapped host arrays (copy kernel)
+    void* loss_view = nullptr;
+    int mode = 1;
+    const SdmaAgents* sdma = nullptr;
+    int device = 0;
     size_t n = 0;
     hipStream_t cs = nullptr;
     hipEvent_t ev = nullptr;
@@ -584,6 +680,21 @@ struct HostSink {
     bool checked = false, registered = false;
     bool lat_sent = false, loss_sent = false;
     uint64_t early_bytes = 0;
+    // SDMA worker
+    struct Job {
+        hipEvent_t ev;
+        void* dst;
+        const void* src;
+        size_t bytes;
+    };
+    std::thread worker;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Job> jobs;
+    bool closing = false;
+    std::string err;
+    std::vector<hsa_signal_t> sigs;
+    std::vector<hipEvent_t> evs;
     bool ok() {
         if (!checked) {
             registered = ready && ready();
@@ -591,15 +702,97 @@ struct HostSink {
         }
         return registered;
     }
+    void work() {
+        (void)hipSetDevice(device);
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return closing || !jobs.empty(); });
+                if (jobs.empty()) return;
+                j = jobs.front();
+                jobs.pop_front();
+            }
+            if (!err.empty()) continue;
+            if (hipEventSynchronize(j.ev) != hipSuccess) {
+                err = "hipEventSynchronize failed before a D2H copy";
+                continue;
+            }
+            hsa_signal_t sg;
+            if (hsa_signal_create(1, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
+                err = "hsa_signal_create failed";
+                continue;
+            }
+            sigs.push_back(sg);
+            if (hsa_amd_memory_async_copy_on_engine(j.dst, sdma->cpu, j.src, sdma->gpu, j.bytes, 0, nullptr, sg,
+                                                    (hsa_amd_sdma_engine_id_t)sdma->engine, true) != HSA_STATUS_SUCCESS)
+                err = "hsa_amd_memory_async_copy_on_engine failed";
+        }
+    }
     // rows [row0, row0 + rows) of a row-major n-column device array, after the work queued on st
     void send_rows(hipStream_t st, const void* dev, void* host, size_t row0, size_t rows, size_t elem) {
         const size_t off = row0 * n * elem, bytes = rows * n * elem;
         if (!bytes) return;
+        const unsigned char* src = (const unsigned char*)dev + off;
+        void* view = host == (void*)lat ? lat_view : host == (void*)loss ? loss_view : nullptr;
+        if (mode == 1 && sdma && sdma->ok) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            evs.push_back(e);
+            HIP_CHECK(hipEventRecord(e, st));
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                jobs.push_back(Job{e, (unsigned char*)(view ? view : host) + off, src, bytes});
+            }
+            if (!worker.joinable()) worker = std::thread([this] { work(); });
+            cv.notify_one();
+            early_bytes += bytes;
+            return;
+        }
         HIP_CHECK(hipEventRecord(ev, st));
         HIP_CHECK(hipStreamWaitEvent(cs, ev, 0));
-        HIP_CHECK(hipMemcpyAsync((unsigned char*)host + off, (const unsigned char*)dev + off, bytes,
-                                 hipMemcpyDeviceToHost, cs));
+        if (mode >= 2 && view) {
+            k_copy_to_host<<<mode, 256, 0, cs>>>(src, (unsigned char*)view + off, bytes);
+            HIP_CHECK(hipGetLastError());
+        } else {
+            HIP_CHECK(hipMemcpyAsync((unsigned char*)host + off, src, bytes, hipMemcpyDeviceToHost, cs));
+        }
         early_bytes += bytes;
+    }
+    // wait for every copy; throws on a failed one
+    void finish() {
+        if (worker.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                closing = true;
+            }
+            cv.notify_one();
+            worker.join();
+        }
+        for (hsa_signal_t sg : sigs) {
+            hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            hsa_signal_destroy(sg);
+        }
+        sigs.clear();
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        evs.clear();
+        HIP_CHECK(hipStreamSynchronize(cs));
+        if (!err.empty()) fail(SRG_ERR_HIP, "D2H copy: " + err);
+    }
+    ~HostSink() {  // an exception unwound past finish(): drain before the buffers go away
+        if (worker.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                closing = true;
+            }
+            cv.notify_one();
+            worker.join();
+        }
+        for (hsa_signal_t sg : sigs) {
+            hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            hsa_signal_destroy(sg);
+        }
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     }
 };
 
@@ -1245,13 +1438,13 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 }
             }
             ms_scan = tm.lap();
-            const size_t lds_rows = (size_t)V * 12;
+            const size_t lds_rows = loss_rows_lds(V);
             if (lds_rows <= 150 * 1024) {
                 // per-row Gauss-Seidel in LDS, writes out_loss directly
                 set_lds(k_loss_rows<K>, lds_rows);
                 HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
                 // host entry: row chunks, each chunk's loss rows sent as soon as it is done
-                const uint32_t nchunk = sink_rows ? std::min<uint32_t>(8, nloc) : 1;
+                const uint32_t nchunk = std::max<uint32_t>(1, std::min<uint32_t>(c.loss_chunks ? c.loss_chunks : sink_rows ? 8 : 1, nloc));
                 for (uint32_t q = 0; q < nchunk; ++q) {
                     const uint32_t r0 = (uint32_t)((uint64_t)nloc * q / nchunk);
                     const uint32_t r1 = (uint32_t)((uint64_t)nloc * (q + 1) / nchunk);
@@ -1777,6 +1970,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         bool ok = false;
         double ms = 0;
         void* p[2] = {nullptr, nullptr};
+        void* view[2] = {nullptr, nullptr};  // device pointers of the mapped registrations
         size_t b[2] = {0, 0};
         hipStream_t wait = nullptr;
         bool join() {
@@ -1802,11 +1996,13 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         reg.th = std::thread([&reg]() {
             const auto t0 = std::chrono::steady_clock::now();
             if (hipSetDevice(reg.device) != hipSuccess) return;
-            if (hipHostRegister(reg.p[0], reg.b[0], hipHostRegisterDefault) != hipSuccess) return;
-            if (hipHostRegister(reg.p[1], reg.b[1], hipHostRegisterDefault) != hipSuccess) {
+            if (hipHostRegister(reg.p[0], reg.b[0], hipHostRegisterMapped) != hipSuccess) return;
+            if (hipHostRegister(reg.p[1], reg.b[1], hipHostRegisterMapped) != hipSuccess) {
                 (void)hipHostUnregister(reg.p[0]);
                 return;
             }
+            for (int i = 0; i < 2; ++i)
+                if (hipHostGetDevicePointer(&reg.view[i], reg.p[i], 0) != hipSuccess) reg.view[i] = nullptr;
             reg.ms = ms_since(t0);
             reg.ok = true;
         });
@@ -1834,7 +2030,17 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         sink.n = n;
         sink.cs = c->d2h_stream;
         sink.ev = c->ev_e;
-        if (early) sink.ready = [&reg]() { return reg.join(); };
+        if (early) {
+            sink.mode = c->d2h_mode;
+            sink.sdma = &c->sdma;
+            sink.device = c->device;
+            sink.ready = [&reg, &sink]() {
+                if (!reg.join()) return false;
+                sink.lat_view = reg.view[0];
+                sink.loss_view = reg.view[1];
+                return true;
+            };
+        }
         if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
         else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr);
         auto t1 = std::chrono::steady_clock::now();
@@ -1848,7 +2054,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         if (nn && !sink.lat_sent) HIP_CHECK(hipMemcpyAsync(out_lat, dol, nn * 8, hipMemcpyDeviceToHost, st));
         if (nn && !sink.loss_sent) HIP_CHECK(hipMemcpyAsync(out_loss, dos, nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
-        HIP_CHECK(hipStreamSynchronize(c->d2h_stream));
+        sink.finish();
         if (stats) {
             stats->ms_h2d = ms_h2d;
             stats->ms_d2h = ms_since(t1);  // the D2H not hidden behind kernels
@@ -1889,6 +2095,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+        c->sdma.init(device);  // SDMA engine for the host entry's early D2H (else hipMemcpyAsync)
         for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     });
@@ -1970,6 +2177,14 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_LOSS_CHUNKS:
+            if (value < 0 || value > 1024) return SRG_ERR_ARG;
+            ctx->loss_chunks = (int)value;
+            return SRG_OK;
+        case SRG_OPT_D2H_MODE:
+            if (value < 0 || value > 1024) return SRG_ERR_ARG;
+            ctx->d2h_mode = (int)value;
             return SRG_OK;
         case SRG_OPT_CHAIN_SPLIT:
             if (!(value == 1 || value == 2 || value == 4 || value == 8)) return SRG_ERR_ARG;

@@ -1266,7 +1266,15 @@ __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ld
 // L[t] = fold(L[U[t]], B[t]) at once, whose solution on the tight DAG is unique (induction on
 // depth), so it equals Dijkstra's lexicographic scores (mod.rs:305-331).  Writes the used
 // columns of the row straight into out_loss (diagonal = raw self-loop loss, mod.rs:216).
+// Targets with several latency-tight predecessors (PRED_MULTI, rare) get their tight in-edges
+// collected once, by the whole workgroup scanning the CSC list in parallel, into an LDS list the
+// sweeps fold over; one thread walking ~V/10 CSC entries with two dependent global loads per
+// entry in every sweep made such rows ~1 ms stragglers (every row-chunk launch waited for one).
+// Overflow past LM_T targets / LM_E edges per target falls back to that per-thread walk.
 constexpr uint32_t U_SELF = 0xFFFFFFFFu, U_NONE = 0xFFFFFFFEu, U_MULTI = 0xFFFFFFFDu;
+constexpr uint32_t U_MLIST = 0xF0000000u;  // U_MLIST + i: multi target i of the LDS list
+constexpr uint32_t LM_T = 32, LM_E = 16;
+constexpr size_t loss_rows_lds(uint32_t V) { return (size_t)V * 12 + LM_T * (4 + 4 + LM_E * 8) + 16; }
 
 template <class K>
 __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__ PRED, size_t ldp, uint32_t V,
@@ -1284,10 +1292,17 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
     uint32_t* U = reinterpret_cast<uint32_t*>(smem_raw);
     float* Bf = reinterpret_cast<float*>(U + V);
     float* L = Bf + V;
-    __shared__ uint32_t changed;
+    uint32_t* m_t = reinterpret_cast<uint32_t*>(L + V);  // [LM_T] multi targets
+    uint32_t* m_n = m_t + LM_T;                          // [LM_T] tight in-edges collected
+    uint32_t* m_u = m_n + LM_T;                          // [LM_T][LM_E] their sources
+    float* m_b = reinterpret_cast<float*>(m_u + LM_T * LM_E);  // [LM_T][LM_E] 1 - loss
+    __shared__ uint32_t changed, nm;
     const uint32_t r = row0 + blockIdx.x;  // launched in row chunks (host entry: D2H per chunk)
     const uint32_t s = nodes[r];
     const uint32_t* prow = PRED + (size_t)r * ldp;
+    if (threadIdx.x == 0) nm = 0;
+    if (threadIdx.x < LM_T) m_n[threadIdx.x] = 0;
+    __syncthreads();
     for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) {
         const uint32_t p = prow[t];
         uint32_t u;
@@ -1298,7 +1313,12 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
         } else if (p == PRED_NONE) {
             u = U_NONE;
         } else if (p == PRED_MULTI) {
+            const uint32_t i = atomicAdd(&nm, 1u);
             u = U_MULTI;
+            if (i < LM_T) {
+                m_t[i] = t;
+                u = U_MLIST + i;
+            }
         } else {
             u = ent_u[p];
             bb = ent_b[p];
@@ -1307,6 +1327,26 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
         Bf[t] = bb;
         L[t] = l;
     }
+    __syncthreads();
+    const uint32_t nml = nm < LM_T ? nm : LM_T;
+    for (uint32_t i = 0; i < nml; ++i) {  // whole workgroup per multi target
+        const uint32_t t = m_t[i];
+        const K dst = DST[(size_t)t * npad + r];
+        for (uint32_t k = csc_off[t] + threadIdx.x; k < csc_off[t + 1]; k += blockDim.x) {
+            const uint32_t e = csc_ent[k];
+            const uint32_t uu = ent_u[e];
+            if (KeyOps<K>::add(DST[(size_t)uu * npad + r], ent_w[e]) != dst) continue;
+            const uint32_t j = atomicAdd(&m_n[i], 1u);
+            if (j < LM_E) {
+                m_u[i * LM_E + j] = uu;
+                m_b[i * LM_E + j] = ent_b[e];
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nml; i += blockDim.x)
+        if (m_n[i] > LM_E) U[m_t[i]] = U_MULTI;  // too many tight in-edges: per-thread walk
+    __syncthreads();
     uint32_t sweeps = 0;
     for (;;) {
         if (threadIdx.x == 0) changed = 0;
@@ -1314,17 +1354,25 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
         uint32_t ch = 0;
         for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) {
             const uint32_t u = U[t];
-            if (u >= U_MULTI) {
-                if (u != U_MULTI) continue;
-                // several latency-tight predecessors: min over them (in-edges of t)
-                const K dst = DST[(size_t)t * npad + r];
+            if (u >= U_MLIST) {
+                if (u >= U_NONE) continue;
                 float v = 1.0f;
-                for (uint32_t k = csc_off[t]; k < csc_off[t + 1]; ++k) {
-                    const uint32_t e = csc_ent[k];
-                    const uint32_t uu = ent_u[e];
-                    if (KeyOps<K>::add(DST[(size_t)uu * npad + r], ent_w[e]) != dst) continue;
-                    const float cnd = fold_loss(L[uu], ent_b[e]);
-                    v = cnd < v ? cnd : v;
+                if (u == U_MULTI) {
+                    // several latency-tight predecessors: min over them (in-edges of t)
+                    const K dst = DST[(size_t)t * npad + r];
+                    for (uint32_t k = csc_off[t]; k < csc_off[t + 1]; ++k) {
+                        const uint32_t e = csc_ent[k];
+                        const uint32_t uu = ent_u[e];
+                        if (KeyOps<K>::add(DST[(size_t)uu * npad + r], ent_w[e]) != dst) continue;
+                        const float cnd = fold_loss(L[uu], ent_b[e]);
+                        v = cnd < v ? cnd : v;
+                    }
+                } else {
+                    const uint32_t i = u - U_MLIST;
+                    for (uint32_t j = 0; j < m_n[i]; ++j) {
+                        const float cnd = fold_loss(L[m_u[i * LM_E + j]], m_b[i * LM_E + j]);
+                        v = cnd < v ? cnd : v;
+                    }
                 }
                 if (v != L[t]) {
                     L[t] = v;

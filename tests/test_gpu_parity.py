@@ -330,6 +330,32 @@ def test_device_entry_matches_host(router):
     assert bits_equal(os_.cpu().numpy(), t.packet_loss)
 
 
+@pytest.mark.parametrize("mode", [1, 0, 2, 32])
+def test_host_entry_early_rows_match_device(router, mode):
+    """Host entry with finished rows shipped while kernels run (table >= 64 MB: the caller's arrays
+    are page-locked and filled by an SDMA engine (mode 1, default), hipMemcpyAsync (0) or a copy
+    kernel of `mode` workgroups) equals the device entry byte for byte; odd n makes the loss rows
+    start off 16-B boundaries."""
+    import torch
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+    V = 2501
+    g = synth.atlas_like(V, seed=77)
+    router.set_option(N.SRG_OPT_D2H_MODE, mode)
+    try:
+        t = router.compute_shortest_paths(g, list(range(V)))
+    finally:
+        router.set_option(N.SRG_OPT_D2H_MODE, 1)
+    assert t.stats["d2h_overlapped_bytes"] == V * V * 12
+    dg = DeviceGraph(g)
+    nodes = torch.arange(V, dtype=torch.int32, device="cuda:0")
+    ol = torch.empty((V, V), dtype=torch.int64, device="cuda:0")
+    os_ = torch.empty((V, V), dtype=torch.float32, device="cuda:0")
+    compute_shortest_paths_device(router, dg, nodes, ol, os_)
+    torch.cuda.synchronize()
+    assert np.array_equal(ol.cpu().numpy().view(np.uint64), t.latency_ns)
+    assert bits_equal(os_.cpu().numpy(), t.packet_loss)
+
+
 @pytest.mark.slow
 def test_c1_full_vs_oracle(router):
     """Config C1 (1000-vertex complete graph), every pair."""

@@ -1,0 +1,160 @@
+// sparse_sim.cpp — CPU model of k_sparse_bf's sweep schedule (latency only), to compare batch
+// compositions and bucket widths by the number of label-row pulls they cause, without a GPU.
+// Not product code; not a checker.  Input: CSR dumped by tools/sparse_sim.py.
+//   usage: sparse_sim <csr.bin> <order.bin> <delta> <nbatches> [stride]
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+int main(int argc, char** argv) {
+    if (argc < 5) return 1;
+    FILE* f = fopen(argv[1], "rb");
+    uint32_t V, A;
+    fread(&V, 4, 1, f);
+    fread(&A, 4, 1, f);
+    std::vector<uint32_t> off(V + 1), src(A), w(A);
+    fread(off.data(), 4, V + 1, f);
+    fread(src.data(), 4, A, f);
+    fread(w.data(), 4, A, f);
+    fclose(f);
+    FILE* g = fopen(argv[2], "rb");
+    std::vector<uint32_t> order(V);
+    fread(order.data(), 4, V, g);
+    fclose(g);
+    const uint32_t delta = (uint32_t)strtoul(argv[3], 0, 10);
+    const int nb = atoi(argv[4]);
+    const int stride = argc > 5 ? atoi(argv[5]) : 1;
+    const int per_lane = argc > 6 ? atoi(argv[6]) : 0;
+    const uint32_t INF = 0xFFFFFFFFu;
+    std::vector<uint32_t> L((size_t)V * 64);
+    std::vector<uint8_t> fprev(V), fcur(V), mark(V), mnext(V), pend(V);
+    double tot_pulls = 0, tot_sweeps = 0, tot_lanechg = 0;
+    const uint32_t nbatch = V / 64;
+    for (int bi = 0; bi < nb; ++bi) {
+        const uint32_t b = (uint32_t)((bi * (size_t)stride) % nbatch);
+        for (size_t i = 0; i < L.size(); ++i) L[i] = INF;
+        std::fill(fprev.begin(), fprev.end(), 0);
+        std::fill(mark.begin(), mark.end(), 0);
+        std::fill(pend.begin(), pend.end(), 0);
+        std::fill(mnext.begin(), mnext.end(), 0);
+        std::fill(fcur.begin(), fcur.end(), 0);
+        for (int l = 0; l < 64; ++l) {
+            uint32_t s = order[b * 64 + l];
+            L[(size_t)s * 64 + l] = 0;
+            fprev[s] = 1;
+            for (uint32_t k = off[s]; k < off[s + 1]; ++k) mark[src[k]] = 1;  // undirected: out == in
+        }
+        uint32_t bound = delta;
+        uint64_t pulls = 0, lanechg = 0;
+        int sweeps = 0;
+        if (per_lane) {
+            // per-lane buckets: a lane of u is pushed only when it changed since its last push and
+            // is below the bound; a vertex row is pulled by its out-neighbours when any lane is pushed
+            std::vector<uint64_t> dirty(V, 0), pm(V, 0);
+            for (int l = 0; l < 64; ++l) dirty[order[b * 64 + l]] |= 1ull << l;
+            for (;;) {
+                bool anyact = false, anydirty = false;
+                for (uint32_t u = 0; u < V; ++u) {
+                    uint64_t bl = 0;
+                    if (dirty[u])
+                        for (int l = 0; l < 64; ++l)
+                            if (((dirty[u] >> l) & 1) && L[(size_t)u * 64 + l] < bound) bl |= 1ull << l;
+                    pm[u] = bl;
+                    anyact |= bl != 0;
+                    anydirty |= dirty[u] != 0;
+                }
+                if (!anydirty) break;
+                if (!anyact) {
+                    bound = bound > INF - delta ? INF : bound + delta;
+                    continue;
+                }
+                for (uint32_t u = 0; u < V; ++u) dirty[u] &= ~pm[u];
+                for (uint32_t t = 0; t < V; ++t) {
+                    bool m = false;
+                    for (uint32_t k = off[t]; k < off[t + 1]; ++k) m |= pm[src[k]] != 0;
+                    if (!m) continue;
+                    pulls++;
+                    uint32_t* lt = &L[(size_t)t * 64];
+                    for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
+                        const uint32_t u = src[k];
+                        if (!pm[u]) continue;
+                        pulls++;
+                        const uint32_t* lu = &L[(size_t)u * 64];
+                        for (int l = 0; l < 64; ++l)
+                            if (((pm[u] >> l) & 1) && lu[l] + w[k] < lt[l]) {
+                                lt[l] = lu[l] + w[k];
+                                dirty[t] |= 1ull << l;
+                                lanechg++;
+                            }
+                    }
+                }
+                ++sweeps;
+            }
+            tot_pulls += pulls;
+            tot_sweeps += sweeps;
+            tot_lanechg += lanechg;
+            continue;
+        }
+        for (;;) {
+            bool any = false, anyp = false;
+            for (uint32_t t = 0; t < V; ++t) {
+                if (!mark[t]) continue;
+                uint32_t* lt = &L[(size_t)t * 64];
+                uint32_t nl[64];
+                for (int l = 0; l < 64; ++l) nl[l] = lt[l];
+                pulls++;  // own row
+                for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
+                    uint32_t u = src[k];
+                    if (!fprev[u]) continue;
+                    pulls++;
+                    const uint32_t* lu = &L[(size_t)u * 64];
+                    for (int l = 0; l < 64; ++l)
+                        if (lu[l] != INF && lu[l] + w[k] < nl[l]) nl[l] = lu[l] + w[k];
+                }
+                bool drop = false, below = false;
+                for (int l = 0; l < 64; ++l)
+                    if (nl[l] < lt[l]) {
+                        drop = true;
+                        lanechg++;
+                        if (nl[l] < bound) below = true;
+                        lt[l] = nl[l];
+                    }
+                if (drop) {
+                    if (below) {
+                        fcur[t] = 1;
+                        pend[t] = 0;
+                        any = true;
+                        for (uint32_t k = off[t]; k < off[t + 1]; ++k) mnext[src[k]] = 1;
+                    } else {
+                        pend[t] = 1;
+                    }
+                }
+            }
+            ++sweeps;
+            for (uint32_t v = 0; v < V; ++v) {
+                fprev[v] = fcur[v];
+                fcur[v] = 0;
+                mark[v] = mnext[v];
+                mnext[v] = 0;
+                anyp |= pend[v] != 0;
+            }
+            if (!any) {
+                if (!anyp) break;
+                bound = bound > INF - delta ? INF : bound + delta;
+                for (uint32_t v = 0; v < V; ++v) {
+                    fprev[v] = pend[v];
+                    if (pend[v])
+                        for (uint32_t k = off[v]; k < off[v + 1]; ++k) mark[src[k]] = 1;
+                    pend[v] = 0;
+                }
+            }
+        }
+        tot_pulls += pulls;
+        tot_sweeps += sweeps;
+        tot_lanechg += lanechg;
+    }
+    printf("{\"pulls_per_arc\": %.3f, \"sweeps\": %.2f, \"lane_changes_per_vertex_lane\": %.3f}\n",
+           tot_pulls / nb / A, tot_sweeps / nb, tot_lanechg / nb / (64.0 * V));
+    return 0;
+}
