@@ -155,6 +155,9 @@ void srg_destroy(srg_ctx* ctx);
                                      * hipMemcpyAsync, N >= 2 = a copy kernel of N workgroups */
 #define SRG_OPT_LOSS_CHUNKS 21       /* dense: k_loss_rows launches (row chunks); 0 (default) = 8 when the host
                                      * entry ships rows early, else 1 */
+#define SRG_OPT_SCAN_GROUPS 22       /* host entry, u32 scan variants 5/6: source-block groups the scan is
+                                     * launched in, each group's loss rows folded and shipped while
+                                     * later groups scan; 0 (default) = 3, 1 = scan, then loss */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -954,16 +954,17 @@ struct alignas(64) V5Grp {
     uint32_t v[16];
 };
 
-// grid: 8 * nbTT * ceil(nbS / 8) workgroups of 512 (XCD-aware: the workgroups of one XCD share
-// the 128-source block, whose staged rows then come out of that XCD's L2)
+// grid: 8 * nbTT * ceil((nbS - c0) / 8) workgroups of 512 for the source blocks [c0, nbS)
+// (XCD-aware: the workgroups of one XCD share the 128-source block, whose staged rows then come
+// out of that XCD's L2)
 __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
-                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
                                                     uint32_t* __restrict__ PRED, size_t ldp) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
-    const uint32_t c = xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
     if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1078,12 +1079,12 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
 // pair j with four v_readlane; the rest of the pair's work is v5's.
 __global__ void __launch_bounds__(512, 4) tight_v6(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
-                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
                                                     uint32_t* __restrict__ PRED, size_t ldp) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
-    const uint32_t c = xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
     if (c >= nbS) return;  // whole workgroup
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);

@@ -330,21 +330,24 @@ def test_device_entry_matches_host(router):
     assert bits_equal(os_.cpu().numpy(), t.packet_loss)
 
 
-@pytest.mark.parametrize("mode", [1, 0, 2, 32])
-def test_host_entry_early_rows_match_device(router, mode):
+@pytest.mark.parametrize("mode,groups", [(1, 0), (0, 0), (2, 1), (32, 0), (1, 1), (1, 2), (1, 7), (0, 3)])
+def test_host_entry_early_rows_match_device(router, mode, groups):
     """Host entry with finished rows shipped while kernels run (table >= 64 MB: the caller's arrays
     are page-locked and filled by an SDMA engine (mode 1, default), hipMemcpyAsync (0) or a copy
-    kernel of `mode` workgroups) equals the device entry byte for byte; odd n makes the loss rows
-    start off 16-B boundaries."""
+    kernel of `mode` workgroups) equals the device entry byte for byte, with the scan launched in
+    `groups` source-block groups interleaved with the loss rows (0 = default 3, 1 = not
+    interleaved, 7 = ragged groups); odd n makes the loss rows start off 16-B boundaries."""
     import torch
     from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
     V = 2501
     g = synth.atlas_like(V, seed=77)
     router.set_option(N.SRG_OPT_D2H_MODE, mode)
+    router.set_option(N.SRG_OPT_SCAN_GROUPS, groups)
     try:
         t = router.compute_shortest_paths(g, list(range(V)))
     finally:
         router.set_option(N.SRG_OPT_D2H_MODE, 1)
+        router.set_option(N.SRG_OPT_SCAN_GROUPS, 0)
     assert t.stats["d2h_overlapped_bytes"] == V * V * 12
     dg = DeviceGraph(g)
     nodes = torch.arange(V, dtype=torch.int32, device="cuda:0")
