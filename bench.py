@@ -256,6 +256,7 @@ def main():
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--d2h-mode", type=int, default=None,
                     help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync, N >= 2 = copy kernel of N workgroups")
+    ap.add_argument("--fw-fold", type=int, default=None, help="symmetric FW: 1 = add,add,min3; 0 = lshl_add_u64,min3")
     ap.add_argument("--scan-groups", type=int, default=None, help="host entry: scan launches interleaved with the loss (0 = auto)")
     ap.add_argument("--loss-chunks", type=int, default=None, help="dense: k_loss_rows launches (0 = auto)")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
@@ -351,6 +352,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
+    if args.fw_fold is not None:
+        router.set_option(N.SRG_OPT_FW_FOLD, args.fw_fold)
     if args.scan_groups is not None:
         router.set_option(N.SRG_OPT_SCAN_GROUPS, args.scan_groups)
     if args.loss_chunks is not None:

@@ -158,6 +158,8 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SCAN_GROUPS 22       /* host entry, u32 scan variants 5/6: source-block groups the scan is
                                      * launched in, each group's loss rows folded and shipped while
                                      * later groups scan; 0 (default) = 3, 1 = scan, then loss */
+#define SRG_OPT_FW_FOLD 23           /* symmetric u32 FW: instructions of a k-pair's two relaxations, 0 (default) =
+                                     * v_lshl_add_u64 + v_min3_u32, 1 = two v_add_u32 + v_min3_u32 (slower) */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -647,8 +647,13 @@ __device__ __forceinline__ void sym_store(const SymOp<T, KC>& o, u64p* __restric
     }
 }
 
-// one stored tile C = (I, J), I <= J, relaxed through pivot block kb (pair-packed, as fw_tile_pk)
-template <int T, int KC>
+// one stored tile C = (I, J), I <= J, relaxed through pivot block kb (k-pair LDS image as fw_tile_pk).
+// FOLD (SRG_OPT_FW_FOLD) picks the instructions of the two relaxations of one k-pair:
+//   0 = one v_lshl_add_u64 over the packed pairs + v_min3_u32
+//   1 = two v_add_u32 over the 32-bit halves + v_min3_u32: the VALU microbenchmark rates (add 0.40,
+//       min3 0.25, lshl_add_u64 0.195 wave-instr/SIMD/cycle) predicted it faster; in the tile it is
+//       slower (C3 bulk launch 0.304 vs 0.242 ms, profiles/r02c/fw_fold.txt), so 0 stays default
+template <int T, int KC, int FOLD = 0>
 __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
     using S = SymOp<T, KC>;
     constexpr int M = T / 16;
@@ -712,8 +717,14 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b) {
-                    const u64p s = add_pairs(ap[a], bp[b]);
-                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                    if constexpr (FOLD == 1) {
+                        const uint32_t lo = (uint32_t)ap[a] + (uint32_t)bp[b];
+                        const uint32_t hi = (uint32_t)(ap[a] >> 32) + (uint32_t)(bp[b] >> 32);
+                        c[a][b] = KeyOps<uint32_t>::min3(c[a][b], lo, hi);
+                    } else {
+                        const u64p s = add_pairs(ap[a], bp[b]);
+                        c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                    }
                 }
         }
         if (ch + 1 < ch1) {  // write late into the other buffer
@@ -741,12 +752,12 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
     }
 }
 
-template <int T, int KC>
+template <int T, int KC, int FOLD = 0>
 __global__ void __launch_bounds__(256, 3) fw_product_sym(uint32_t* __restrict__ D, size_t ld, int kb, SymSet s, int prio) {
     int I, J;
     if (!sym_tile(s, (int)blockIdx.x, I, J)) return;  // whole workgroup
     if (prio) __builtin_amdgcn_s_setprio(3);  // chain (line) launches: see fw_phase1
-    fw_tile_sym<T, KC>(D, ld, kb, I, J);
+    fw_tile_sym<T, KC, FOLD>(D, ld, kb, I, J);
 }
 
 // lower triangle <- transpose of the upper one, 64 x 64 blocks (bi > bj) through LDS

@@ -484,6 +484,7 @@ struct srg_ctx {
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
     int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync, >= 2 = copy kernel of that many workgroups (SRG_OPT_D2H_MODE)
     SdmaAgents sdma;
+    int fw_fold = 0;                 // symmetric FW: 0 = v_lshl_add_u64 + v_min3 per k-pair, 1 = two v_add_u32 + v_min3 (SRG_OPT_FW_FOLD; 1 measured 0.304 vs 0.242 ms per bulk launch)
     int scan_groups = 0;             // host entry: v5 scan launches interleaved with the loss rows (0 = auto: 3) (SRG_OPT_SCAN_GROUPS)
     int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
     int scan_variant = 5;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs, 3/4 = LDS u-chunks (one source per lane), 5 (default) / 6 = LDS u-chunks, two sources per lane (scalar / vector record stream)
@@ -999,13 +1000,13 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
 // fw_tile_sym), then the lower triangle is mirrored.  The chain of pivot k1 updates line k1
 // (row k1 = column k1^T) w.r.t. kb, closes k1, and updates line k1 w.r.t. k1; the bulk of kb
 // is every stored tile off the lines kb and k1.
-template <int T>
+template <int T, int FOLD>
 void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
                     int& prof_n) {
     constexpr int KCS = 16;
     const int nb = pl.nb;
     const size_t lds = pk_lds_bytes<T, KCS>();
-    set_lds(fw_product_sym<T, KCS>, lds);
+    set_lds(fw_product_sym<T, KCS, FOLD>, lds);
     const bool prof = c.profiling && nb > 2;
     if (prof) {
         while (c.prof_events.size() < (size_t)2 * nb) {
@@ -1018,14 +1019,14 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
     // line launches sit on the critical chain: split-K so that ~nb x split workgroups share a tile
     const int lsplit = std::max(1, std::min(c.chain_split, T / KCS));
     auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
-        fw_product_sym<T, KCS><<<dim3(nb, 1, lsplit), 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
+        fw_product_sym<T, KCS, FOLD><<<dim3(nb, 1, lsplit), 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
     };
     fw_phase1<uint32_t, T><<<1, 512, 0, st>>>(D, Vp, 0, c.chain_prio);
     if (nb > 1) line(0, 0, 0, -1, st);
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
         if (k1 >= nb) {
-            if (nb > 1) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
+            if (nb > 1) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
             break;
         }
         HIP_CHECK(hipEventRecord(c.ev_a, st));
@@ -1037,7 +1038,7 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
         const int m = nb - 2;  // lines kb and k1 excluded
         const bool timed = prof && m > 0;
         if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        if (m > 0) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
+        if (m > 0) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
         if (timed) {
             HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
             prof_relax += (uint64_t)m * (m + 1) / 2 * T * T * T;
@@ -1096,7 +1097,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     int prof_n = 0;
     const bool sym_fw = sizeof(K) == 4 && T == 128 && c.fw_symmetric && !g.directed && !multi && c.fw_packed != 0;
     if (sym_fw) {
-        if constexpr (sizeof(K) == 4 && T == 128) fw_blocked_sym<T>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
+        if constexpr (sizeof(K) == 4 && T == 128) {
+            if (c.fw_fold == 1) fw_blocked_sym<T, 1>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
+            else fw_blocked_sym<T, 0>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
+        }
     } else if constexpr (sizeof(K) == 4) {
         switch (c.fw_packed) {
             case 0: fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n); break;
@@ -2213,6 +2217,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_FW_FOLD:
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            ctx->fw_fold = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_GROUPS:
             if (value < 0 || value > 1024) return SRG_ERR_ARG;

@@ -137,15 +137,17 @@ def test_fw_symmetric_matches_general(V):
     g = synth.atlas_like(V, seed=V + 7)
     nodes = np.random.default_rng(V).permutation(V).tolist()
     out = []
-    for sym in (0, 1):
+    for sym, fold in ((0, 1), (1, 1), (1, 0)):  # general FW; symmetric with either fold (SRG_OPT_FW_FOLD)
         r = Router(0)
         r.set_option(N.SRG_OPT_FW_SYMMETRIC, sym)
+        r.set_option(N.SRG_OPT_FW_FOLD, fold)
         t = r.compute_shortest_paths(g, nodes)
         assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
         out.append(t)
         r.close()
-    assert np.array_equal(out[0].latency_ns, out[1].latency_ns)
-    assert bits_equal(out[0].packet_loss, out[1].packet_loss)
+    for o in out[1:]:
+        assert np.array_equal(out[0].latency_ns, o.latency_ns)
+        assert bits_equal(out[0].packet_loss, o.packet_loss)
     if V <= 300:
         lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
         assert_parity(out[1], lat, loss)
