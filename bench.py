@@ -256,6 +256,7 @@ def main():
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--d2h-mode", type=int, default=None,
                     help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync, N >= 2 = copy kernel of N workgroups")
+    ap.add_argument("--chain-cus", type=int, default=None, help="symmetric FW: CUs reserved for the chain (0 = none)")
     ap.add_argument("--fw-fold", type=int, default=None, help="symmetric FW: 1 = add,add,min3; 0 = lshl_add_u64,min3")
     ap.add_argument("--scan-groups", type=int, default=None, help="host entry: scan launches interleaved with the loss (0 = auto)")
     ap.add_argument("--loss-chunks", type=int, default=None, help="dense: k_loss_rows launches (0 = auto)")
@@ -352,6 +353,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
+    if args.chain_cus is not None:
+        router.set_option(N.SRG_OPT_CHAIN_CUS, args.chain_cus)
     if args.fw_fold is not None:
         router.set_option(N.SRG_OPT_FW_FOLD, args.fw_fold)
     if args.scan_groups is not None:
@@ -426,7 +429,8 @@ def main():
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
             f"w{args.sparse_wgs or 2}" + (f":lm{args.sparse_lane_masks}" if args.sparse_lane_masks else "")
             + (f":sl{args.sparse_split_labels}" if args.sparse_split_labels else "")
-            + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else ""))
+            + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
+            + (f":fold{args.fw_fold}" if args.fw_fold else "") + (f":cus{args.chain_cus}" if args.chain_cus else ""))
     roofline = None
     if agg.get("prof_launches") and kind == 3:
         # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
@@ -442,7 +446,8 @@ def main():
                     "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
                     "bytes_per_source": per_src, "sources_per_launch": int(srcs), "traffic_source": tsrc,
                     # measured HBM bytes per launch over this run's launch time: the real HBM rate
-                    "traffic_GBps": round(traffic / (avg_ms * 1e-3) / 1e9, 1) if traffic else None}
+                    "traffic_GBps": round(traffic / (avg_ms * 1e-3) / 1e9, 1) if traffic else None,
+                    "workload_key": wkey}
     elif agg.get("prof_launches"):
         avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
         relax = agg["prof_relaxations"] / agg["prof_launches"]
@@ -463,7 +468,13 @@ def main():
                     "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
                     "ops_per_relaxation": OPS_PER_RELAX.get(kind, 2.0), "relax_per_s": round(relax / (avg_ms * 1e-3), 1),
-                    "traffic_source": tsrc}
+                    "traffic_source": tsrc, "workload_key": wkey}
+        if kind == 0 and args.fw_packed and not args.fw_fold:
+            # v_min* issue at half rate on gfx950: the pair-packed relaxation pair (v_lshl_add_u64 +
+            # v_min3_u32) measured 0.187 wave-instr/SIMD/cycle = 2 relaxations per 10.7 cycles per
+            # wave = 0.748 of the 2-op lane peak (profiles/r01_valu_rate_microbench.txt)
+            roofline["instruction_mix_ceiling_frac"] = 0.748
+            roofline["frac_of_mix_ceiling"] = round(achieved / VALU_PEAK_TOPS / 0.748, 4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.simulate_rank:

@@ -37,8 +37,11 @@ extern "C" {
 #define SRG_ERR_NO_EDGE 2       /* "No edge connecting node {src_id} to {dst_id}"       mod.rs:266-268 */
 #define SRG_ERR_MULTI_EDGE 3    /* "More than one edge connecting node {a} to {b}"      mod.rs:269-274 */
 #define SRG_ERR_UNREACHABLE 4   /* assert_eq!(paths.len(), nodes.len().pow(2)) panics   mod.rs:219 */
-#define SRG_ERR_LATENCY_RANGE 5 /* latency.convert(Nano).unwrap() overflow (mod.rs:336) or a
-                                   path sum beyond 2^62 ns (reference would wrap u64) */
+#define SRG_ERR_LATENCY_RANGE 5 /* latency.convert(Nano).unwrap() overflow (mod.rs:336), or a used
+                                   pair with no path below 2^62 ns on a graph whose worst-case path
+                                   sum reaches 2^62 (unreachable, or a sum the reference's u64 would
+                                   wrap); a graph whose used pairs all have paths below 2^62 ns
+                                   succeeds whatever its edge latencies */
 #define SRG_ERR_HIP 6           /* HIP runtime failure (no device, launch failure) */
 #define SRG_ERR_OOM 7           /* device allocation failed */
 #define SRG_ERR_PARSE 8         /* GML / attribute error from NetworkGraph::parse (mod.rs:134-181) */
@@ -133,11 +136,12 @@ void srg_destroy(srg_ctx* ctx);
                                      per SIMD); 3 = 16-deep with prefetch; 0 = one add per relaxation */
 #define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 5 (default) = two sources per lane over
                                      LDS-staged rows (ds_read_b64) with a 4-pair scalar record stream; 6 = the
-                                     same with the records in vector registers (v_readlane); 4 / 3 = one source per
+                                     same with the records in vector registers (v_readlane); 7 = the records staged
+                                     in LDS with the rows (no scalar loads in the loop); 4 / 3 = one source per
                                      lane over LDS-staged rows (v_readlane / s_load entry reads); 2 = entries
                                      grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches
                                      broadcast with v_readlane */
-#define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) */
+#define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) / 16 (one workgroup per CU) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
                                         0 = a single bucket (plain Bellman-Ford); default 1 */
@@ -160,6 +164,8 @@ void srg_destroy(srg_ctx* ctx);
                                      * later groups scan; 0 (default) = 3, 1 = scan, then loss */
 #define SRG_OPT_FW_FOLD 23           /* symmetric u32 FW: instructions of a k-pair's two relaxations, 0 (default) =
                                      * v_lshl_add_u64 + v_min3_u32, 1 = two v_add_u32 + v_min3_u32 (slower) */
+#define SRG_OPT_CHAIN_CUS 24         /* symmetric u32 FW: CUs reserved for the lookahead chain through CU-masked
+                                     * streams (n evenly spaced CU ids; -n = the lowest n ids); 0 = none */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -51,6 +51,7 @@ SRG_OPT_D2H_MODE = 20
 SRG_OPT_LOSS_CHUNKS = 21
 SRG_OPT_SCAN_GROUPS = 22
 SRG_OPT_FW_FOLD = 23
+SRG_OPT_CHAIN_CUS = 24
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

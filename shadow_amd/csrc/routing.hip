@@ -484,6 +484,9 @@ struct srg_ctx {
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
     int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync, >= 2 = copy kernel of that many workgroups (SRG_OPT_D2H_MODE)
     SdmaAgents sdma;
+    int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
+    int cu_streams_for = 0;          // chain_cus the two CU-masked streams below were made for
+    hipStream_t cu_bulk = nullptr, cu_chain = nullptr;
     int fw_fold = 0;                 // symmetric FW: 0 = v_lshl_add_u64 + v_min3 per k-pair, 1 = two v_add_u32 + v_min3 (SRG_OPT_FW_FOLD; 1 measured 0.304 vs 0.242 ms per bulk launch)
     int scan_groups = 0;             // host entry: v5 scan launches interleaved with the loss rows (0 = auto: 3) (SRG_OPT_SCAN_GROUPS)
     int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
@@ -518,7 +521,7 @@ struct srg_ctx {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e})
             if (e) (void)hipEventDestroy(e);
-        for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream})
+        for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream, cu_bulk, cu_chain})
             if (s) (void)hipStreamDestroy(s);
     }
 };
@@ -562,6 +565,8 @@ struct Prelude {
     float* selfloss;
     Flags* flags;
     std::vector<uint32_t> nodes_h;  // host copy of `nodes` (partitioning, error text)
+    bool range_risk = false;         // max_lat * (V-1) >= 2^62: an INF used pair on the u64 keys may be a
+                                     // path >= 2^62 ns (SRG_ERR_LATENCY_RANGE), not an unreachable one
 };
 
 Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, hipStream_t st,
@@ -1016,20 +1021,48 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
         }
     }
     hipStream_t aux = c.aux_stream;
+    // SRG_OPT_CHAIN_CUS: the chain (pivot closure + line launches) gets CUs of its own through two
+    // CU-masked streams, so its single-workgroup closure does not queue behind, or share a CU with,
+    // the bulk tiles (beside them it took ~170 us instead of ~70)
+    hipStream_t bulk = st;
+    if (c.chain_cus != 0) {
+        if (c.cu_streams_for != c.chain_cus) {
+            for (hipStream_t* x : {&c.cu_bulk, &c.cu_chain})
+                if (*x) {
+                    HIP_CHECK(hipStreamDestroy(*x));
+                    *x = nullptr;
+                }
+            int ncu = 256;
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+            const int r = std::min(std::abs(c.chain_cus), ncu / 2);
+            std::vector<uint32_t> mb((ncu + 31) / 32, 0u), mc((ncu + 31) / 32, 0u);
+            for (int i = 0; i < ncu; ++i) {
+                const bool chain = c.chain_cus > 0 ? (i % (ncu / r) == 0 && i / (ncu / r) < r) : i < r;
+                (chain ? mc : mb)[i / 32] |= 1u << (i % 32);
+            }
+            HIP_CHECK(hipExtStreamCreateWithCUMask(&c.cu_bulk, (uint32_t)mb.size(), mb.data()));
+            HIP_CHECK(hipExtStreamCreateWithCUMask(&c.cu_chain, (uint32_t)mc.size(), mc.data()));
+            c.cu_streams_for = c.chain_cus;
+        }
+        bulk = c.cu_bulk;
+        aux = c.cu_chain;
+        HIP_CHECK(hipEventRecord(c.ev_b, st));
+        HIP_CHECK(hipStreamWaitEvent(bulk, c.ev_b, 0));
+    }
     // line launches sit on the critical chain: split-K so that ~nb x split workgroups share a tile
     const int lsplit = std::max(1, std::min(c.chain_split, T / KCS));
     auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
         fw_product_sym<T, KCS, FOLD><<<dim3(nb, 1, lsplit), 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
     };
-    fw_phase1<uint32_t, T><<<1, 512, 0, st>>>(D, Vp, 0, c.chain_prio);
-    if (nb > 1) line(0, 0, 0, -1, st);
+    fw_phase1<uint32_t, T><<<1, 512, 0, bulk>>>(D, Vp, 0, c.chain_prio);
+    if (nb > 1) line(0, 0, 0, -1, bulk);
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
         if (k1 >= nb) {
-            if (nb > 1) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
+            if (nb > 1) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
             break;
         }
-        HIP_CHECK(hipEventRecord(c.ev_a, st));
+        HIP_CHECK(hipEventRecord(c.ev_a, bulk));
         HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
         line(k1, kb, kb, -1, aux);  // line k1 (incl. tile (k1, k1)) w.r.t. kb
         fw_phase1<uint32_t, T><<<1, 512, 0, aux>>>(D, Vp, k1, c.chain_prio);
@@ -1037,14 +1070,18 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
         HIP_CHECK(hipEventRecord(c.ev_d, aux));
         const int m = nb - 2;  // lines kb and k1 excluded
         const bool timed = prof && m > 0;
-        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        if (m > 0) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, st>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
+        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], bulk));
+        if (m > 0) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
         if (timed) {
-            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
+            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], bulk));
             prof_relax += (uint64_t)m * (m + 1) / 2 * T * T * T;
             ++prof_n;
         }
-        HIP_CHECK(hipStreamWaitEvent(st, c.ev_d, 0));
+        HIP_CHECK(hipStreamWaitEvent(bulk, c.ev_d, 0));
+    }
+    if (bulk != st) {
+        HIP_CHECK(hipEventRecord(c.ev_b, bulk));
+        HIP_CHECK(hipStreamWaitEvent(st, c.ev_b, 0));
     }
     const unsigned nb64 = (unsigned)(Vp / 64);
     k_sym_mirror<uint32_t><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
@@ -1202,10 +1239,15 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                                                                       P.selflat, P.selfloss, out_lat, out_loss,
                                                                       P.flags, 1);
     HIP_CHECK(hipGetLastError());
-    if (reduce_flag(&P.flags->unreachable_used_pair))
+    if (reduce_flag(&P.flags->unreachable_used_pair)) {
+        if (sizeof(K) == 8 && P.range_risk)
+            fail(SRG_ERR_LATENCY_RANGE, "a used pair has no path below 2^62 ns (max edge latency " +
+                                            std::to_string(P.es.max_lat) +
+                                            " ns): unreachable, or a latency sum the reference's u64 would wrap");
         fail(SRG_ERR_UNREACHABLE,
              "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
              "from another used node)");
+    }
     if (exchange) exchange_rows(out_lat, 8);  // overlaps the scan and the loss pass below
     // host entry, one rank: the latency table is final -- it leaves during the scan / loss pass
     const bool sink_rows = sink && !multi && pl.contiguous && nloc == n && sink->ok();
@@ -1249,7 +1291,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    const bool v5 = sizeof(K) == 4 && (c.scan_variant == 5 || c.scan_variant == 6);  // pair-lane LDS scans
+    const bool v5 = sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 8) || c.scan_variant >= 91);  // pair-lane LDS scans (9x: timing experiments)
     const size_t npad = v5 ? ((size_t)nloc + 127) / 128 * 128 : ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
@@ -1407,7 +1449,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             if constexpr (sizeof(K) == 4) {
                 if (v5) {
                     const uint32_t nbS5 = (uint32_t)(npad / V5_SB);
-                    auto scan5 = c.scan_variant == 6 ? tight_v6 : tight_v5;
+                    auto scan5 = c.scan_variant == 6 ? tight_v6 : c.scan_variant == 7 ? tight_v7<0> : c.scan_variant == 8 ? tight_v7<1>
+                                 : c.scan_variant == 91 ? tight_v7<0, 1> : c.scan_variant == 92 ? tight_v7<0, 2> : tight_v5;
                     // host entry: the scan runs in source-block groups, each group's loss rows folded
                     // right after it and shipped while later groups scan (loss rows on a second
                     // stream beside the next group's scan were starved of CUs: 24.7 ms vs 20.8)
@@ -1719,6 +1762,12 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                                  : (c.sparse_group == 4 ? k_sparse_bf<4, false, true> : k_sparse_bf<SP_G, false, true>))
                         : (gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true, false> : k_sparse_bf<SP_G, true, false>)
                                  : (c.sparse_group == 4 ? k_sparse_bf<4, false, false> : k_sparse_bf<SP_G, false, false>));
+        if (c.sparse_wgs_per_cu == 1 && !c.sparse_split_labels) {  // 128-VGPR budget (no spills)
+            kern = gbits ? (c.sparse_group == 16 ? k_sparse_bf<16, true, false, 4>
+                            : c.sparse_group == 4 ? k_sparse_bf<4, true, false, 4> : k_sparse_bf<SP_G, true, false, 4>)
+                         : (c.sparse_group == 16 ? k_sparse_bf<16, false, false, 4>
+                            : c.sparse_group == 4 ? k_sparse_bf<4, false, false, 4> : k_sparse_bf<SP_G, false, false, 4>);
+        }
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, nodes, n,
                      P.selflat, P.selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb, lm};
@@ -1809,11 +1858,11 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     }
     Prelude P = prelude(c, g, nodes, n, st, true);
     if (n == 0) return;
-    // u64 path requires every path sum < 2^62 (INF); reference would wrap a u64 (mod.rs:327)
+    // u64 keys hold path sums below INF = 2^62 (a sum of two keys never wraps); a graph whose
+    // worst-case path could reach 2^62 still runs, and only a used pair left at INF is an error:
+    // SRG_ERR_LATENCY_RANGE then, since it may be a path the reference would wrap (mod.rs:327)
     const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (g.V > 1 ? g.V - 1 : 1);
-    if (bound >= ((unsigned __int128)1 << 62))
-        fail(SRG_ERR_LATENCY_RANGE, "path latency sum could exceed 2^62 ns (max edge latency " +
-                                        std::to_string(P.es.max_lat) + " ns)");
+    P.range_risk = bound >= ((unsigned __int128)1 << 62);
     const int G = c.comm ? c.comm->nranks : 1, rk = c.comm ? c.comm->rank : 0;
     if (choose_sparse(c, g) && P.es.max_lat < 0xFFFFFFFFull) {
         if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
@@ -2185,11 +2234,11 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (!(value >= 0 && value <= 6 && value == (int)value)) return SRG_ERR_ARG;
+            if (!((value >= 0 && value <= 8) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
-            if (value != 4 && value != 8) return SRG_ERR_ARG;
+            if (value != 4 && value != 8 && value != 16) return SRG_ERR_ARG;  // 16: one workgroup per CU only
             ctx->sparse_group = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_WGS_PER_CU:
@@ -2217,6 +2266,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_CHAIN_CUS:
+            if (value < -128 || value > 128 || value != (int)value) return SRG_ERR_ARG;
+            ctx->chain_cus = (int)value;
             return SRG_OK;
         case SRG_OPT_FW_FOLD:
             if (value != 0 && value != 1) return SRG_ERR_ARG;

@@ -158,8 +158,11 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
 // masked) only in lanes whose candidate latency does not exceed the target's latency at the
 // start of its group -- every other candidate loses the lexicographic min on latency alone.
 // The fold itself is unchanged (u64 keys rebuilt in registers), so the fixpoint is the same.
-template <int G, bool GB, bool SPL>
-__global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_bf(SparseArgs a) {
+// WPE = waves per SIMD the register budget is sized for: 8 (two 1024-thread workgroups per CU,
+// <= 64 VGPRs: the kernel spills ~90 B per lane to scratch) or 4 (one workgroup per CU, <= 128
+// VGPRs, no spills; SRG_OPT_SPARSE_WGS_PER_CU = 1).
+template <int G, bool GB, bool SPL, int WPE = 8>
+__global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
     const uint32_t nw = (V + 63) / 64;  // 64-vertex windows

@@ -1222,6 +1222,168 @@ __global__ void __launch_bounds__(512, 4) tight_v6(const uint32_t* __restrict__ 
     }
 }
 
+// Variant 7: variant 5 with the record stream staged in LDS next to the rows.  v5 reads each
+// 4-pair group with an s_load from the record array (L2 / Infinity Cache latency, one group
+// ahead) and its s_waitcnt also drains the LDS row reads; here chunk k+1's rows AND records (the
+// 8 wave slices of a chunk are one contiguous range) are copied into the other LDS buffers by
+// LDS-DMA (global_load_lds, no staging registers) while chunk k is checked, so the loop issues
+// only LDS reads.  The slice bounds (goff) of chunk k+2 are vector-loaded a chunk ahead; the
+// end-of-chunk barrier drains every DMA.  Slices past V7_RC staged pairs read the rest with
+// uniform vector loads.  V7_PIPE = 1: the next group's records are read behind the current
+// group's rows.
+constexpr uint32_t V7_RC = 448;  // staged pairs per chunk and buffer (7 waves x 64 lanes x 16 B)
+
+template <int PIPE, int DBG = 0>
+__global__ void __launch_bounds__(512, 4) tight_v7(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
+                                                    const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
+                                                    uint32_t* __restrict__ PRED, size_t ldp) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
+    __shared__ __attribute__((aligned(16))) uint4 recs[2 * V7_RC];             // 2 x 7 KB record ring
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r0 = c * V5_SB + 2 * lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t t0 = b * V5_TT + wave * V5_TW;
+    const bool active = t0 < NT;
+    const uint4* rec4 = reinterpret_cast<const uint4*>(rec);
+    v16u_v5 ndl, ndh, stl, sth;
+#pragma unroll
+    for (uint32_t j = 0; j < V5_TW; ++j) {
+        uint32_t dl = 0, dh = 0;
+        if (active) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ((t0 + j) * (uint32_t)npad + r0) * 4u, 0, 0);
+            dl = v[0];
+            dh = v[1];
+        }
+        ndl[j] = 0u - dl;
+        ndh[j] = 0u - dh;
+        stl[j] = PRED_NONE;
+        sth[j] = PRED_NONE;
+    }
+    // lane j < 9 of every wave holds goff[(b*nK + k)*8 + j] of a chunk k
+    auto go_load = [&](uint32_t k) { return goff[((size_t)b * nK + min(k, nK - 1)) * V5_WAVES + min(lane, V5_WAVES)]; };
+    // LDS-DMA of chunk k's rows and records into buffer buf (lane-linear 1-KB pieces per wave)
+    auto stage = [&](uint32_t k, uint32_t buf, uint32_t gk) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {  // rows 2*wave + 16*i, +1: 512 B each
+            const uint32_t u = k * V5_UC + 2 * wave + 16 * i + (lane >> 5);
+            const uint32_t* src = DST + (size_t)min(u, V - 1) * npad + c * V5_SB + (lane & 31) * 4;
+            __builtin_amdgcn_global_load_lds(src, &rows[buf * (V5_UC * V5_SB) + (2 * wave + 16 * i) * V5_SB], 16, 0, 0);
+        }
+        const uint32_t rbase = (uint32_t)__builtin_amdgcn_readlane((int)gk, 0);
+        const uint32_t rend = (uint32_t)__builtin_amdgcn_readlane((int)gk, (int)V5_WAVES);
+        const uint32_t rcnt = min(rend - rbase, V7_RC);
+        if (wave * 64 < rcnt) {  // wave-uniform; lanes past rcnt copy a clamped (unused) record
+            const uint32_t p = rbase + min(wave * 64 + lane, rcnt - 1);
+            __builtin_amdgcn_global_load_lds(&rec4[p], &recs[buf * V7_RC + wave * 64], 16, 0, 0);
+        }
+    };
+    uint32_t gcur = go_load(0);
+    stage(0, 0, gcur);
+    uint32_t gnext = go_load(1);
+    __syncthreads();
+    const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows);
+    for (uint32_t k = 0; k < nK; ++k) {
+        const uint32_t buf = k & 1u;
+        uint32_t gafter = 0;
+        if (k + 1 < nK) {
+            stage(k + 1, buf ^ 1u, gnext);  // the other buffers: their readers (chunk k - 1) passed the last barrier
+            gafter = go_load(k + 2);
+        }
+        if (active && DBG != 1) {  // DBG (timing experiments only, wrong results): 1 = no pair loop
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)gcur, 0);
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)gcur, (int)wave);
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)gcur, (int)wave + 1);
+            const uint32_t vb = buf * (V5_UC * V5_SB * 4u) + lane * 8u;
+            const uint4* rl = recs + buf * V7_RC;
+            auto grp = [&](uint32_t p, uint4* R) {  // the 4 records of pair group p (uniform)
+                const uint32_t li = p - base;
+                if (li + 4 <= V7_RC) {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) R[i] = rl[li + i];
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) R[i] = rec4[p + i];
+                }
+            };
+            auto check = [&](const uint4* R, const uint2* A, uint32_t p) {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane((int)R[i].x) >> 16;
+                    const uint32_t dl = ndl[tl], dh = ndh[tl];
+                    const uint32_t w0 = R[i].y, w1 = R[i].w;
+                    const uint32_t x0l = A[2 * i].x + w0 + dl, x0h = A[2 * i].y + w0 + dh;
+                    const uint32_t x1l = A[2 * i + 1].x + w1 + dl, x1h = A[2 * i + 1].y + w1 + dh;
+                    const uint32_t m = min(min(x0l, x0h), min(x1l, x1h));
+                    if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                        const uint32_t e0 = 2 * (p + i);
+                        uint32_t sl = stl[tl], sh = sth[tl];
+                        if (x0l == 0) sl = (sl == PRED_NONE) ? e0 : PRED_MULTI;
+                        if (x1l == 0) sl = (sl == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                        if (x0h == 0) sh = (sh == PRED_NONE) ? e0 : PRED_MULTI;
+                        if (x1h == 0) sh = (sh == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                        stl[tl] = sl;
+                        sth[tl] = sh;
+                    }
+                }
+            };
+            if (p0 < p1) {
+                uint4 R[4];
+                grp(p0, R);
+                for (uint32_t p = p0; p < p1; p += 4) {
+                    uint2 A[8];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        if constexpr (DBG == 2) {  // 2 = no row reads
+                            A[2 * i] = make_uint2(R[i].x, R[i].z);
+                            A[2 * i + 1] = make_uint2(R[i].z, R[i].x);
+                        } else {
+                            A[2 * i] = *reinterpret_cast<const uint2*>(lds + vb + (R[i].x & 0xFFFFu));
+                            A[2 * i + 1] = *reinterpret_cast<const uint2*>(lds + vb + R[i].z);
+                        }
+                    }
+                    if constexpr (PIPE) {
+                        uint4 Rn[4];
+                        grp(min(p + 4, p1 - 4), Rn);  // the next group's records behind the row reads
+                        check(R, A, p);
+#pragma unroll
+                        for (uint32_t i = 0; i < 4; ++i) R[i] = Rn[i];
+                    } else {
+                        check(R, A, p);
+                        if (p + 4 < p1) grp(p + 4, R);
+                    }
+                }
+            }
+        }
+        gcur = gnext;
+        gnext = gafter;
+        if (k + 1 < nK) __syncthreads();  // drains the DMAs of chunk k + 1 (vmcnt) and orders the buffers
+    }
+    if (!active) return;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t r = r0 + h;
+        if (r >= n) continue;
+        const uint32_t s = nodes[r];
+        uint32_t o[V5_TW];
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; ++j) {
+            const uint32_t t = t0 + j;
+            const uint32_t nd = h ? ndh[j] : ndl[j];
+            const uint32_t st = h ? sth[j] : stl[j];
+            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+        }
+        uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; j += 4) out[j / 4] = make_uint4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,

@@ -110,7 +110,7 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_scan_variants_match_oracle(variant):
     """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs
     (the default), LDS-staged u-chunks (one or two sources per lane)."""
@@ -137,10 +137,12 @@ def test_fw_symmetric_matches_general(V):
     g = synth.atlas_like(V, seed=V + 7)
     nodes = np.random.default_rng(V).permutation(V).tolist()
     out = []
-    for sym, fold in ((0, 1), (1, 1), (1, 0)):  # general FW; symmetric with either fold (SRG_OPT_FW_FOLD)
+    # general FW; symmetric with either fold (SRG_OPT_FW_FOLD) and with the chain on reserved CUs
+    for sym, fold, cus in ((0, 1, 0), (1, 1, 0), (1, 0, 0), (1, 0, 16), (1, 0, -8)):
         r = Router(0)
         r.set_option(N.SRG_OPT_FW_SYMMETRIC, sym)
         r.set_option(N.SRG_OPT_FW_FOLD, fold)
+        r.set_option(N.SRG_OPT_CHAIN_CUS, cus)
         t = r.compute_shortest_paths(g, nodes)
         assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
         out.append(t)
@@ -153,7 +155,7 @@ def test_fw_symmetric_matches_general(V):
         assert_parity(out[1], lat, loss)
 
 
-@pytest.mark.parametrize("variant", [2, 5, 6])
+@pytest.mark.parametrize("variant", [2, 5, 6, 7, 8])
 def test_scan_variants_ragged_sources(variant):
     """Several 128-source blocks, target tiles and u-chunks, with n and V off every block size and
     a used-node subset in random order (lanes past n, targets past V, sentinel pairs)."""
@@ -231,8 +233,9 @@ def test_unused_isolated_vertex_keeps_u32(router):
 
 
 def test_latency_range_is_an_error(router):
-    """Documented divergence: when a path sum could reach 2^62 ns the library
-    returns SRG_ERR_LATENCY_RANGE, where the release build of the reference would wrap u64
+    """Documented divergence: when a used pair has no path below 2^62 ns on a
+    graph whose worst-case path sum reaches 2^62, the library returns SRG_ERR_LATENCY_RANGE, where
+    the release build of the reference would wrap u64
     silently (mod.rs:327 `+` on u64, overflow checks off in src/Cargo.toml:56-61).  The Rust
     binding panics on it, like the `.unwrap()` of an overflowing unit conversion (mod.rs:336)."""
     big = 2 ** 61
@@ -243,6 +246,13 @@ def test_latency_range_is_an_error(router):
     ok = Edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [1, 1, 1, 2 ** 40, 2 ** 40], [0.0] * 5, False)
     t = router.compute_shortest_paths(ok, [0, 1, 2])
     assert t[(0, 2)].latency_ns == 2 ** 41 and t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+    # worst case max_lat * (V-1) >= 2^62, but no used shortest path comes near it (a "disabled"
+    # 2^61-ns link beside a 2-hop route): the reference's Dijkstra succeeds, and so does this
+    dis = Edges(3, [0, 1, 2, 0, 1, 0], [0, 1, 2, 1, 2, 2], [1, 1, 1, 1, 1, big], [0.0] * 6, False)
+    t = router.compute_shortest_paths(dis, [0, 1, 2])
+    assert t[(0, 2)].latency_ns == 2 and t[(2, 0)].latency_ns == 2
+    lat, loss = oracle.compute_shortest_paths(dis.as_tuple(), [0, 1, 2])
+    assert_parity(t, lat, loss)
 
 
 def test_deterministic_bytes(router):

@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+out=gpurun_out/${1:-cus}
+mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "symmetric" --timeout 200 --timeout-method thread > $out/t.log 2>&1 || { tail -30 $out/t.log; exit 1; }
+tail -1 $out/t.log
+run() { timeout -k 10 200 python -u bench.py --no-cpu --entry device --steps 5 "$@" > $out/b.json 2>$out/b.err || { tail -20 $out/b.err; exit 1; }
+  python -c "import json,sys;d=json.load(open('$out/b.json'));r=d['roofline'];print(sys.argv[1:], d['ms_per_step'], 'fw', d['breakdown_ms']['ms_fw'], 'bulk', r['avg_launch_ms'], 'frac', r['frac'])" "$@"; }
+for c in 0 8 16 32 -8 -16 -32 0; do run --chain-cus $c; done

@@ -1,7 +1,7 @@
 """Per-launch PMC averages of the sparse kernel k_sparse_bf from a tools/pmc_sparse.sh output
 directory -> profiles/sparse_pmc_latest.json (read by bench.py --graph ba).
 
-usage: python tools/pmc_extract_sparse.py PMC_DIR SOURCE_TEXT
+usage: python tools/pmc_extract_sparse.py PMC_DIR SOURCE_TEXT [WORKLOAD_KEY]
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB and on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads, so hbm = 2*FETCH + WRITE (an upper
 estimate for the sparse kernel, whose label reads are 512-byte wave rows but whose CSR reads are
@@ -19,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     d, source = sys.argv[1], sys.argv[2]
+    wkey = sys.argv[3] if len(sys.argv) > 3 else None
     acc = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -27,7 +28,7 @@ def main():
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {c: sum(v) / len(v) for c, v in acc.items()}
     fetch, write = avg.get("FETCH_SIZE", 0.0), avg.get("WRITE_SIZE", 0.0)
-    out = {"source": source, "kernel": "srg::k_sparse_bf(srg::SparseArgs)",
+    out = {"source": source, "workload_key": wkey, "kernel": "srg::k_sparse_bf(srg::SparseArgs)",
            "launches_averaged": len(acc.get("FETCH_SIZE", [])),
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
