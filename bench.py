@@ -256,6 +256,7 @@ def main():
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--d2h-mode", type=int, default=None,
                     help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync, N >= 2 = copy kernel of N workgroups")
+    ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")
     ap.add_argument("--chain-cus", type=int, default=None, help="symmetric FW: CUs reserved for the chain (0 = none)")
     ap.add_argument("--fw-fold", type=int, default=None, help="symmetric FW: 1 = add,add,min3; 0 = lshl_add_u64,min3")
     ap.add_argument("--scan-groups", type=int, default=None, help="host entry: scan launches interleaved with the loss (0 = auto)")
@@ -353,6 +354,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
+    if args.h2d_codec is not None:
+        router.set_option(N.SRG_OPT_H2D_CODEC, args.h2d_codec)
     if args.chain_cus is not None:
         router.set_option(N.SRG_OPT_CHAIN_CUS, args.chain_cus)
     if args.fw_fold is not None:

@@ -166,6 +166,9 @@ void srg_destroy(srg_ctx* ctx);
                                      * v_lshl_add_u64 + v_min3_u32, 1 = two v_add_u32 + v_min3_u32 (slower) */
 #define SRG_OPT_CHAIN_CUS 24         /* symmetric u32 FW: CUs reserved for the lookahead chain through CU-masked
                                      * streams (n evenly spaced CU ids; -n = the lowest n ids); 0 = none */
+#define SRG_OPT_H2D_CODEC 25         /* host entry: 1 (default) = the edge list crosses PCIe narrowed (u16
+                                     * endpoints, u32 latencies; 12 instead of 20 B per edge) when every
+                                     * endpoint < 65536 and latency < 2^32, widened on the device; 0 = plain */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

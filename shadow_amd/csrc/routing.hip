@@ -16,6 +16,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -415,6 +416,58 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 }  // namespace
 
+// Host-side worker pool for the host entry's H2D codec: run(f) calls f(w, nw) on nw threads
+// (the caller is worker 0) and returns when all are done.
+struct HostPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::function<void(int, int)> job;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool stop = false;
+    int size() const { return (int)th.size() + 1; }
+    void start(int n) {
+        for (int w = 1; w < n; ++w)
+            th.emplace_back([this, w] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int, int)> f;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        f = job;
+                    }
+                    f(w, size());
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--pending == 0) done_cv.notify_one();
+                }
+            });
+    }
+    void run(const std::function<void(int, int)>& f) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = f;
+            pending = (int)th.size();
+            ++gen;
+        }
+        cv.notify_all();
+        f(0, size());
+        std::unique_lock<std::mutex> lk(mu);
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
 // The HSA agents of a HIP device (matched by PCI domain / bus / device), for SDMA copies.
 struct SdmaAgents {
     bool ok = false;
@@ -484,6 +537,12 @@ struct srg_ctx {
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
     int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync, >= 2 = copy kernel of that many workgroups (SRG_OPT_D2H_MODE)
     SdmaAgents sdma;
+    int h2d_codec = 1;               // host entry: narrowed edge list over PCIe (SRG_OPT_H2D_CODEC)
+    HostPool* pool = nullptr;        // its host workers
+    void* h_ring = nullptr;          // its page-locked staging ring (hipHostMalloc)
+    size_t h_ring_bytes = 0;
+    hipEvent_t ev_ring[3] = {nullptr, nullptr, nullptr};
+    DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
     int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
     int cu_streams_for = 0;          // chain_cus the two CU-masked streams below were made for
     hipStream_t cu_bulk = nullptr, cu_chain = nullptr;
@@ -523,6 +582,11 @@ struct srg_ctx {
             if (e) (void)hipEventDestroy(e);
         for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream, cu_bulk, cu_chain})
             if (s) (void)hipStreamDestroy(s);
+        delete pool;
+        for (hipEvent_t e : ev_ring)
+            if (e) (void)hipEventDestroy(e);
+        if (h_ring) (void)hipHostFree(h_ring);
+        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l}) b->release();
     }
 };
 
@@ -2014,11 +2078,110 @@ void order_events_device(srg_ctx& c, const EvIn& in, uint64_t* deliver, uint32_t
     }
 }
 
+__global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const uint16_t* __restrict__ d16,
+                              const uint32_t* __restrict__ l32, uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                              uint64_t* __restrict__ lat) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        src[i] = s16[i];
+        dst[i] = d16[i];
+        lat[i] = l32[i];
+    }
+}
+
+// H2D codec of the host entry (SRG_OPT_H2D_CODEC): the edge list crosses PCIe narrowed -- u16
+// endpoints (V <= 65536) and u32 latencies -- 12 B instead of 20 B per edge, then is widened on
+// the device.  Host threads narrow chunk i+1 into a page-locked ring while chunk i is in flight.
+// Returns false (nothing usable staged) when an endpoint >= 65536 or a latency >= 2^32 is seen:
+// the caller then ships the plain arrays, whose checks report such edges as the reference does.
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st);
+
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
     T* d = (T*)b.get(std::max<size_t>(count, 1) * sizeof(T));
     if (count) HIP_CHECK(hipMemcpyAsync(d, host, count * sizeof(T), hipMemcpyHostToDevice, st));
     return d;
+}
+
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st) {
+    const size_t E = g->num_edges;
+    constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
+    constexpr int NB = 3;                   // ring slots
+    const size_t slot = CE * 16;
+    if (!c.pool) {
+        c.pool = new HostPool();
+        const unsigned hw = std::thread::hardware_concurrency();
+        int nt = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+        if (const char* e = std::getenv("SRG_CODEC_THREADS")) nt = std::max(1, std::atoi(e));  // experiments
+        c.pool->start(nt);
+    }
+    if (c.h_ring_bytes < slot * NB) {
+        if (c.h_ring) HIP_CHECK(hipHostFree(c.h_ring));
+        c.h_ring = nullptr;
+        c.h_ring_bytes = 0;
+        HIP_CHECK(hipHostMalloc(&c.h_ring, slot * NB, hipHostMallocDefault));
+        c.h_ring_bytes = slot * NB;
+    }
+    for (hipEvent_t& e : c.ev_ring)
+        if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    uint16_t* s16 = (uint16_t*)c.b_n16s.get(E * 2);
+    uint16_t* d16 = (uint16_t*)c.b_n16d.get(E * 2);
+    uint32_t* l32 = (uint32_t*)c.b_n32l.get(E * 4);
+    dg.src = (uint32_t*)c.b_src.get(E * 4);
+    dg.dst = (uint32_t*)c.b_dst.get(E * 4);
+    dg.lat = (uint64_t*)c.b_lat.get(E * 8);
+    dg.loss = (float*)c.b_loss.get(E * 4);
+    std::atomic<bool> bad{false};
+    const bool dbg = std::getenv("SRG_DEBUG_CODEC") != nullptr;
+    double t_conv = 0, t_wait = 0;
+    const size_t nch = (E + CE - 1) / CE;
+    for (size_t ch = 0; ch < nch; ++ch) {
+        const int b = (int)(ch % NB);
+        auto tw = std::chrono::steady_clock::now();
+        if (ch >= (size_t)NB) HIP_CHECK(hipEventSynchronize(c.ev_ring[b]));  // the slot's previous DMA is done
+        const size_t e0 = ch * CE, ne = std::min(CE, E - e0);
+        unsigned char* base = (unsigned char*)c.h_ring + (size_t)b * slot;
+        uint16_t* hs = (uint16_t*)base;
+        uint16_t* hd = hs + CE;
+        uint32_t* hl = (uint32_t*)(hd + CE);
+        float* hb = (float*)(hl + CE);
+        auto tc = std::chrono::steady_clock::now();
+        t_wait += std::chrono::duration<double, std::milli>(tc - tw).count();
+        c.pool->run([&](int w, int nw) {
+            const size_t a = ne * w / nw, z = ne * (w + 1) / nw;
+            const uint32_t* src = g->src + e0;
+            const uint32_t* dst = g->dst + e0;
+            const uint64_t* lat = g->latency_ns + e0;
+            uint32_t orx = 0;
+            uint64_t orl = 0;
+            for (size_t i = a; i < z; ++i) {
+                const uint32_t x = src[i], y = dst[i];
+                const uint64_t l = lat[i];
+                orx |= x | y;
+                orl |= l;
+                hs[i] = (uint16_t)x;
+                hd[i] = (uint16_t)y;
+                hl[i] = (uint32_t)l;
+            }
+            std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
+            if ((orx >> 16) || (orl >> 32)) bad.store(true, std::memory_order_relaxed);
+        });
+        t_conv += ms_since(tc);
+        if (bad.load()) {
+            HIP_CHECK(hipStreamSynchronize(st));  // no DMA may still read the ring
+            return false;
+        }
+        HIP_CHECK(hipMemcpyAsync(s16 + e0, hs, ne * 2, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d16 + e0, hd, ne * 2, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, hb, ne * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipEventRecord(c.ev_ring[b], st));
+        k_widen_edges<<<grid_for(ne), kThreads, 0, st>>>(ne, s16 + e0, d16 + e0, l32 + e0, (uint32_t*)dg.src + e0,
+                                                          (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (dbg) std::fprintf(stderr, "codec: %zu chunks, %d threads, convert %.2f ms, slot waits %.2f ms\n", nch,
+                          c.pool->size(), t_conv, t_wait);
+    return true;
 }
 
 int guard(char* errbuf, size_t errlen, const std::function<void()>& body) {
@@ -2104,10 +2267,14 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         const size_t E = g->num_edges, n = num_nodes;
         DevGraph dg{g->num_vertices, (int)g->directed, g->num_edges, nullptr, nullptr, nullptr, nullptr,
                     nullptr, g->node_ids};
-        dg.src = stage_in(c->b_src, g->src, E, st);
-        dg.dst = stage_in(c->b_dst, g->dst, E, st);
-        dg.lat = stage_in(c->b_lat, g->latency_ns, E, st);
-        dg.loss = stage_in(c->b_loss, g->packet_loss, E, st);
+        // narrowed edge list over PCIe when it fits (falls back to the plain arrays otherwise)
+        const bool coded = c->h2d_codec && E >= ((size_t)1 << 20) && g->num_vertices <= 65536 && codec_in(*c, g, dg, st);
+        if (!coded) {
+            dg.src = stage_in(c->b_src, g->src, E, st);
+            dg.dst = stage_in(c->b_dst, g->dst, E, st);
+            dg.lat = stage_in(c->b_lat, g->latency_ns, E, st);
+            dg.loss = stage_in(c->b_loss, g->packet_loss, E, st);
+        }
         const uint32_t* dn = stage_in(c->b_nodes, nodes, n, st);
         uint64_t* dol = (uint64_t*)c->b_olat.get(std::max<size_t>(nn, 1) * 8);
         float* dos = (float*)c->b_oloss.get(std::max<size_t>(nn, 1) * 4);
@@ -2266,6 +2433,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_H2D_CODEC:
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            ctx->h2d_codec = (int)value;
             return SRG_OK;
         case SRG_OPT_CHAIN_CUS:
             if (value < -128 || value > 128 || value != (int)value) return SRG_ERR_ARG;

@@ -371,6 +371,34 @@ def test_host_entry_early_rows_match_device(router, mode, groups):
     assert bits_equal(os_.cpu().numpy(), t.packet_loss)
 
 
+def test_h2d_codec_matches_plain(router):
+    """Host entry H2D codec (SRG_OPT_H2D_CODEC: u16 endpoints + u32 latencies over PCIe, widened on
+    the device) gives the same bytes as the plain transfer; a latency >= 2^32 makes it fall back
+    to the plain arrays (same result again), and oracle rows pin both."""
+    V = 1500  # 1.12 M edges: past the codec's 2^20-edge threshold
+    g = synth.atlas_like(V, seed=31)
+    nodes = list(range(V))
+    out = {}
+    for codec in (1, 0):
+        router.set_option(N.SRG_OPT_H2D_CODEC, codec)
+        out[codec] = router.compute_shortest_paths(g, nodes)
+    router.set_option(N.SRG_OPT_H2D_CODEC, 1)
+    assert np.array_equal(out[0].latency_ns, out[1].latency_ns)
+    assert bits_equal(out[0].packet_loss, out[1].packet_loss)
+    rows = [0, 7, 1499]
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
+    assert np.array_equal(out[1].latency_ns[rows], lat) and bits_equal(out[1].packet_loss[rows], loss)
+    # one edge of 2^33 ns (never on a shortest path): the codec cannot narrow it
+    big = Edges(V, g.src, g.dst, g.latency_ns.copy(), g.packet_loss, directed=False)
+    k = int(np.nonzero(big.src != big.dst)[0][5])
+    big.latency_ns[k] = 2 ** 33
+    t = router.compute_shortest_paths(big, nodes)
+    router.set_option(N.SRG_OPT_H2D_CODEC, 0)
+    t0 = router.compute_shortest_paths(big, nodes)
+    router.set_option(N.SRG_OPT_H2D_CODEC, 1)
+    assert np.array_equal(t.latency_ns, t0.latency_ns) and bits_equal(t.packet_loss, t0.packet_loss)
+
+
 @pytest.mark.slow
 def test_c1_full_vs_oracle(router):
     """Config C1 (1000-vertex complete graph), every pair."""
