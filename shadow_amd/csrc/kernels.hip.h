@@ -110,21 +110,24 @@ __device__ __forceinline__ void st16(K* p, const Vec16<K>& v) { stv<K, 16 / size
 //   c = min(c, C_0 + R_0, ..., C_{R-1} + R_{R-1})   (C_i, R_i = step-i values; v_min3 pairs)
 // which equals R sequential FW steps.  The owners then publish the next group's rows and
 // columns into the other half of a double-buffered LDS strip.
-template <class K, int T>
+template <class K, int T, int NTH = 512>
 struct P1Geo {
-    static constexpr int MR = T / 32, MC = T / 16;
+    static constexpr int MR = T / (NTH / 16), MC = T / 16;
     static constexpr int HR = MR / 2, HC = MC / 2;
     __device__ __forceinline__ static int row(int ty, int a) { return a < HR ? ty * HR + a : T / 2 + ty * HR + (a - HR); }
     __device__ __forceinline__ static int col(int tx, int b) { return b < HC ? tx * HC + b : T / 2 + tx * HC + (b - HC); }
 };
 
-template <class K, int T>
-__global__ void __launch_bounds__(512) fw_phase1(K* __restrict__ D, size_t ld, int kb, int prio) {
+// NTH = 1024 (SRG_OPT_P1_THREADS): twice the waves, half the elements per thread -- a larger share
+// of the issue slots of the CU it shares with the bulk tiles of the symmetric FW.
+template <class K, int T, int NTH = 512>
+__global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, int kb, int prio) {
     // prio: the chain runs beside the bulk tiles; a raised wave priority wins the VALU issue
     // arbitration on the SIMDs it shares with them (MI355X_MICROARCH.md, waves per SIMD)
     if (prio) __builtin_amdgcn_s_setprio(3);
-    using G = P1Geo<K, T>;
+    using G = P1Geo<K, T, NTH>;
     constexpr int MR = G::MR, MC = G::MC, HR = G::HR, HC = G::HC;
+    static_assert(HR >= 1, "phase-1 geometry");
     constexpr int R = 4;
     __shared__ __attribute__((aligned(16))) K prow[2][R][T];  // prow[.][j][col] = D[k0+j][col]
     __shared__ __attribute__((aligned(16))) K pcol[2][R][T];  // pcol[.][j][row] = D[row][k0+j]

@@ -546,6 +546,7 @@ struct srg_ctx {
     int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
     int cu_streams_for = 0;          // chain_cus the two CU-masked streams below were made for
     hipStream_t cu_bulk = nullptr, cu_chain = nullptr;
+    int p1_threads = 512;            // symmetric FW pivot closure workgroup size, 512 / 1024 (SRG_OPT_P1_THREADS)
     int fw_fold = 0;                 // symmetric FW: 0 = v_lshl_add_u64 + v_min3 per k-pair, 1 = two v_add_u32 + v_min3 (SRG_OPT_FW_FOLD; 1 measured 0.304 vs 0.242 ms per bulk launch)
     int scan_groups = 0;             // host entry: v5 scan launches interleaved with the loss rows (0 = auto: 3) (SRG_OPT_SCAN_GROUPS)
     int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
@@ -1118,7 +1119,11 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
     auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
         fw_product_sym<T, KCS, FOLD><<<dim3(nb, 1, lsplit), 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
     };
-    fw_phase1<uint32_t, T><<<1, 512, 0, bulk>>>(D, Vp, 0, c.chain_prio);
+    auto phase1 = [&](int k, hipStream_t s) {
+        if (c.p1_threads == 1024) fw_phase1<uint32_t, T, 1024><<<1, 1024, 0, s>>>(D, Vp, k, c.chain_prio);
+        else fw_phase1<uint32_t, T><<<1, 512, 0, s>>>(D, Vp, k, c.chain_prio);
+    };
+    phase1(0, bulk);
     if (nb > 1) line(0, 0, 0, -1, bulk);
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
@@ -1129,7 +1134,7 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
         HIP_CHECK(hipEventRecord(c.ev_a, bulk));
         HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
         line(k1, kb, kb, -1, aux);  // line k1 (incl. tile (k1, k1)) w.r.t. kb
-        fw_phase1<uint32_t, T><<<1, 512, 0, aux>>>(D, Vp, k1, c.chain_prio);
+        phase1(k1, aux);
         line(k1, k1, k1, -1, aux);  // line k1 w.r.t. its own closed pivot
         HIP_CHECK(hipEventRecord(c.ev_d, aux));
         const int m = nb - 2;  // lines kb and k1 excluded
@@ -1355,7 +1360,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    const bool v5 = sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 8) || c.scan_variant >= 91);  // pair-lane LDS scans (9x: timing experiments)
+    const bool v5 = sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 9) || c.scan_variant >= 91);  // pair-lane LDS scans (9x: timing experiments)
     const size_t npad = v5 ? ((size_t)nloc + 127) / 128 * 128 : ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
@@ -1525,9 +1530,14 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                         auto cut = [&](uint32_t q) { return q == ng ? nbS5 : std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8); };
                         const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                         if (c1 == c0) continue;
-                        scan5<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
-                            (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
-                            v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp);
+                        if (c.scan_variant == 9)
+                            tight_v9<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                                (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
+                                v5_goff, (const uint32_t*)c.b_entkey.get(0), v5_cnt, PRED, Vp);
+                        else
+                            scan5<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                                (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
+                                v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp);
                         HIP_CHECK(hipGetLastError());
                         if (interleave) {
                             const uint32_t r0 = c0 * V5_SB, r1 = std::min<uint32_t>(c1 * V5_SB, nloc);
@@ -2401,7 +2411,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (!((value >= 0 && value <= 8) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
+            if (!((value >= 0 && value <= 9) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
@@ -2433,6 +2443,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_P1_THREADS:
+            if (value != 512 && value != 1024) return SRG_ERR_ARG;
+            ctx->p1_threads = (int)value;
             return SRG_OK;
         case SRG_OPT_H2D_CODEC:
             if (value != 0 && value != 1) return SRG_ERR_ARG;

@@ -1384,6 +1384,150 @@ __global__ void __launch_bounds__(512, 4) tight_v7(const uint32_t* __restrict__ 
     }
 }
 
+// Variant 9: variant 7's LDS staging with the per-pair scalar chain removed.  The timing
+// decomposition of v7 put 9.6 of its 18.6 ms stage in the pair loop's own instruction chain, and
+// v5's PMC counted 11.5 SALU instructions per pair (register indexing of the pair's target with
+// s_set_gpr_idx, record copies, per-pair branches) against one scalar unit per CU.  Here the 16
+// targets of a wave are a statically unrolled loop (their -d and state registers are plain
+// operands), each target's pairs (its run of the slice, count from k_v5_count) a short dynamic
+// loop two pairs at a time (both pairs' records and rows read before either is checked), and
+// the hit test is one ballot per two pairs.
+__global__ void __launch_bounds__(512, 4) tight_v9(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
+                                                    const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
+                                                    const uint32_t* __restrict__ ecnt, uint32_t* __restrict__ PRED,
+                                                    size_t ldp) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
+    __shared__ __attribute__((aligned(16))) uint4 recs[2 * V7_RC];             // 2 x 7 KB record ring
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r0 = c * V5_SB + 2 * lane;
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t t0 = b * V5_TT + wave * V5_TW;
+    const bool active = t0 < NT;
+    const uint4* rec4 = reinterpret_cast<const uint4*>(rec);
+    uint32_t ndl[V5_TW], ndh[V5_TW], stl[V5_TW], sth[V5_TW];
+#pragma unroll
+    for (uint32_t j = 0; j < V5_TW; ++j) {
+        uint32_t dl = 0, dh = 0;
+        if (active) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ((t0 + j) * (uint32_t)npad + r0) * 4u, 0, 0);
+            dl = v[0];
+            dh = v[1];
+        }
+        ndl[j] = 0u - dl;
+        ndh[j] = 0u - dh;
+        stl[j] = PRED_NONE;
+        sth[j] = PRED_NONE;
+    }
+    auto go_load = [&](uint32_t k) { return goff[((size_t)b * nK + min(k, nK - 1)) * V5_WAVES + min(lane, V5_WAVES)]; };
+    // lane j < 16: entries of target t0 + j in chunk k
+    auto cnt_load = [&](uint32_t k) {
+        return ecnt[((size_t)b * nK + min(k, nK - 1)) * V5_TT + wave * V5_TW + (lane & (V5_TW - 1))];
+    };
+    auto stage = [&](uint32_t k, uint32_t buf, uint32_t gk) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t u = k * V5_UC + 2 * wave + 16 * i + (lane >> 5);
+            const uint32_t* src = DST + (size_t)min(u, V - 1) * npad + c * V5_SB + (lane & 31) * 4;
+            __builtin_amdgcn_global_load_lds(src, &rows[buf * (V5_UC * V5_SB) + (2 * wave + 16 * i) * V5_SB], 16, 0, 0);
+        }
+        const uint32_t rbase = (uint32_t)__builtin_amdgcn_readlane((int)gk, 0);
+        const uint32_t rend = (uint32_t)__builtin_amdgcn_readlane((int)gk, (int)V5_WAVES);
+        const uint32_t rcnt = min(rend - rbase, V7_RC);
+        if (wave * 64 < rcnt) {
+            const uint32_t p = rbase + min(wave * 64 + lane, rcnt - 1);
+            __builtin_amdgcn_global_load_lds(&rec4[p], &recs[buf * V7_RC + wave * 64], 16, 0, 0);
+        }
+    };
+    uint32_t gcur = go_load(0), ccur = cnt_load(0);
+    stage(0, 0, gcur);
+    uint32_t gnext = go_load(1), cnext = cnt_load(1);
+    __syncthreads();
+    const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows);
+    for (uint32_t k = 0; k < nK; ++k) {
+        const uint32_t buf = k & 1u;
+        uint32_t gafter = 0, cafter = 0;
+        if (k + 1 < nK) {
+            stage(k + 1, buf ^ 1u, gnext);
+            gafter = go_load(k + 2);
+            cafter = cnt_load(k + 2);
+        }
+        if (active) {
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)gcur, 0);
+            uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)gcur, (int)wave);
+            const uint32_t vb = buf * (V5_UC * V5_SB * 4u) + lane * 8u;
+            const uint4* rl = recs + buf * V7_RC;
+            auto rd = [&](uint32_t q) -> uint4 {  // record of pair q (uniform)
+                const uint32_t li = q - base;
+                return li < V7_RC ? rl[li] : rec4[q];
+            };
+#pragma unroll
+            for (uint32_t j = 0; j < V5_TW; ++j) {
+                const uint32_t np = ((uint32_t)__builtin_amdgcn_readlane((int)ccur, (int)j) + 1u) >> 1;
+                const uint32_t pend = p + np;
+                const uint32_t dl = ndl[j], dh = ndh[j];
+                for (; p < pend; p += 2) {
+                    const bool two = p + 1 < pend;
+                    const uint4 R0 = rd(p), R1 = rd(two ? p + 1 : p);
+                    const uint2 a00 = *reinterpret_cast<const uint2*>(lds + vb + (R0.x & 0xFFFFu));
+                    const uint2 a01 = *reinterpret_cast<const uint2*>(lds + vb + R0.z);
+                    const uint2 a10 = *reinterpret_cast<const uint2*>(lds + vb + (R1.x & 0xFFFFu));
+                    const uint2 a11 = *reinterpret_cast<const uint2*>(lds + vb + R1.z);
+                    const uint32_t y0l = a00.x + R0.y + dl, y0h = a00.y + R0.y + dh;
+                    const uint32_t y1l = a01.x + R0.w + dl, y1h = a01.y + R0.w + dh;
+                    uint32_t z0l = a10.x + R1.y + dl, z0h = a10.y + R1.y + dh;
+                    uint32_t z1l = a11.x + R1.w + dl, z1h = a11.y + R1.w + dh;
+                    if (!two) z0l = z0h = z1l = z1h = 1u;  // the second pair is the first again: no hit
+                    const uint32_t m = min(min(min(y0l, y0h), min(y1l, y1h)), min(min(z0l, z0h), min(z1l, z1h)));
+                    if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                        const uint32_t e0 = 2 * p, e1 = e0 + 2;
+                        uint32_t sl = stl[j], sh = sth[j];
+                        if (y0l == 0) sl = (sl == PRED_NONE) ? e0 : PRED_MULTI;
+                        if (y1l == 0) sl = (sl == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                        if (z0l == 0) sl = (sl == PRED_NONE) ? e1 : PRED_MULTI;
+                        if (z1l == 0) sl = (sl == PRED_NONE) ? e1 + 1 : PRED_MULTI;
+                        if (y0h == 0) sh = (sh == PRED_NONE) ? e0 : PRED_MULTI;
+                        if (y1h == 0) sh = (sh == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                        if (z0h == 0) sh = (sh == PRED_NONE) ? e1 : PRED_MULTI;
+                        if (z1h == 0) sh = (sh == PRED_NONE) ? e1 + 1 : PRED_MULTI;
+                        stl[j] = sl;
+                        sth[j] = sh;
+                    }
+                }
+                p = pend;
+            }
+        }
+        gcur = gnext;
+        gnext = gafter;
+        ccur = cnext;
+        cnext = cafter;
+        if (k + 1 < nK) __syncthreads();  // drains the DMAs of chunk k + 1 (vmcnt) and orders the buffers
+    }
+    if (!active) return;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t r = r0 + h;
+        if (r >= n) continue;
+        const uint32_t s = nodes[r];
+        uint32_t o[V5_TW];
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; ++j) {
+            const uint32_t t = t0 + j;
+            const uint32_t nd = h ? ndh[j] : ndl[j];
+            const uint32_t st = h ? sth[j] : stl[j];
+            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+        }
+        uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; j += 4) out[j / 4] = make_uint4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,

@@ -110,7 +110,7 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_scan_variants_match_oracle(variant):
     """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs
     (the default), LDS-staged u-chunks (one or two sources per lane)."""
@@ -138,11 +138,13 @@ def test_fw_symmetric_matches_general(V):
     nodes = np.random.default_rng(V).permutation(V).tolist()
     out = []
     # general FW; symmetric with either fold (SRG_OPT_FW_FOLD) and with the chain on reserved CUs
-    for sym, fold, cus in ((0, 1, 0), (1, 1, 0), (1, 0, 0), (1, 0, 16), (1, 0, -8)):
+    for sym, fold, cus, p1t in ((0, 1, 0, 512), (1, 1, 0, 512), (1, 0, 0, 512), (1, 0, 16, 512), (1, 0, -8, 512),
+                                (1, 0, 0, 1024)):
         r = Router(0)
         r.set_option(N.SRG_OPT_FW_SYMMETRIC, sym)
         r.set_option(N.SRG_OPT_FW_FOLD, fold)
         r.set_option(N.SRG_OPT_CHAIN_CUS, cus)
+        r.set_option(N.SRG_OPT_P1_THREADS, p1t)
         t = r.compute_shortest_paths(g, nodes)
         assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
         out.append(t)
@@ -155,7 +157,7 @@ def test_fw_symmetric_matches_general(V):
         assert_parity(out[1], lat, loss)
 
 
-@pytest.mark.parametrize("variant", [2, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [2, 5, 6, 7, 8, 9])
 def test_scan_variants_ragged_sources(variant):
     """Several 128-source blocks, target tiles and u-chunks, with n and V off every block size and
     a used-node subset in random order (lanes past n, targets past V, sentinel pairs)."""
@@ -177,7 +179,7 @@ def test_scan_v5_equals_v2_full_c3():
     g = synth.atlas_like(10000, seed=10000)
     nodes = np.arange(10000, dtype=np.uint32)
     out = []
-    for v in (2, 5, 6):
+    for v in (2, 5, 6, 9):
         r = Router(0)
         r.set_option(N.SRG_OPT_SCAN_VARIANT, v)
         t = r.compute_shortest_paths(g, nodes)

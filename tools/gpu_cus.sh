@@ -7,4 +7,4 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "
 tail -1 $out/t.log
 run() { timeout -k 10 200 python -u bench.py --no-cpu --entry device --steps 5 "$@" > $out/b.json 2>$out/b.err || { tail -20 $out/b.err; exit 1; }
   python -c "import json,sys;d=json.load(open('$out/b.json'));r=d['roofline'];print(sys.argv[1:], d['ms_per_step'], 'fw', d['breakdown_ms']['ms_fw'], 'bulk', r['avg_launch_ms'], 'frac', r['frac'])" "$@"; }
-for c in 0 8 16 32 -8 -16 -32 0; do run --chain-cus $c; done
+for t in 512 1024 512 1024; do run --p1-threads $t; done
