@@ -26,6 +26,7 @@ int main(int argc, char** argv) {
     const int nb = atoi(argv[4]);
     const int stride = argc > 5 ? atoi(argv[5]) : 1;
     const int per_lane = argc > 6 ? atoi(argv[6]) : 0;
+    const int gs_act = argc > 7 ? atoi(argv[7]) : 0;  // 1: arcs from vertices changed earlier in this sweep are pulled too
     const uint32_t INF = 0xFFFFFFFFu;
     std::vector<uint32_t> L((size_t)V * 64);
     std::vector<uint8_t> fprev(V), fcur(V), mark(V), mnext(V), pend(V);
@@ -106,7 +107,7 @@ int main(int argc, char** argv) {
                 pulls++;  // own row
                 for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
                     uint32_t u = src[k];
-                    if (!fprev[u]) continue;
+                    if (!fprev[u] && !(gs_act && fcur[u])) continue;
                     pulls++;
                     const uint32_t* lu = &L[(size_t)u * 64];
                     for (int l = 0; l < 64; ++l)
