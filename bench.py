@@ -256,6 +256,7 @@ def main():
     ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
     ap.add_argument("--d2h-mode", type=int, default=None,
                     help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync, N >= 2 = copy kernel of N workgroups")
+    ap.add_argument("--sparse-relabel", type=int, default=None, help="sparse: 1 = degree-dealt vertex ids (default), 0 = given ids")
     ap.add_argument("--p1-threads", type=int, default=None, help="symmetric FW pivot closure threads (512/1024)")
     ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")
     ap.add_argument("--chain-cus", type=int, default=None, help="symmetric FW: CUs reserved for the chain (0 = none)")
@@ -355,6 +356,8 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
+    if args.sparse_relabel is not None:
+        router.set_option(N.SRG_OPT_SPARSE_RELABEL, args.sparse_relabel)
     if args.p1_threads is not None:
         router.set_option(N.SRG_OPT_P1_THREADS, args.p1_threads)
     if args.h2d_codec is not None:
@@ -437,7 +440,8 @@ def main():
             + (f":sl{args.sparse_split_labels}" if args.sparse_split_labels else "")
             + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
             + (f":fold{args.fw_fold}" if args.fw_fold else "") + (f":cus{args.chain_cus}" if args.chain_cus else "")
-            + (f":p1t{args.p1_threads}" if args.p1_threads and args.p1_threads != 512 else ""))
+            + (f":p1t{args.p1_threads}" if args.p1_threads and args.p1_threads != 512 else "")
+            + (":norelabel" if args.sparse_relabel == 0 else ""))
     roofline = None
     if agg.get("prof_launches") and kind == 3:
         # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row

@@ -170,6 +170,9 @@ void srg_destroy(srg_ctx* ctx);
                                      * endpoints, u32 latencies; 12 instead of 20 B per edge) when every
                                      * endpoint < 65536 and latency < 2^32, widened on the device; 0 = plain */
 #define SRG_OPT_P1_THREADS 26        /* symmetric u32 FW: threads of the pivot-closure workgroup, 512 (default) / 1024 */
+#define SRG_OPT_SPARSE_RELABEL 27    /* sparse: 1 = vertices dealt over the 64-vertex windows in descending
+                                     * in-degree order (balances the waves' sweep work; measured no gain on
+                                     * C4); 0 (default) = given ids */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -54,6 +54,7 @@ SRG_OPT_FW_FOLD = 23
 SRG_OPT_CHAIN_CUS = 24
 SRG_OPT_H2D_CODEC = 25
 SRG_OPT_P1_THREADS = 26
+SRG_OPT_SPARSE_RELABEL = 27
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

@@ -34,6 +34,28 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[5]], ids=lambda k: f"V{k['V']}_s{k['seed']}")
+def test_bf_relabel_vs_oracle(bf_router, kw):
+    """The sparse path with degree-dealt vertex ids (SRG_OPT_SPARSE_RELABEL 1) against the oracle
+    (every other sparse test runs the default given ids)."""
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
+    g = synth.random_graph(V, dens, seed, **kw)
+    nodes = list(range(V))
+    bf_router.set_option(N.SRG_OPT_SPARSE_RELABEL, 1)
+    try:
+        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    except oracle.OracleError as e:
+        with pytest.raises(NetGraphError) as ei:
+            bf_router.compute_shortest_paths(g, nodes)
+        assert ei.value.code == e.code
+        return
+    t = bf_router.compute_shortest_paths(g, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    assert np.array_equal(t.latency_ns, lat)
+    assert bits_equal(t.packet_loss, loss)
+
+
 @pytest.mark.parametrize("kw", CASES, ids=lambda k: f"V{k['V']}_s{k['seed']}")
 def test_bf_random_vs_oracle(bf_router, kw):
     kw = dict(kw)
@@ -107,8 +129,8 @@ def test_bf_lane_masks(bf_router, kw, div, lm, sl):
 
 
 def test_bf_variants_c4_equal():
-    """C4 at full size: whole-row pulls, lane-masked pulls and split labels give identical
-    2.5e9-pair tables."""
+    """C4 at full size: whole-row pulls, lane-masked pulls and split labels, with and without the
+    degree-dealt vertex relabeling, give identical 2.5e9-pair tables."""
     import torch
     from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
     V = 50000
@@ -119,10 +141,11 @@ def test_bf_variants_c4_equal():
     ref = None
     ol = torch.empty((V, V), dtype=torch.int64, device=dev)
     os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
-    for lm, sl in ((0, 0), (1, 0), (0, 1), (1, 1)):
+    for lm, sl, rl in ((0, 0, 1), (1, 0, 1), (0, 1, 1), (1, 1, 1), (0, 0, 0)):
         r = Router(0)
         r.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, lm)
         r.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, sl)
+        r.set_option(N.SRG_OPT_SPARSE_RELABEL, rl)
         st = compute_shortest_paths_device(r, dg, nodes_t, ol, os_)
         torch.cuda.synchronize()
         assert st["path_kind"] == N.SRG_PATH_SPARSE_U32
