@@ -244,7 +244,9 @@ def main():
                     help="host = srg_compute_shortest_paths (host edge list in, host table out: H2D + D2H "
                          "included); device = srg_compute_shortest_paths_device (inputs/outputs in HBM)")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
-    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange (the default)")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: every rank ends with the whole table (RCCL row exchange; host entry: all rows D2H)")
     ap.add_argument("--sparse-group", type=int, default=None, help="sparse: label rows in flight per wave (4/8)")
     ap.add_argument("--sparse-wgs", type=int, default=None, help="sparse: resident batches per CU (1/2)")
     ap.add_argument("--sparse-delta-div", type=int, default=None,
@@ -331,7 +333,10 @@ def main():
         if router is None:
             log(f"[rank {rank}] multi-rank build unavailable ({fallback}): running independent replicas")
             strong = False
-        elif args.no_gather:
+        elif not args.gather:
+            # the row-distributed table: each rank's output holds the rows of the sources it
+            # routes (the layout one Shadow process driving N GPUs through an in-process rank
+            # group, srg_comm_init_local, writes into its single array); --gather replicates it
             router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
     if not strong:
         router = Router(local)
@@ -513,6 +518,8 @@ def main():
             "config": {"workload": f"{gdesc}, all {V} nodes used, {entry_desc}",
                        "entry": args.entry, "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
                        "parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single",
+                       **({"output": "row-distributed (each rank holds its sources' rows)" if not args.gather
+                           else "gathered (every rank holds the whole table)"} if strong else {}),
                        **({"fallback": fallback} if fallback else {}),
                        "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
             "apsp_wall_ms": round(ms_per_step, 3),

@@ -121,7 +121,9 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_PROFILING 1
 #define SRG_OPT_SPARSE_THRESHOLD 2
 #define SRG_OPT_GATHER_OUTPUT 3   /* multi-rank: 1 (default) = every rank ends with all rows;
-                                     0 = each rank fills only the rows of the sources it owns */
+                                     0 = each rank fills only the rows of the sources it owns (the host
+                                     entry then copies only those rows to the caller, and
+                                     stats.min_latency_ns is over those rows) */
 #define SRG_OPT_ALGORITHM 4       /* SRG_ALGO_*: how compute_shortest_paths routes */
 #define SRG_ALGO_AUTO 0           /* sparse when V >= 2048 and arcs * 32 < V^2, else dense */
 #define SRG_ALGO_DENSE 1          /* blocked FW + tight-DAG loss pass */

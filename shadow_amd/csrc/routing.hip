@@ -543,6 +543,7 @@ struct srg_ctx {
     size_t h_ring_bytes = 0;
     hipEvent_t ev_ring[3] = {nullptr, nullptr, nullptr};
     DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
+    size_t own_row0 = 0, own_row1 = ~(size_t)0;  // multi-rank without output exchange: the output rows this rank filled
     int sparse_relabel = 0;          // sparse: degree-dealt vertex ids (SRG_OPT_SPARSE_RELABEL; measured no gain on C4)
     DevBuf b_perm, b_rsrc, b_rdst, b_rslat, b_rsloss, b_rcols;  // its relabeled copies
     int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
@@ -1168,6 +1169,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const size_t VV = Vp * Vp;
     const bool multi = c.comm && c.comm->nranks > 1;
     Timer tm(st);
+    if (multi && !c.gather_output && pl.contiguous) {  // this rank's rows: one block in `nodes` order
+        c.own_row0 = pl.first[pl.g];
+        c.own_row1 = (size_t)pl.first[pl.g] + pl.cnt[pl.g];
+    }
 
     K* W = (K*)c.b_W.get(VV * sizeof(K));
     uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
@@ -1826,6 +1831,10 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     // this rank's sources, in graph-locality (BFS) order, in batches of 64 lanes: sources of
     // one batch are close to each other, so their Bellman-Ford frontiers move together
     const uint32_t p0 = (uint32_t)((uint64_t)rk * n / G), p1 = (uint32_t)((uint64_t)(rk + 1) * n / G);
+    if (multi && !c.gather_output) {  // this rank's rows: positions [p0, p1) of `nodes`
+        c.own_row0 = p0;
+        c.own_row1 = p1;
+    }
     const uint32_t nloc = p1 - p0;
     const uint32_t nbatch = (nloc + 63) / 64;
     std::vector<uint32_t> h_off(V + 1), h_src(arcs);
@@ -2378,18 +2387,25 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 return true;
             };
         }
+        c->own_row0 = 0;
+        c->own_row1 = ~(size_t)0;
         if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
         else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr);
+        // multi-rank without the output exchange: only this rank's rows leave the device
+        const size_t r0 = std::min<size_t>(c->own_row0, n), r1 = std::min<size_t>(c->own_row1, n);
+        const size_t rows_off = r1 > r0 ? r0 * n : 0, rows_nn = r1 > r0 ? (r1 - r0) * n : nn;
         auto t1 = std::chrono::steady_clock::now();
         unsigned long long hmin = ~0ull;
         if (nn && stats) {  // smallest latency over the table (feeds the runahead, manager.rs:238-243)
             unsigned long long* dmin = (unsigned long long*)c->b_multi.get(8);
             HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 8, st));
-            k_min_u64<<<grid_for(nn, 1024), kThreads, 0, st>>>(dol, nn, dmin);
+            k_min_u64<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dol + rows_off, rows_nn, dmin);  // own rows
             HIP_CHECK(hipMemcpyAsync(&hmin, dmin, 8, hipMemcpyDeviceToHost, st));
         }
-        if (nn && !sink.lat_sent) HIP_CHECK(hipMemcpyAsync(out_lat, dol, nn * 8, hipMemcpyDeviceToHost, st));
-        if (nn && !sink.loss_sent) HIP_CHECK(hipMemcpyAsync(out_loss, dos, nn * 4, hipMemcpyDeviceToHost, st));
+        if (nn && !sink.lat_sent)
+            HIP_CHECK(hipMemcpyAsync(out_lat + rows_off, dol + rows_off, rows_nn * 8, hipMemcpyDeviceToHost, st));
+        if (nn && !sink.loss_sent)
+            HIP_CHECK(hipMemcpyAsync(out_loss + rows_off, dos + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         sink.finish();
         if (stats) {

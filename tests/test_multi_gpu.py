@@ -84,9 +84,12 @@ def test_ranks_match_single_gpu(c):
     assert sum(t.stats["local_sources"] for t in out) == len(nodes)
 
 
-def test_ranks_without_exchange_fill_own_rows():
+@pytest.mark.parametrize("kind", ["scrambled", "all"])
+def test_ranks_without_exchange_fill_own_rows(kind):
+    """Output exchange off: each rank fills the rows of the sources it owns (with sorted nodes
+    those rows are one block, and the host entry copies only that block to the caller)."""
     e = synth.random_graph(400, 0.04, 11)
-    nodes = node_list("scrambled", 400, 11)
+    nodes = node_list(kind, 400, 11)
     lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
     out, errs = run_ranks(3, e, nodes, gather=False)
     assert errs == [None] * 3

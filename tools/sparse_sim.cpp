@@ -26,12 +26,13 @@ int main(int argc, char** argv) {
     const int nb = atoi(argv[4]);
     const int stride = argc > 5 ? atoi(argv[5]) : 1;
     const int per_lane = argc > 6 ? atoi(argv[6]) : 0;
-    const int gs_act = argc > 7 ? atoi(argv[7]) : 0;  // 1: arcs from vertices changed earlier in this sweep are pulled too
+    const int gs_act = argc > 7 ? atoi(argv[7]) : 0;
+    const int NL = argc > 8 ? atoi(argv[8]) : 64;  // sources per batch (lanes)  // 1: arcs from vertices changed earlier in this sweep are pulled too
     const uint32_t INF = 0xFFFFFFFFu;
     std::vector<uint32_t> L((size_t)V * 64);
     std::vector<uint8_t> fprev(V), fcur(V), mark(V), mnext(V), pend(V);
     double tot_pulls = 0, tot_sweeps = 0, tot_lanechg = 0;
-    const uint32_t nbatch = V / 64;
+    const uint32_t nbatch = V / NL;
     for (int bi = 0; bi < nb; ++bi) {
         const uint32_t b = (uint32_t)((bi * (size_t)stride) % nbatch);
         for (size_t i = 0; i < L.size(); ++i) L[i] = INF;
@@ -40,8 +41,8 @@ int main(int argc, char** argv) {
         std::fill(pend.begin(), pend.end(), 0);
         std::fill(mnext.begin(), mnext.end(), 0);
         std::fill(fcur.begin(), fcur.end(), 0);
-        for (int l = 0; l < 64; ++l) {
-            uint32_t s = order[b * 64 + l];
+        for (int l = 0; l < NL; ++l) {
+            uint32_t s = order[b * NL + l];
             L[(size_t)s * 64 + l] = 0;
             fprev[s] = 1;
             for (uint32_t k = off[s]; k < off[s + 1]; ++k) mark[src[k]] = 1;  // undirected: out == in
@@ -53,13 +54,13 @@ int main(int argc, char** argv) {
             // per-lane buckets: a lane of u is pushed only when it changed since its last push and
             // is below the bound; a vertex row is pulled by its out-neighbours when any lane is pushed
             std::vector<uint64_t> dirty(V, 0), pm(V, 0);
-            for (int l = 0; l < 64; ++l) dirty[order[b * 64 + l]] |= 1ull << l;
+            for (int l = 0; l < NL; ++l) dirty[order[b * NL + l]] |= 1ull << l;
             for (;;) {
                 bool anyact = false, anydirty = false;
                 for (uint32_t u = 0; u < V; ++u) {
                     uint64_t bl = 0;
                     if (dirty[u])
-                        for (int l = 0; l < 64; ++l)
+                        for (int l = 0; l < NL; ++l)
                             if (((dirty[u] >> l) & 1) && L[(size_t)u * 64 + l] < bound) bl |= 1ull << l;
                     pm[u] = bl;
                     anyact |= bl != 0;
@@ -82,7 +83,7 @@ int main(int argc, char** argv) {
                         if (!pm[u]) continue;
                         pulls++;
                         const uint32_t* lu = &L[(size_t)u * 64];
-                        for (int l = 0; l < 64; ++l)
+                        for (int l = 0; l < NL; ++l)
                             if (((pm[u] >> l) & 1) && lu[l] + w[k] < lt[l]) {
                                 lt[l] = lu[l] + w[k];
                                 dirty[t] |= 1ull << l;
@@ -103,18 +104,18 @@ int main(int argc, char** argv) {
                 if (!mark[t]) continue;
                 uint32_t* lt = &L[(size_t)t * 64];
                 uint32_t nl[64];
-                for (int l = 0; l < 64; ++l) nl[l] = lt[l];
+                for (int l = 0; l < NL; ++l) nl[l] = lt[l];
                 pulls++;  // own row
                 for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
                     uint32_t u = src[k];
                     if (!fprev[u] && !(gs_act && fcur[u])) continue;
                     pulls++;
                     const uint32_t* lu = &L[(size_t)u * 64];
-                    for (int l = 0; l < 64; ++l)
+                    for (int l = 0; l < NL; ++l)
                         if (lu[l] != INF && lu[l] + w[k] < nl[l]) nl[l] = lu[l] + w[k];
                 }
                 bool drop = false, below = false;
-                for (int l = 0; l < 64; ++l)
+                for (int l = 0; l < NL; ++l)
                     if (nl[l] < lt[l]) {
                         drop = true;
                         lanechg++;
@@ -156,6 +157,6 @@ int main(int argc, char** argv) {
         tot_lanechg += lanechg;
     }
     printf("{\"pulls_per_arc\": %.3f, \"sweeps\": %.2f, \"lane_changes_per_vertex_lane\": %.3f}\n",
-           tot_pulls / nb / A, tot_sweeps / nb, tot_lanechg / nb / (64.0 * V));
+           tot_pulls / nb / A, tot_sweeps / nb, tot_lanechg / nb / ((double)NL * V));
     return 0;
 }

@@ -75,7 +75,7 @@ def main():
         o.tofile("/tmp/ssim/order.bin")
         for div in divs:
             r = subprocess.run([exe, "/tmp/ssim/csr.bin", "/tmp/ssim/order.bin", str(maxw // div), str(nb), "61", os.environ.get("PER_LANE", "0"),
-                                os.environ.get("GS_ACT", "0")],
+                                os.environ.get("GS_ACT", "0"), os.environ.get("LANES", "64")],
                                capture_output=True, text=True)
             print(name, "delta=max/%d" % div, r.stdout.strip(), flush=True)
 
