@@ -175,6 +175,9 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SPARSE_RELABEL 27    /* sparse: 1 = vertices dealt over the 64-vertex windows in descending
                                      * in-degree order (balances the waves' sweep work; measured no gain on
                                      * C4); 0 (default) = given ids */
+#define SRG_OPT_SCAN_U64_LOW 28      /* u64 keys: 1 (default) = the pair-lane LDS scan (variant 5) on the keys'
+                                     * low 32 bits, exact with the loss pass's multi-predecessor check;
+                                     * 0 = the generic u64 scan */
 #define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -544,6 +544,8 @@ struct srg_ctx {
     hipEvent_t ev_ring[3] = {nullptr, nullptr, nullptr};
     DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
     size_t own_row0 = 0, own_row1 = ~(size_t)0;  // multi-rank without output exchange: the output rows this rank filled
+    int scan_u64_low = 1;            // u64 keys: pair-lane scan on the keys' low words (SRG_OPT_SCAN_U64_LOW; 0 = generic u64 scan)
+    DevBuf b_DST2;                   // its low-word DST
     int sparse_relabel = 0;          // sparse: degree-dealt vertex ids (SRG_OPT_SPARSE_RELABEL; measured no gain on C4)
     DevBuf b_perm, b_rsrc, b_rdst, b_rslat, b_rsloss, b_rcols;  // its relabeled copies
     int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
@@ -590,7 +592,7 @@ struct srg_ctx {
         for (hipEvent_t e : ev_ring)
             if (e) (void)hipEventDestroy(e);
         if (h_ring) (void)hipHostFree(h_ring);
-        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_perm, &b_rsrc, &b_rdst, &b_rslat, &b_rsloss, &b_rcols})
+        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_DST2, &b_perm, &b_rsrc, &b_rdst, &b_rslat, &b_rsloss, &b_rcols})
             b->release();
     }
 };
@@ -1069,6 +1071,12 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     }
 }
 
+// low 32 bits of u64 keys (the u64 path's scan input, tight_v5 with inf_check = 0)
+__global__ void k_low_words(const uint64_t* __restrict__ x, size_t n, uint32_t* __restrict__ lo) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        lo[i] = (uint32_t)x[i];
+}
+
 // Symmetric blocked FW (undirected graph, one rank, u32 pair-packed tiles): the same
 // lookahead schedule as fw_blocked over the stored tiles I <= J only (kernels.hip.h
 // fw_tile_sym), then the lower triangle is mirrored.  The chain of pivot k1 updates line k1
@@ -1368,7 +1376,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    const bool v5 = sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 9) || c.scan_variant >= 91);  // pair-lane LDS scans (9x: timing experiments)
+    // pair-lane LDS scans (9x: timing experiments); u64 keys run variant 5 on the keys' low words
+    // (tight_sparse.hip.h: exact together with the loss pass's multi-predecessor check)
+    const bool v5lo = sizeof(K) == 8 && c.scan_u64_low;
+    const bool v5 = (sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 9) || c.scan_variant >= 91)) || v5lo;
     const size_t npad = v5 ? ((size_t)nloc + 127) / 128 * 128 : ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
@@ -1483,14 +1494,12 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         float* ent_b = (float*)c.b_entb.get(Eb * 4);
         uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
         if (v5) {
-            if constexpr (sizeof(K) == 4) {
-                HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
-                uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
-                const size_t nwaves = (size_t)nw64 * nK5;
-                k_v5_fill<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK5, v5_cnt,
-                                                                                   v5_goff, cscoff, cscfill, rec, ent_w,
-                                                                                   ent_u, ent_b, cscent);
-            }
+            HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+            uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
+            const size_t nwaves = (size_t)nw64 * nK5;
+            k_v5_fill<K><<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK5, v5_cnt,
+                                                                                  v5_goff, cscoff, cscfill, rec, ent_w,
+                                                                                  ent_u, ent_b, cscent);
         } else if (lds) {
             if constexpr (sizeof(K) == 4) {
                 const size_t nwaves = (size_t)nw64 * nK;
@@ -1523,10 +1532,22 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             K* DST = (K*)c.b_DST.get(dst_bytes);
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
             const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
-            if constexpr (sizeof(K) == 4) {
-                if (v5) {
+            // the scan's DST: the keys themselves (u32), or their low words (u64 keys)
+            const uint32_t* DSTs = (const uint32_t*)DST;
+            uint32_t dsts_bytes = (uint32_t)std::min<size_t>(dst_bytes, 0xFFFFFFFFull);
+            if (v5lo) {
+                const size_t cnt = dst_bytes / 8;
+                uint32_t* lo = (uint32_t*)c.b_DST2.get(cnt * 4);
+                k_low_words<<<grid_for(cnt), kThreads, 0, st>>>(reinterpret_cast<const uint64_t*>(DST), cnt, lo);
+                DSTs = lo;
+                dsts_bytes = (uint32_t)(cnt * 4);
+            }
+            const uint32_t inf_check = v5lo ? 0u : 1u;
+            if (v5) {
+                {
                     const uint32_t nbS5 = (uint32_t)(npad / V5_SB);
-                    auto scan5 = c.scan_variant == 6 ? tight_v6 : c.scan_variant == 7 ? tight_v7<0> : c.scan_variant == 8 ? tight_v7<1>
+                    auto scan5 = v5lo ? tight_v5
+                                 : c.scan_variant == 6 ? tight_v6 : c.scan_variant == 7 ? tight_v7<0> : c.scan_variant == 8 ? tight_v7<1>
                                  : c.scan_variant == 91 ? tight_v7<0, 1> : c.scan_variant == 92 ? tight_v7<0, 2> : tight_v5;
                     // host entry: the scan runs in source-block groups, each group's loss rows folded
                     // right after it and shipped while later groups scan (loss rows on a second
@@ -1538,14 +1559,14 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                         auto cut = [&](uint32_t q) { return q == ng ? nbS5 : std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8); };
                         const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                         if (c1 == c0) continue;
-                        if (c.scan_variant == 9)
+                        if (c.scan_variant == 9 && !v5lo)
                             tight_v9<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
-                                (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
-                                v5_goff, (const uint32_t*)c.b_entkey.get(0), v5_cnt, PRED, Vp);
+                                DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
+                                v5_goff, (const uint32_t*)c.b_entkey.get(0), v5_cnt, PRED, Vp, inf_check);
                         else
                             scan5<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
-                                (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
-                                v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp);
+                                DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
+                                v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
                         HIP_CHECK(hipGetLastError());
                         if (interleave) {
                             const uint32_t r0 = c0 * V5_SB, r1 = std::min<uint32_t>(c1 * V5_SB, nloc);
@@ -1557,7 +1578,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                             sink->send_rows(st, out_loss, sink->loss, r0, r1 - r0, 4);
                         }
                     }
-                } else if (lds) {
+                }
+            } else if constexpr (sizeof(K) == 4) {
+                if (lds) {
                     auto kern = c.scan_variant == 4 ? tight_lds_u32_rl : tight_lds_u32;
                     kern<<<8u * nbTT * ((nbS + 7) / 8), LS_WAVES * 64, 0, st>>>(
                         (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, (uint32_t)Vp, nbTT, nbS, nK,
@@ -2530,6 +2553,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
+            return SRG_OK;
+        case SRG_OPT_SCAN_U64_LOW:
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            ctx->scan_u64_low = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_RELABEL:
             if (value != 0 && value != 1) return SRG_ERR_ARG;

@@ -896,12 +896,16 @@ __global__ void __launch_bounds__(256) k_v5_count(const unsigned long long* __re
 
 // records rec[e] = (lo | tl << 16, w) for entry e = 2 * pair + slot, plus ent_w / ent_u / ent_b
 // (k_loss_rows) and the CSC lists (any order: the MULTI fold is a min)
+// K = u64 (the u64-key path): records carry the low 32 bits of w (the scan then works on the
+// low words of the keys, see tight_v5), ent_w the exact key (the loss pass's multi-predecessor
+// check is exact).
+template <class K>
 __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __restrict__ ess,
-                                                  const uint32_t* __restrict__ W, const uint32_t* __restrict__ WL,
+                                                  const K* __restrict__ W, const uint32_t* __restrict__ WL,
                                                   size_t ld, uint32_t V, uint32_t nw64, uint32_t nK,
                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ goff,
                                                   const uint32_t* __restrict__ csc_off, uint32_t* __restrict__ csc_fill,
-                                                  uint2* __restrict__ rec, uint32_t* __restrict__ ent_w,
+                                                  uint2* __restrict__ rec, K* __restrict__ ent_w,
                                                   uint32_t* __restrict__ ent_u, float* __restrict__ ent_b,
                                                   uint32_t* __restrict__ csc_ent) {
     const uint32_t lane = threadIdx.x & 63;
@@ -924,8 +928,8 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
     const uint32_t cbase = t < V ? csc_off[t] : 0u;
     for (uint32_t u = u0; u < u1; ++u) {
         if (!((ess[(size_t)u * nw64 + w64] >> lane) & 1ull)) continue;
-        const uint32_t w = W[(size_t)u * ld + t];
-        rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), w);  // the pair's target: first slot only
+        const K w = W[(size_t)u * ld + t];
+        rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), (uint32_t)w);  // the pair's target: first slot only
         ent_w[e] = w;
         ent_u[e] = u;
         ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));
@@ -934,7 +938,7 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
     }
     if (c & 1u) {  // odd run: a sentinel second slot (w = INF is never tight on a reachable target)
         rec[e] = make_uint2(0u, KeyOps<uint32_t>::INF);
-        ent_w[e] = KeyOps<uint32_t>::INF;
+        ent_w[e] = KeyOps<K>::INF;
         ent_u[e] = 0;
         ent_b[e] = 1.0f;
     }
@@ -942,7 +946,7 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
         const uint32_t total = incl;
         for (size_t q = 2 * ((size_t)pbase + total); q < 2 * (size_t)goff[g + 1]; ++q) {
             rec[q] = make_uint2(0u, KeyOps<uint32_t>::INF);
-            ent_w[q] = KeyOps<uint32_t>::INF;
+            ent_w[q] = KeyOps<K>::INF;
             ent_u[q] = 0;
             ent_b[q] = 1.0f;
         }
@@ -954,6 +958,13 @@ struct alignas(64) V5Grp {
     uint32_t v[16];
 };
 
+// u64 keys (inf_check = 0): DST and the record weights hold the LOW 32 bits of the keys, and the
+// test a + w == d runs mod 2^32.  That is exact in combination with the loss pass: the true tight
+// predecessor of a reachable target always matches, so a single match IS it, and any false
+// match (a + w - d a nonzero multiple of 2^32) adds a second one, i.e. PRED_MULTI, which
+// k_loss_rows resolves with the exact u64 keys (DST / ent_w of type K).  Targets unreachable
+// from the source are not used pairs (certified before the scan) and are no tight predecessor
+// of a reachable target, so their entries are never read through a single match.
 // grid: 8 * nbTT * ceil((nbS - c0) / 8) workgroups of 512 for the source blocks [c0, nbS)
 // (XCD-aware: the workgroups of one XCD share the 128-source block, whose staged rows then come
 // out of that XCD's L2)
@@ -961,7 +972,7 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
-                                                    uint32_t* __restrict__ PRED, size_t ldp) {
+                                                    uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
     const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
@@ -1063,7 +1074,7 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
             const uint32_t t = t0 + j;
             const uint32_t nd = h ? ndh[j] : ndl[j];
             const uint32_t st = h ? sth[j] : stl[j];
-            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+            o[j] = (t >= V || t == s || (inf_check && nd == 0u - KeyOps<uint32_t>::INF)) ? PRED_NONE : st;
         }
         uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
 #pragma unroll
@@ -1081,7 +1092,7 @@ __global__ void __launch_bounds__(512, 4) tight_v6(const uint32_t* __restrict__ 
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
-                                                    uint32_t* __restrict__ PRED, size_t ldp) {
+                                                    uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
     const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
@@ -1214,7 +1225,7 @@ __global__ void __launch_bounds__(512, 4) tight_v6(const uint32_t* __restrict__ 
             const uint32_t t = t0 + j;
             const uint32_t nd = h ? ndh[j] : ndl[j];
             const uint32_t st = h ? sth[j] : stl[j];
-            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+            o[j] = (t >= V || t == s || (inf_check && nd == 0u - KeyOps<uint32_t>::INF)) ? PRED_NONE : st;
         }
         uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
 #pragma unroll
@@ -1238,7 +1249,7 @@ __global__ void __launch_bounds__(512, 4) tight_v7(const uint32_t* __restrict__ 
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
-                                                    uint32_t* __restrict__ PRED, size_t ldp) {
+                                                    uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     __shared__ __attribute__((aligned(16))) uint4 recs[2 * V7_RC];             // 2 x 7 KB record ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
@@ -1376,7 +1387,7 @@ __global__ void __launch_bounds__(512, 4) tight_v7(const uint32_t* __restrict__ 
             const uint32_t t = t0 + j;
             const uint32_t nd = h ? ndh[j] : ndl[j];
             const uint32_t st = h ? sth[j] : stl[j];
-            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+            o[j] = (t >= V || t == s || (inf_check && nd == 0u - KeyOps<uint32_t>::INF)) ? PRED_NONE : st;
         }
         uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
 #pragma unroll
@@ -1397,7 +1408,7 @@ __global__ void __launch_bounds__(512, 4) tight_v9(const uint32_t* __restrict__ 
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
                                                     const uint32_t* __restrict__ ecnt, uint32_t* __restrict__ PRED,
-                                                    size_t ldp) {
+                                                    size_t ldp, uint32_t inf_check) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     __shared__ __attribute__((aligned(16))) uint4 recs[2 * V7_RC];             // 2 x 7 KB record ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
@@ -1520,7 +1531,7 @@ __global__ void __launch_bounds__(512, 4) tight_v9(const uint32_t* __restrict__ 
             const uint32_t t = t0 + j;
             const uint32_t nd = h ? ndh[j] : ndl[j];
             const uint32_t st = h ? sth[j] : stl[j];
-            o[j] = (t >= V || t == s || nd == 0u - KeyOps<uint32_t>::INF) ? PRED_NONE : st;
+            o[j] = (t >= V || t == s || (inf_check && nd == 0u - KeyOps<uint32_t>::INF)) ? PRED_NONE : st;
         }
         uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
 #pragma unroll

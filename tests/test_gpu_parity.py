@@ -373,6 +373,34 @@ def test_host_entry_early_rows_match_device(router, mode, groups):
     assert bits_equal(os_.cpu().numpy(), t.packet_loss)
 
 
+@pytest.mark.parametrize("shift,offset", [(32, 0), (32, 1), (40, 7), (0, 2 ** 33)])
+def test_u64_low_word_scan(router, shift, offset):
+    """u64 keys: the pair-lane scan on the keys' low 32 bits (SRG_OPT_SCAN_U64_LOW) equals the
+    generic u64 scan and the oracle.  Latencies that are multiples of 2^32 make every candidate
+    match in the low words (false matches everywhere: the loss pass's exact multi-predecessor
+    check must resolve them); with offsets the low words are informative again."""
+    g = synth.random_graph(300, 0.08, 5 + shift, lat_lo=1, lat_hi=6, parallel=0.1)
+    lat = g.latency_ns.astype(np.uint64) * np.uint64(2 ** shift) + np.uint64(offset)
+    e = Edges(g.num_vertices, g.src, g.dst, lat, g.packet_loss, directed=False)
+    nodes = list(range(300))
+    try:
+        ref_lat, ref_loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
+    except oracle.OracleError as err:
+        with pytest.raises(NetGraphError) as ei:
+            router.compute_shortest_paths(e, nodes)
+        assert ei.value.code == err.code
+        return
+    out = []
+    for low in (1, 0):
+        router.set_option(N.SRG_OPT_SCAN_U64_LOW, low)
+        t = router.compute_shortest_paths(e, nodes)
+        assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+        out.append(t)
+    router.set_option(N.SRG_OPT_SCAN_U64_LOW, 1)
+    for t in out:
+        assert_parity(t, ref_lat, ref_loss)
+
+
 def test_h2d_codec_matches_plain(router):
     """Host entry H2D codec (SRG_OPT_H2D_CODEC: u16 endpoints + u32 latencies over PCIe, widened on
     the device) gives the same bytes as the plain transfer; a latency >= 2^32 makes it fall back
