@@ -2278,11 +2278,16 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st) 
             std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
             if ((orx >> 16) || (orl >> 32)) bad.store(true, std::memory_order_relaxed);
         });
-        t_conv += ms_since(tc);
+        const double dt = ms_since(tc);
+        t_conv += dt;
         if (bad.load()) {
             HIP_CHECK(hipStreamSynchronize(st));  // no DMA may still read the ring
             return false;
         }
+        // the host is busy (narrowing this chunk took longer than shipping it plain would at
+        // ~55 GB/s): the remaining edges go plain, straight from the caller's arrays
+        bool slow = ch + 1 < nch && dt > (double)ne * 20.0 / 55e9 * 1e3;
+        if (const char* f = std::getenv("SRG_CODEC_SLOW_AFTER")) slow = ch + 1 < nch && ch >= (size_t)std::atoll(f);  // tests
         HIP_CHECK(hipMemcpyAsync(s16 + e0, hs, ne * 2, hipMemcpyHostToDevice, st));
         HIP_CHECK(hipMemcpyAsync(d16 + e0, hd, ne * 2, hipMemcpyHostToDevice, st));
         HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
@@ -2291,6 +2296,15 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st) 
         k_widen_edges<<<grid_for(ne), kThreads, 0, st>>>(ne, s16 + e0, d16 + e0, l32 + e0, (uint32_t*)dg.src + e0,
                                                           (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
         HIP_CHECK(hipGetLastError());
+        if (slow) {
+            const size_t r0 = e0 + ne, rn = E - r0;
+            HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.src + r0, g->src + r0, rn * 4, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.dst + r0, g->dst + r0, rn * 4, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync((uint64_t*)dg.lat + r0, g->latency_ns + r0, rn * 8, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync((float*)dg.loss + r0, g->packet_loss + r0, rn * 4, hipMemcpyHostToDevice, st));
+            if (dbg) std::fprintf(stderr, "codec: host slow after chunk %zu (%.2f ms), rest plain\n", ch, dt);
+            break;
+        }
     }
     if (dbg) std::fprintf(stderr, "codec: %zu chunks, %d threads, convert %.2f ms, slot waits %.2f ms\n", nch,
                           c.pool->size(), t_conv, t_wait);

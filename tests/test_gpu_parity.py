@@ -429,6 +429,21 @@ def test_h2d_codec_matches_plain(router):
     assert np.array_equal(t.latency_ns, t0.latency_ns) and bits_equal(t.packet_loss, t0.packet_loss)
 
 
+def test_h2d_codec_host_slow_fallback(router, monkeypatch):
+    """The codec's mid-transfer switch to plain arrays (taken when narrowing a chunk on the host
+    is slower than shipping it plain; forced here after the first chunk) gives the same bytes."""
+    V = 2100  # 2.2 M edges: two codec chunks
+    g = synth.atlas_like(V, seed=33)
+    nodes = list(range(V))
+    monkeypatch.setenv("SRG_CODEC_SLOW_AFTER", "0")
+    t = router.compute_shortest_paths(g, nodes)
+    monkeypatch.delenv("SRG_CODEC_SLOW_AFTER")
+    router.set_option(N.SRG_OPT_H2D_CODEC, 0)
+    t0 = router.compute_shortest_paths(g, nodes)
+    router.set_option(N.SRG_OPT_H2D_CODEC, 1)
+    assert np.array_equal(t.latency_ns, t0.latency_ns) and bits_equal(t.packet_loss, t0.packet_loss)
+
+
 @pytest.mark.slow
 def test_c1_full_vs_oracle(router):
     """Config C1 (1000-vertex complete graph), every pair."""
