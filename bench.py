@@ -382,6 +382,8 @@ def main():
     if args.simulate_rank:
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)
+        if not args.gather:  # as the N > 1 default: this rank's rows only
+            router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
 
     if args.entry == "host":
         import numpy as np
@@ -446,7 +448,8 @@ def main():
             + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
             + (f":fold{args.fw_fold}" if args.fw_fold else "") + (f":cus{args.chain_cus}" if args.chain_cus else "")
             + (f":p1t{args.p1_threads}" if args.p1_threads and args.p1_threads != 512 else "")
-            + (":norelabel" if args.sparse_relabel == 0 else ""))
+            + (":relabel" if args.sparse_relabel else "")
+            + (f":n{world}" if world > 1 else "") + (f":sim{args.simulate_rank}" if args.simulate_rank else ""))
     roofline = None
     if agg.get("prof_launches") and kind == 3:
         # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
