@@ -178,7 +178,11 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SCAN_U64_LOW 28      /* u64 keys: 1 (default) = the pair-lane LDS scan (variant 5) on the keys'
                                      * low 32 bits, exact with the loss pass's multi-predecessor check;
                                      * 0 = the generic u64 scan */
-#define SRG_OPT_CHAIN_SPLIT 19      /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
+#define SRG_OPT_EDGE_SHARD 29        /* host entry, multi-rank: 1 = each rank ships 1/N of the edge list over
+                                     * its own PCIe link and the ranks exchange the slices over the GPU
+                                     * links (allgatherv); 0 = every rank ships the whole list; -1 (default)
+                                     * = 1 when the group has >= 4 ranks */
+#define SRG_OPT_CHAIN_SPLIT 19     /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */
 int srg_set_option(srg_ctx* ctx, int option, double value);

@@ -546,6 +546,9 @@ struct srg_ctx {
     size_t own_row0 = 0, own_row1 = ~(size_t)0;  // multi-rank without output exchange: the output rows this rank filled
     int scan_u64_low = 1;            // u64 keys: pair-lane scan on the keys' low words (SRG_OPT_SCAN_U64_LOW; 0 = generic u64 scan)
     DevBuf b_DST2;                   // its low-word DST
+    int edge_shard = -1;             // host entry, multi-rank: ship 1/N of the edges, allgatherv the rest (SRG_OPT_EDGE_SHARD)
+    const uint32_t* sim_edges = nullptr;  // simulated rank: the edge list whose other slices are resident
+    size_t sim_E = 0;
     int sparse_relabel = 0;          // sparse: degree-dealt vertex ids (SRG_OPT_SPARSE_RELABEL; measured no gain on C4)
     DevBuf b_perm, b_rsrc, b_rdst, b_rslat, b_rsloss, b_rcols;  // its relabeled copies
     int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
@@ -2207,7 +2210,7 @@ __global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const 
 // the device.  Host threads narrow chunk i+1 into a page-locked ring while chunk i is in flight.
 // Returns false (nothing usable staged) when an endpoint >= 65536 or a latency >= 2^32 is seen:
 // the caller then ships the plain arrays, whose checks report such edges as the reference does.
-bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st);
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1);
 
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
@@ -2216,8 +2219,10 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
     return d;
 }
 
-bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st) {
-    const size_t E = g->num_edges;
+// Ships edges [a0, a1) into the full-length device arrays (the rank's slice when the edge list
+// is sharded, else all of it).
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1) {
+    const size_t E = g->num_edges, A = a1 - a0;
     constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
     constexpr int NB = 3;                   // ring slots
     const size_t slot = CE * 16;
@@ -2247,12 +2252,12 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st) 
     std::atomic<bool> bad{false};
     const bool dbg = std::getenv("SRG_DEBUG_CODEC") != nullptr;
     double t_conv = 0, t_wait = 0;
-    const size_t nch = (E + CE - 1) / CE;
+    const size_t nch = (A + CE - 1) / CE;
     for (size_t ch = 0; ch < nch; ++ch) {
         const int b = (int)(ch % NB);
         auto tw = std::chrono::steady_clock::now();
         if (ch >= (size_t)NB) HIP_CHECK(hipEventSynchronize(c.ev_ring[b]));  // the slot's previous DMA is done
-        const size_t e0 = ch * CE, ne = std::min(CE, E - e0);
+        const size_t e0 = a0 + ch * CE, ne = std::min(CE, a1 - e0);
         unsigned char* base = (unsigned char*)c.h_ring + (size_t)b * slot;
         uint16_t* hs = (uint16_t*)base;
         uint16_t* hd = hs + CE;
@@ -2298,7 +2303,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st) 
                                                           (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
         HIP_CHECK(hipGetLastError());
         if (slow) {
-            const size_t r0 = e0 + ne, rn = E - r0;
+            const size_t r0 = e0 + ne, rn = a1 - r0;
             HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.src + r0, g->src + r0, rn * 4, hipMemcpyHostToDevice, st));
             HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.dst + r0, g->dst + r0, rn * 4, hipMemcpyHostToDevice, st));
             HIP_CHECK(hipMemcpyAsync((uint64_t*)dg.lat + r0, g->latency_ns + r0, rn * 8, hipMemcpyHostToDevice, st));
@@ -2395,13 +2400,63 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         const size_t E = g->num_edges, n = num_nodes;
         DevGraph dg{g->num_vertices, (int)g->directed, g->num_edges, nullptr, nullptr, nullptr, nullptr,
                     nullptr, g->node_ids};
+        // Multi-rank: every rank needs the whole edge list (W's rows feed the essential-entry
+        // records of every source), but each GPU has its own PCIe link and the GPUs a mesh of
+        // their own: rank r ships edges [E r/N, E (r+1)/N) and the slices are exchanged device to
+        // device.  The slice ranges are a function of (E, N) only, so every rank agrees on them.
+        const int nr = c->comm ? c->comm->nranks : 1, rk = c->comm ? c->comm->rank : 0;
+        const bool shard = nr > 1 && (c->edge_shard == 1 || (c->edge_shard < 0 && nr >= 4));
+        const size_t a0 = shard ? E * rk / nr : 0, a1 = shard ? E * (rk + 1) / nr : E;
         // narrowed edge list over PCIe when it fits (falls back to the plain arrays otherwise)
-        const bool coded = c->h2d_codec && E >= ((size_t)1 << 20) && g->num_vertices <= 65536 && codec_in(*c, g, dg, st);
+        const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) && g->num_vertices <= 65536 &&
+                           codec_in(*c, g, dg, st, a0, a1);
         if (!coded) {
-            dg.src = stage_in(c->b_src, g->src, E, st);
-            dg.dst = stage_in(c->b_dst, g->dst, E, st);
-            dg.lat = stage_in(c->b_lat, g->latency_ns, E, st);
-            dg.loss = stage_in(c->b_loss, g->packet_loss, E, st);
+            const size_t cnt = std::max<size_t>(E, 1);
+            dg.src = (uint32_t*)c->b_src.get(cnt * 4);
+            dg.dst = (uint32_t*)c->b_dst.get(cnt * 4);
+            dg.lat = (uint64_t*)c->b_lat.get(cnt * 8);
+            dg.loss = (float*)c->b_loss.get(cnt * 4);
+            if (a1 > a0) {
+                HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.src + a0, g->src + a0, (a1 - a0) * 4, hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.dst + a0, g->dst + a0, (a1 - a0) * 4, hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync((uint64_t*)dg.lat + a0, g->latency_ns + a0, (a1 - a0) * 8,
+                                         hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync((float*)dg.loss + a0, g->packet_loss + a0, (a1 - a0) * 4,
+                                         hipMemcpyHostToDevice, st));
+            }
+        }
+        const bool sim = shard && std::strcmp(c->comm->kind(), "simulated") == 0;
+        if (sim && (c->sim_edges != g->src || c->sim_E != E)) {
+            // SRG_OPT_SIMULATE_RANK elides the exchange: the other slices are shipped once per
+            // edge list (a warm-up call), so later calls time this rank's slice and stay valid
+            auto put = [&](size_t e0, size_t e1) {
+                if (e1 <= e0) return;
+                HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.src + e0, g->src + e0, (e1 - e0) * 4, hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.dst + e0, g->dst + e0, (e1 - e0) * 4, hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync((uint64_t*)dg.lat + e0, g->latency_ns + e0, (e1 - e0) * 8,
+                                         hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, g->packet_loss + e0, (e1 - e0) * 4,
+                                         hipMemcpyHostToDevice, st));
+            };
+            put(0, a0);
+            put(a1, E);
+            c->sim_edges = g->src;
+            c->sim_E = E;
+        }
+        if (shard) {  // the wide arrays, so each rank may have shipped its slice coded or plain
+            std::vector<size_t> offs(nr), lens(nr);
+            auto gather = [&](const void* p, size_t elem) {
+                for (int q = 0; q < nr; ++q) {
+                    const size_t q0 = E * q / nr, q1 = E * (q + 1) / nr;
+                    offs[q] = q0 * elem;
+                    lens[q] = (q1 - q0) * elem;
+                }
+                c->comm->allgatherv(const_cast<void*>(p), offs.data(), lens.data(), st);
+            };
+            gather(dg.src, 4);
+            gather(dg.dst, 4);
+            gather(dg.lat, 8);
+            gather(dg.loss, 4);
         }
         const uint32_t* dn = stage_in(c->b_nodes, nodes, n, st);
         uint64_t* dol = (uint64_t*)c->b_olat.get(std::max<size_t>(nn, 1) * 8);
@@ -2517,6 +2572,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             const int v = (int)value;
             delete ctx->comm;
             ctx->comm = nullptr;
+            ctx->sim_edges = nullptr;
             if (v > 0) {
                 const int nr = v / 1000, rk = v % 1000;
                 if (nr < 1 || rk >= nr) return SRG_ERR_ARG;
@@ -2572,6 +2628,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SCAN_U64_LOW:
             if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->scan_u64_low = (int)value;
+            return SRG_OK;
+        case SRG_OPT_EDGE_SHARD:
+            if (value != 0 && value != 1 && value != -1) return SRG_ERR_ARG;
+            ctx->edge_shard = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_RELABEL:
             if (value != 0 && value != 1) return SRG_ERR_ARG;

@@ -15,7 +15,7 @@ from helpers import bits_equal
 pytestmark = pytest.mark.gpu
 
 
-def run_ranks(G, edges, nodes, gather=True, threshold=None):
+def run_ranks(G, edges, nodes, gather=True, threshold=None, shard=None):
     group = LocalGroup(G)
     routers = [Router(0) for _ in range(G)]
     for r, rt in enumerate(routers):
@@ -25,6 +25,8 @@ def run_ranks(G, edges, nodes, gather=True, threshold=None):
             rt.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
         if threshold is not None:
             rt.set_option(N.SRG_OPT_SPARSE_THRESHOLD, threshold)
+        if shard is not None:
+            rt.set_option(N.SRG_OPT_EDGE_SHARD, shard)
     out, errs = [None] * G, [None] * G
 
     def work(r):
@@ -103,6 +105,54 @@ def test_ranks_without_exchange_fill_own_rows(kind):
         assert bits_equal(t.packet_loss[rows], loss[rows])
         covered[rows] = True
     assert covered.all()
+
+
+@pytest.mark.parametrize("G,shard", [(2, 1), (3, 1), (4, 0), (8, 1)])
+def test_edge_sharded_host_entry(G, shard):
+    """SRG_OPT_EDGE_SHARD: each rank ships only its 1/G slice of the edge list and the slices are
+    exchanged between the ranks (default on from 4 ranks); every rank still gets the oracle's
+    table.  E is not a multiple of G, so the slices are ragged."""
+    e = synth.random_graph(350, 0.07, 20 + G, parallel=0.1)
+    assert e.num_edges % G
+    nodes = node_list("scrambled", 350, 20 + G)
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
+    out, errs = run_ranks(G, e, nodes, shard=shard)
+    assert errs == [None] * G, errs
+    for r, t in enumerate(out):
+        assert np.array_equal(t.latency_ns, lat), f"rank {r} latency"
+        assert bits_equal(t.packet_loss, loss), f"rank {r} loss"
+
+
+def test_edge_sharded_codec_slices():
+    """Edge sharding with the H2D codec active on every rank's slice (>= 2^20 edges per slice):
+    the exchanged widened slices equal the single-GPU build."""
+    e = synth.atlas_like(2100, seed=2100)
+    assert e.num_edges >= 2 * (1 << 20) + 2
+    nodes = list(range(0, 2100, 7))
+    r1 = Router(0)
+    ref = r1.compute_shortest_paths(e, nodes)
+    r1.close()
+    out, errs = run_ranks(2, e, nodes, shard=1)
+    assert errs == [None] * 2, errs
+    for r, t in enumerate(out):
+        assert np.array_equal(t.latency_ns, ref.latency_ns), f"rank {r} latency"
+        assert bits_equal(t.packet_loss, ref.packet_loss), f"rank {r} loss"
+
+
+def test_edge_sharded_bad_edge_on_one_slice():
+    """An out-of-range endpoint in the last rank's slice: every rank reports the reference's
+    error (the checks run on the exchanged whole list), none hangs."""
+    from shadow_amd.graph import Edges
+    g = synth.random_graph(200, 0.05, 21)
+    dst = g.dst.copy()
+    dst[-1] = 200  # only rank G-1 ships it
+    e = Edges(200, g.src, dst, g.latency_ns, g.packet_loss, False)
+    single = Router(0)
+    with pytest.raises(NetGraphError) as ref:
+        single.compute_shortest_paths(e, list(range(200)))
+    single.close()
+    out, errs = run_ranks(4, e, list(range(200)), shard=1)
+    assert all(isinstance(x, NetGraphError) and x.code == ref.value.code for x in errs), errs
 
 
 def test_ranks_agree_on_errors():
