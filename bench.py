@@ -261,6 +261,11 @@ def main():
     ap.add_argument("--sparse-relabel", type=int, default=None, help="sparse: 1 = degree-dealt vertex ids (default), 0 = given ids")
     ap.add_argument("--p1-threads", type=int, default=None, help="symmetric FW pivot closure threads (512/1024)")
     ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")
+    ap.add_argument("--late-loss", type=int, default=None,
+                    help="host entry: 1 = edge losses shipped beside the W build and FW (default), 0 = with the edges")
+    ap.add_argument("--edge-shard", type=int, default=None,
+                    help="host entry, N > 1: 1 = each rank ships 1/N of the edges and the ranks exchange them, "
+                         "0 = every rank ships all, -1 = auto (default: on from 4 ranks)")
     ap.add_argument("--chain-cus", type=int, default=None, help="symmetric FW: CUs reserved for the chain (0 = none)")
     ap.add_argument("--fw-fold", type=int, default=None, help="symmetric FW: 1 = add,add,min3; 0 = lshl_add_u64,min3")
     ap.add_argument("--scan-groups", type=int, default=None, help="host entry: scan launches interleaved with the loss (0 = auto)")
@@ -367,6 +372,10 @@ def main():
         router.set_option(N.SRG_OPT_P1_THREADS, args.p1_threads)
     if args.h2d_codec is not None:
         router.set_option(N.SRG_OPT_H2D_CODEC, args.h2d_codec)
+    if args.late_loss is not None:
+        router.set_option(N.SRG_OPT_LATE_LOSS, args.late_loss)
+    if args.edge_shard is not None:
+        router.set_option(N.SRG_OPT_EDGE_SHARD, args.edge_shard)
     if args.chain_cus is not None:
         router.set_option(N.SRG_OPT_CHAIN_CUS, args.chain_cus)
     if args.fw_fold is not None:

@@ -182,6 +182,9 @@ void srg_destroy(srg_ctx* ctx);
                                      * its own PCIe link and the ranks exchange the slices over the GPU
                                      * links (allgatherv); 0 = every rank ships the whole list; -1 (default)
                                      * = 1 when the group has >= 4 ranks */
+#define SRG_OPT_LATE_LOSS 30         /* host entry: 1 (default) = the edge losses cross PCIe after the endpoints
+                                     * and latencies, on their own stream beside the W build and FW (which
+                                     * need no loss); 0 = with them */
 #define SRG_OPT_CHAIN_SPLIT 19     /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
 #define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
                                           source's loss only where its candidate latency can still win */

@@ -57,6 +57,7 @@ SRG_OPT_P1_THREADS = 26
 SRG_OPT_SPARSE_RELABEL = 27
 SRG_OPT_SCAN_U64_LOW = 28
 SRG_OPT_EDGE_SHARD = 29
+SRG_OPT_LATE_LOSS = 30
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

@@ -137,7 +137,7 @@ __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const 
         if (s == t) {
             atomicAdd(&selfcnt[s], 1u);
             self_lat[s] = l;      // meaningful only when the count ends at exactly 1
-            self_loss[s] = loss[e];
+            if (loss) self_loss[s] = loss[e];  // null: the loss arrives later (k_self_loss)
         } else {
             mx = l > mx ? l : mx;
             ovf |= (l == UINT64_MAX);
@@ -151,6 +151,15 @@ __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const 
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_lat, mx);
     if (bad) atomicOr(&st->bad_endpoint, 1u);
     if (ovf) atomicOr(&st->lat_overflow, 1u);
+}
+
+// the self-loops' loss, when the edge losses arrive after k_edge_scan (host entry, late loss)
+__global__ void k_self_loss(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                            const float* __restrict__ loss, uint32_t V, float* __restrict__ self_loss) {
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e];
+        if (s == dst[e] && s < V) self_loss[s] = loss[e];
+    }
 }
 
 template <class K>
@@ -201,7 +210,8 @@ __global__ void k_w_key(uint64_t E, const uint32_t* __restrict__ src, const uint
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
         if (s == t) continue;  // self-loops never shorten a path; kept for the diagonal only
-        const unsigned long long k = ((unsigned long long)lat[e] << 32) | __float_as_uint(loss[e] + 0.0f);
+        // null loss: latency only (WL is then built by k_w_loss once the losses have arrived)
+        const unsigned long long k = ((unsigned long long)lat[e] << 32) | (loss ? __float_as_uint(loss[e] + 0.0f) : 0u);
         atomicMin(&KW[(size_t)s * ld + t], k);
     }
 }
@@ -546,6 +556,12 @@ struct srg_ctx {
     size_t own_row0 = 0, own_row1 = ~(size_t)0;  // multi-rank without output exchange: the output rows this rank filled
     int scan_u64_low = 1;            // u64 keys: pair-lane scan on the keys' low words (SRG_OPT_SCAN_U64_LOW; 0 = generic u64 scan)
     DevBuf b_DST2;                   // its low-word DST
+    int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
+    int wl_grid = 0;                 // its WL build's workgroups (0 = 64; env SRG_WL_GRID, experiments)
+    hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
+    hipEvent_t ev_build = nullptr, ev_wl = nullptr, ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr;
+    void* h_lring = nullptr;         // pinned ring of the late loss H2D
+    hipEvent_t ev_lring[3] = {nullptr, nullptr, nullptr};
     int edge_shard = -1;             // host entry, multi-rank: ship 1/N of the edges, allgatherv the rest (SRG_OPT_EDGE_SHARD)
     const uint32_t* sim_edges = nullptr;  // simulated rank: the edge list whose other slices are resident
     size_t sim_E = 0;
@@ -587,8 +603,11 @@ struct srg_ctx {
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_build, ev_wl, ev_ledges, ev_lin, ev_ldone})
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_lring)
+            if (e) (void)hipEventDestroy(e);
+        if (h_lring) (void)hipHostFree(h_lring);
         for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream, cu_bulk, cu_chain})
             if (s) (void)hipStreamDestroy(s);
         delete pool;
@@ -602,6 +621,58 @@ struct srg_ctx {
 
 namespace {
 
+// Host entry with SRG_OPT_LATE_LOSS: the edge losses cross PCIe on their own stream after the
+// endpoints and latencies, while the W build and FW (which need no loss) run.  Every reader of
+// `DevGraph::loss` first calls loss_arrive() on its stream.
+struct LateLoss {
+    hipStream_t ls = nullptr;   // c.loss_stream
+    std::thread th;             // queues the chunked H2D of the losses (pinned ring) on c.loss_stream
+    hipEvent_t ev_in = nullptr;  // recorded by `th` after the last loss chunk
+    hipEvent_t ev_done = nullptr;  // the losses and the self-loop losses are on the device
+    bool joined = false, applied = false;
+    std::string err;
+    // Work that `th` queues on `ls` after the last chunk (the main thread must not block on the
+    // ring while it launches FW): handed over once by give(), or nothing when join() comes first.
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> post;
+    bool post_set = false;
+    void give(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            post = std::move(f);
+            post_set = true;
+        }
+        cv.notify_all();
+    }
+    std::function<void()> take() {  // called by `th`
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return post_set; });
+        return post;
+    }
+    void join() {
+        if (!joined) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                post_set = true;  // no work handed over: release the helper
+            }
+            cv.notify_all();
+            if (th.joinable()) th.join();
+            joined = true;
+        }
+        if (!err.empty()) fail(SRG_ERR_HIP, "loss H2D: " + err);
+    }
+    ~LateLoss() {  // no DMA into the ring or the device losses may outlive the call
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            post_set = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();
+        if (ls) (void)hipStreamSynchronize(ls);
+    }
+};
+
 struct DevGraph {
     uint32_t V;
     int directed;
@@ -612,7 +683,29 @@ struct DevGraph {
     const float* loss;
     const uint32_t* ids_dev;    // may be null
     const uint32_t* ids_host;   // may be null (host entry)
+    LateLoss* late = nullptr;   // non-null: `loss` is still in flight (loss_arrive before reading it)
 };
+
+// the self-loop losses, then ev_done, on stream s (after the loss chunks)
+void self_loss_done(const DevGraph& g, float* self_loss, hipStream_t s) {
+    if (g.E) k_self_loss<<<grid_for(g.E), kThreads, 0, s>>>(g.E, g.src, g.dst, g.loss, g.V, self_loss);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(g.late->ev_done, s));
+}
+
+// Make `s` wait until g.loss (and the self-loop losses) are on the device.
+void loss_arrive(const DevGraph& g, float* self_loss, hipStream_t s) {
+    LateLoss* L = g.late;
+    if (!L) return;
+    L->join();  // every command of the helper is queued (ev_in / ev_done recorded)
+    if (!L->applied) {
+        HIP_CHECK(hipStreamWaitEvent(s, L->ev_in, 0));
+        self_loss_done(g, self_loss, s);
+        L->applied = true;
+    } else {
+        HIP_CHECK(hipStreamWaitEvent(s, L->ev_done, 0));
+    }
+}
 
 uint32_t node_gml_id(const DevGraph& g, uint32_t v, hipStream_t st) {
     if (g.ids_host) return g.ids_host[v];
@@ -659,7 +752,7 @@ Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     HIP_CHECK(hipMemsetAsync(P.flags, 0, sizeof(Flags), st));
     if (n) k_check_nodes<<<grid_for(n), kThreads, 0, st>>>(nodes, n, V, mark, P.flags);
     if (g.E)
-        k_edge_scan<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, V, P.selfcnt,
+        k_edge_scan<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.late ? nullptr : g.loss, V, P.selfcnt,
                                                        P.selflat, P.selfloss, es);
     HIP_CHECK(hipGetLastError());
     Flags fl;
@@ -1188,15 +1281,41 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     K* W = (K*)c.b_W.get(VV * sizeof(K));
     uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
     K* D = (K*)c.b_D.get(VV * sizeof(K));
+    bool wl_late = false;  // WL is being built on c.loss_stream (late loss): st waits ev_wl before reading it
     if constexpr (sizeof(K) == 4) {
         // packed (latency, loss) keys: one atomic pass, then a tiled symmetrize + split pass
         static_assert(T % 64 == 0, "tile");
         unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
         HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, st));
-        if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, KW, Vp);
+        wl_late = g.late && !g.late->applied;
+        if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, wl_late ? nullptr : g.loss, KW, Vp);
         const unsigned nb64 = (unsigned)(Vp / 64);
         k_w_split<<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, (uint32_t*)W, WL, (uint32_t*)D);
+        if (wl_late) {
+            // W is final: the loss side builds WL (min loss among the min-latency parallel
+            // edges, as k_w_split would) beside FW, which reads only D
+            // (queued by the loss helper thread after its last chunk)
+            hipStream_t ls = c.loss_stream;
+            HIP_CHECK(hipEventRecord(c.ev_build, st));
+            hipEvent_t ev_build = c.ev_build, ev_wl = c.ev_wl;
+            float* selfloss = P.selfloss;
+            const DevGraph gg = g;
+            const unsigned wl_grid = c.wl_grid ? (unsigned)c.wl_grid : 64u;
+            g.late->applied = true;
+            g.late->give([=]() {
+                HIP_CHECK(hipStreamWaitEvent(ls, ev_build, 0));
+                self_loss_done(gg, selfloss, ls);
+                // narrow grids: these run beside the FW tiles and should take few CU slots
+                k_fill<uint32_t><<<wl_grid, kThreads, 0, ls>>>(WL, VV, 0xFFFFFFFFu);
+                if (gg.E)
+                    k_w_loss<K><<<wl_grid, kThreads, 0, ls>>>(gg.E, gg.src, gg.dst, gg.lat, gg.loss, gg.directed, W,
+                                                              WL, Vp);
+                HIP_CHECK(hipGetLastError());
+                HIP_CHECK(hipEventRecord(ev_wl, ls));
+            });
+        }
     } else {
+        loss_arrive(g, P.selfloss, st);
         k_fill<K><<<grid_for(VV), kThreads, 0, st>>>(W, VV, KeyOps<K>::INF);
         HIP_CHECK(hipMemsetAsync(WL, 0xFF, VV * 4, st));
         if (g.E) {
@@ -1239,6 +1358,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     }
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
+    if (wl_late) {
+        g.late->join();
+        HIP_CHECK(hipStreamWaitEvent(st, c.ev_wl, 0));
+    }
     if (prof_n && stats) {
         double sum = 0;
         for (int i = 0; i < prof_n; ++i) {
@@ -2046,6 +2169,7 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     P.range_risk = bound >= ((unsigned __int128)1 << 62);
     const int G = c.comm ? c.comm->nranks : 1, rk = c.comm ? c.comm->rank : 0;
     if (choose_sparse(c, g) && P.es.max_lat < 0xFFFFFFFFull) {
+        loss_arrive(g, P.selfloss, st);
         if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
     }
     if (P.es.max_lat < 0xFFFFFFFFull) {
@@ -2067,6 +2191,7 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
 void direct_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
                    float* out_loss, hipStream_t st) {
     Prelude P = prelude(c, g, nodes, n, st, false);
+    loss_arrive(g, P.selfloss, st);
     if (n == 0) return;
     int32_t* pos = (int32_t*)c.b_pos.get((size_t)g.V * 4);
     uint32_t* cnt = (uint32_t*)c.b_cnt.get((size_t)n * n * 4);
@@ -2210,7 +2335,7 @@ __global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const 
 // the device.  Host threads narrow chunk i+1 into a page-locked ring while chunk i is in flight.
 // Returns false (nothing usable staged) when an endpoint >= 65536 or a latency >= 2^32 is seen:
 // the caller then ships the plain arrays, whose checks report such edges as the reference does.
-bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1);
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss);
 
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
@@ -2221,7 +2346,7 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
 
 // Ships edges [a0, a1) into the full-length device arrays (the rank's slice when the edge list
 // is sharded, else all of it).
-bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1) {
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss) {
     const size_t E = g->num_edges, A = a1 - a0;
     constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
     constexpr int NB = 3;                   // ring slots
@@ -2281,7 +2406,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
                 hd[i] = (uint16_t)y;
                 hl[i] = (uint32_t)l;
             }
-            std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
+            if (with_loss) std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
             if ((orx >> 16) || (orl >> 32)) bad.store(true, std::memory_order_relaxed);
         });
         const double dt = ms_since(tc);
@@ -2297,7 +2422,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
         HIP_CHECK(hipMemcpyAsync(s16 + e0, hs, ne * 2, hipMemcpyHostToDevice, st));
         HIP_CHECK(hipMemcpyAsync(d16 + e0, hd, ne * 2, hipMemcpyHostToDevice, st));
         HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
-        HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, hb, ne * 4, hipMemcpyHostToDevice, st));
+        if (with_loss) HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, hb, ne * 4, hipMemcpyHostToDevice, st));
         HIP_CHECK(hipEventRecord(c.ev_ring[b], st));
         k_widen_edges<<<grid_for(ne), kThreads, 0, st>>>(ne, s16 + e0, d16 + e0, l32 + e0, (uint32_t*)dg.src + e0,
                                                           (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
@@ -2307,7 +2432,8 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.src + r0, g->src + r0, rn * 4, hipMemcpyHostToDevice, st));
             HIP_CHECK(hipMemcpyAsync((uint32_t*)dg.dst + r0, g->dst + r0, rn * 4, hipMemcpyHostToDevice, st));
             HIP_CHECK(hipMemcpyAsync((uint64_t*)dg.lat + r0, g->latency_ns + r0, rn * 8, hipMemcpyHostToDevice, st));
-            HIP_CHECK(hipMemcpyAsync((float*)dg.loss + r0, g->packet_loss + r0, rn * 4, hipMemcpyHostToDevice, st));
+            if (with_loss)
+                HIP_CHECK(hipMemcpyAsync((float*)dg.loss + r0, g->packet_loss + r0, rn * 4, hipMemcpyHostToDevice, st));
             if (dbg) std::fprintf(stderr, "codec: host slow after chunk %zu (%.2f ms), rest plain\n", ch, dt);
             break;
         }
@@ -2315,6 +2441,50 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     if (dbg) std::fprintf(stderr, "codec: %zu chunks, %d threads, convert %.2f ms, slot waits %.2f ms\n", nch,
                           c.pool->size(), t_conv, t_wait);
     return true;
+}
+
+// Late loss H2D: a helper thread copies the losses chunk by chunk into a pinned ring and queues
+// each chunk's DMA on c.loss_stream behind the last endpoint/latency chunk (so the two never
+// share the PCIe link); loss_arrive() later joins it and orders the readers after the last DMA.
+void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, LateLoss& L) {
+    constexpr size_t CE = (size_t)2 << 20;
+    constexpr int NB = 3;
+    if (!c.h_lring) HIP_CHECK(hipHostMalloc(&c.h_lring, CE * 4 * NB, hipHostMallocDefault));
+    for (hipEvent_t* e : {&c.ev_lring[0], &c.ev_lring[1], &c.ev_lring[2], &c.ev_lin, &c.ev_ldone})
+        if (!*e) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    L.ev_in = c.ev_lin;
+    L.ev_done = c.ev_ldone;
+    HIP_CHECK(hipEventRecord(c.ev_ledges, st));
+    HIP_CHECK(hipStreamWaitEvent(c.loss_stream, c.ev_ledges, 0));
+    dg.late = &L;
+    const int device = c.device;
+    L.th = std::thread([&c, g, &dg, &L, device]() {
+        constexpr size_t CE = (size_t)2 << 20;  // losses per chunk (8 MB)
+        constexpr int NB = 3;
+        try {
+            HIP_CHECK(hipSetDevice(device));
+            const size_t E = g->num_edges;
+            float* dloss = const_cast<float*>(dg.loss);
+            for (size_t ch = 0, e0 = 0; e0 < E; ++ch, e0 += CE) {
+                const int b = (int)(ch % NB);
+                if (ch >= (size_t)NB) HIP_CHECK(hipEventSynchronize(c.ev_lring[b]));
+                const size_t ne = std::min(CE, E - e0);
+                float* slot = (float*)c.h_lring + (size_t)b * CE;
+                c.pool->run([&](int w, int nw) {
+                    const size_t a = ne * w / nw, z = ne * (w + 1) / nw;
+                    std::memcpy(slot + a, g->packet_loss + e0 + a, (z - a) * 4);
+                });
+                HIP_CHECK(hipMemcpyAsync(dloss + e0, slot, ne * 4, hipMemcpyHostToDevice, c.loss_stream));
+                HIP_CHECK(hipEventRecord(c.ev_lring[b], c.loss_stream));
+            }
+            HIP_CHECK(hipEventRecord(L.ev_in, c.loss_stream));
+            if (auto post = L.take()) post();
+        } catch (const Failure& f) {
+            L.err = f.msg;
+        } catch (const std::exception& e) {
+            L.err = e.what();
+        }
+    });
 }
 
 int guard(char* errbuf, size_t errlen, const std::function<void()>& body) {
@@ -2408,8 +2578,14 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         const bool shard = nr > 1 && (c->edge_shard == 1 || (c->edge_shard < 0 && nr >= 4));
         const size_t a0 = shard ? E * rk / nr : 0, a1 = shard ? E * (rk + 1) / nr : E;
         // narrowed edge list over PCIe when it fits (falls back to the plain arrays otherwise)
+        // late loss: the losses follow the endpoints and latencies on their own stream, beside
+        // the W build and FW (dense u32 path: WL is built from them on c->loss_stream)
+        const bool want_late = c->late_loss && !direct && !shard;
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) && g->num_vertices <= 65536 &&
-                           codec_in(*c, g, dg, st, a0, a1);
+                           codec_in(*c, g, dg, st, a0, a1, !want_late);
+        LateLoss late;
+        late.ls = c->loss_stream;
+        if (coded && want_late) start_late_loss(*c, g, dg, st, late);
         if (!coded) {
             const size_t cnt = std::max<size_t>(E, 1);
             dg.src = (uint32_t*)c->b_src.get(cnt * 4);
@@ -2484,6 +2660,10 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         c->own_row1 = ~(size_t)0;
         if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
         else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr);
+        if (dg.late) {  // a path that never read the losses (error-free early return): drain
+            dg.late->join();
+            HIP_CHECK(hipStreamSynchronize(c->loss_stream));
+        }
         // multi-rank without the output exchange: only this rank's rows leave the device
         const size_t r0 = std::min<size_t>(c->own_row0, n), r1 = std::min<size_t>(c->own_row1, n);
         const size_t rows_off = r1 > r0 ? r0 * n : 0, rows_nn = r1 > r0 ? (r1 - r0) * n : nn;
@@ -2542,7 +2722,12 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
         c->sdma.init(device);  // SDMA engine for the host entry's early D2H (else hipMemcpyAsync)
-        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e})
+        // the late-loss H2D and WL build share the D2H stream (idle until FW ends): a fifth
+        // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
+        // serialise the W build and FW behind the loss DMAs (measured: build 1.0 -> 3.6 ms)
+        c->loss_stream = c->d2h_stream;
+        if (const char* e = std::getenv("SRG_WL_GRID")) c->wl_grid = std::max(0, std::atoi(e));
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_build, &c->ev_wl, &c->ev_ledges})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     });
     if (rc != SRG_OK) {
@@ -2628,6 +2813,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SCAN_U64_LOW:
             if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->scan_u64_low = (int)value;
+            return SRG_OK;
+        case SRG_OPT_LATE_LOSS:
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            ctx->late_loss = (int)value;
             return SRG_OK;
         case SRG_OPT_EDGE_SHARD:
             if (value != 0 && value != 1 && value != -1) return SRG_ERR_ARG;

@@ -506,3 +506,39 @@ def test_c2_sampled_rows(router):
     assert np.array_equal(np.diag(t.latency_ns), e.latency_ns[:4096])
     off = ~np.eye(4096, dtype=bool)
     assert np.array_equal(t.latency_ns[off], t.latency_ns.T[off])
+
+
+@pytest.mark.parametrize("kind", ["dense", "parallel", "u64", "sparse"])
+def test_late_loss_matches_with_loss(router, kind):
+    """Host entry with SRG_OPT_LATE_LOSS (the losses cross PCIe after the endpoints/latencies,
+    beside the W build and FW; WL and the self-loop losses are built once they land) gives the
+    bytes of the in-line transfer, on the dense u32 path (WL on the loss stream), with parallel
+    edges (min loss among the min-latency ones), on the u64 rerun after a failed u32
+    certification, and on the sparse path; oracle rows pin them."""
+    V = 1500  # >= 2^20 edges: the codec (and so the late loss) is active
+    if kind == "dense" or kind == "sparse":
+        g = synth.atlas_like(V, seed=37)
+    elif kind == "parallel":
+        g = synth.random_graph(V, 0.9, 38, lat_lo=1, lat_hi=40, parallel=0.2)
+    else:  # latencies in [2^31, 2^32): u32 keys first, certification fails, u64 rerun
+        g = synth.random_graph(V, 0.95, 39, lat_lo=2 ** 31, lat_hi=2 ** 32 - 2)
+    assert g.num_edges >= 1 << 20
+    nodes = list(range(0, V, 3))
+    if kind == "sparse":
+        router.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_SPARSE)
+    out = {}
+    try:
+        for late in (0, 1):
+            router.set_option(N.SRG_OPT_LATE_LOSS, late)
+            out[late] = router.compute_shortest_paths(g, nodes)
+    finally:
+        router.set_option(N.SRG_OPT_LATE_LOSS, 1)
+        router.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_AUTO)
+    want = {"dense": N.SRG_PATH_DENSE_U32, "parallel": N.SRG_PATH_DENSE_U32, "u64": N.SRG_PATH_DENSE_U64,
+            "sparse": N.SRG_PATH_SPARSE_U32}[kind]
+    assert out[1].stats["path_kind"] == want
+    assert np.array_equal(out[0].latency_ns, out[1].latency_ns)
+    assert bits_equal(out[0].packet_loss, out[1].packet_loss)
+    rows = [0, 1, len(nodes) - 1]
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
+    assert np.array_equal(out[1].latency_ns[rows], lat) and bits_equal(out[1].packet_loss[rows], loss)
