@@ -1505,8 +1505,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // pair-lane LDS scans (9x: timing experiments); u64 keys run variant 5 on the keys' low words
     // (tight_sparse.hip.h: exact together with the loss pass's multi-predecessor check)
     const bool v5lo = sizeof(K) == 8 && c.scan_u64_low;
-    const bool v5 = (sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 9) || c.scan_variant >= 91)) || v5lo;
-    const size_t npad = v5 ? ((size_t)nloc + 127) / 128 * 128 : ((size_t)nloc + 63) / 64 * 64;
+    const bool v5 = (sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 10) || c.scan_variant >= 91)) || v5lo;
+    const bool v10 = v5 && c.scan_variant == 10;  // four sources per lane: 256-source blocks
+    const uint32_t SB = v10 ? V10_SB : V5_SB;
+    const size_t npad = v5 ? ((size_t)nloc + SB - 1) / SB * SB : ((size_t)nloc + 63) / 64 * 64;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;  // == nbT * TB targets
     // LDS-staged scan (SRG_OPT_SCAN_VARIANT 3, default): entries by (target tile, u-chunk, target)
@@ -1671,7 +1673,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             const uint32_t inf_check = v5lo ? 0u : 1u;
             if (v5) {
                 {
-                    const uint32_t nbS5 = (uint32_t)(npad / V5_SB);
+                    const uint32_t nbS5 = (uint32_t)(npad / SB);
+                    if (v10) set_lds(tight_v10, 2 * V5_UC * V10_SB * 4);
                     auto scan5 = v5lo ? tight_v5
                                  : c.scan_variant == 6 ? tight_v6 : c.scan_variant == 7 ? tight_v7<0> : c.scan_variant == 8 ? tight_v7<1>
                                  : c.scan_variant == 91 ? tight_v7<0, 1> : c.scan_variant == 92 ? tight_v7<0, 2> : tight_v5;
@@ -1685,7 +1688,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                         auto cut = [&](uint32_t q) { return q == ng ? nbS5 : std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8); };
                         const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                         if (c1 == c0) continue;
-                        if (c.scan_variant == 9 && !v5lo)
+                        if (v10)
+                            tight_v10<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 2 * V5_UC * V10_SB * 4, st>>>(
+                                DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
+                                v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
+                        else if (c.scan_variant == 9 && !v5lo)
                             tight_v9<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
                                 DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
                                 v5_goff, (const uint32_t*)c.b_entkey.get(0), v5_cnt, PRED, Vp, inf_check);
@@ -1695,7 +1702,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                                 v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
                         HIP_CHECK(hipGetLastError());
                         if (interleave) {
-                            const uint32_t r0 = c0 * V5_SB, r1 = std::min<uint32_t>(c1 * V5_SB, nloc);
+                            const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);
                             if (r1 <= r0) continue;
                             k_loss_rows<K><<<r1 - r0, 1024, lds_rows, st>>>(
                                 PRED, Vp, V, lnodes, nloc, ent_u, ent_b, ent_w, DST, npad, cscoff, cscent, P.selfloss,
@@ -2777,7 +2784,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (!((value >= 0 && value <= 9) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
+            if (!((value >= 0 && value <= 10) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:

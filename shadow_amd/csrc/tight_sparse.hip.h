@@ -1539,6 +1539,132 @@ __global__ void __launch_bounds__(512, 4) tight_v9(const uint32_t* __restrict__ 
     }
 }
 
+// Variant 10: variant 5 with FOUR sources per lane (256 per workgroup).  v5's time goes to the
+// per-pair instruction chain (record -> target index -> -d -> adds -> min -> compare -> branch),
+// whose cost does not depend on how many sources a lane checks; here one ds_read_b128 of the
+// staged 1-KB row feeds four sources, so each pair's chain is paid for 8 checks per lane instead
+// of 4, and the records are streamed once per 256 sources instead of per 128.  Same records as
+// v5 (the row offset lo = (u - u0) * 512 is doubled for the 1-KB rows); the u-chunk ring is 2 x
+// 64 KB (one workgroup per CU, 2 waves per SIMD).
+constexpr uint32_t V10_SB = 256;  // sources per workgroup (4 per lane)
+typedef uint32_t v16u_v10 __attribute__((ext_vector_type(16)));
+__global__ void __launch_bounds__(512) tight_v10(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+                                                  const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                  uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
+                                                  const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
+                                                  uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rows10[];  // 2 x V5_UC x V10_SB (128 KB)
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r0 = c * V10_SB + 4 * lane;  // this lane's four sources (columns of DST)
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t t0 = b * V5_TT + wave * V5_TW;
+    const bool active = t0 < NT;  // a wave past the targets still stages and syncs
+    v16u_v10 nd0, nd1, nd2, nd3, s0, s1, s2, s3;
+#pragma unroll
+    for (uint32_t j = 0; j < V5_TW; ++j) {
+        uint32_t d[4] = {0, 0, 0, 0};
+        if (active) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((t0 + j) * (uint32_t)npad + r0) * 4u, 0, 0);
+            d[0] = v[0];
+            d[1] = v[1];
+            d[2] = v[2];
+            d[3] = v[3];
+        }
+        nd0[j] = 0u - d[0];
+        nd1[j] = 0u - d[1];
+        nd2[j] = 0u - d[2];
+        nd3[j] = 0u - d[3];
+        s0[j] = s1[j] = s2[j] = s3[j] = PRED_NONE;
+    }
+    // staging by LDS-DMA (no staging registers: the -d and state vectors need them): each wave
+    // loads 8 of the chunk's 64 rows, one 1-KB row per instruction (16 B per lane)
+    auto stage = [&](uint32_t k, uint32_t buf) {
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t u = k * V5_UC + wave + 8 * i;  // rows >= V are never referenced by a record
+            const uint32_t* src = DST + (size_t)min(u, V - 1) * npad + c * V10_SB + lane * 4;
+            __builtin_amdgcn_global_load_lds(src, &rows10[buf * (V5_UC * V10_SB) + (wave + 8 * i) * V10_SB], 16, 0, 0);
+        }
+    };
+    stage(0, 0);
+    __syncthreads();  // drains the DMAs (vmcnt) and publishes the rows
+    const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows10);
+    for (uint32_t k = 0; k < nK; ++k) {
+        // the slice bounds are loaded before the next chunk's DMAs are issued, so waiting for
+        // them (vmcnt is in order) does not wait for the DMAs
+        const size_t q = ((size_t)b * nK + k) * V5_WAVES + wave;
+        const uint32_t g0 = goff[q], g1 = goff[q + 1];
+        if (k + 1 < nK) stage(k + 1, (k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
+        if (active) {
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane(g0);
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane(g1);
+            const uint32_t vb = (k & 1u) * (V5_UC * V10_SB * 4u) + lane * 16u;
+            if (p0 < p1) {
+                V5Grp cur = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)p0);
+                for (uint32_t p = p0; p < p1; p += 4) {
+                    const V5Grp nxt = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p + 4));
+                    uint4 A[8];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        A[2 * i] = *reinterpret_cast<const uint4*>(lds + vb + 2u * (cur.v[4 * i] & 0xFFFFu));
+                        A[2 * i + 1] = *reinterpret_cast<const uint4*>(lds + vb + 2u * cur.v[4 * i + 2]);
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        const uint32_t tl = cur.v[4 * i] >> 16;
+                        const uint32_t d0 = nd0[tl], d1 = nd1[tl], d2 = nd2[tl], d3 = nd3[tl];
+                        const uint32_t w0 = cur.v[4 * i + 1], w1 = cur.v[4 * i + 3];
+                        const uint4 a = A[2 * i], e = A[2 * i + 1];
+                        const uint32_t x00 = a.x + w0 + d0, x01 = a.y + w0 + d1, x02 = a.z + w0 + d2, x03 = a.w + w0 + d3;
+                        const uint32_t x10 = e.x + w1 + d0, x11 = e.y + w1 + d1, x12 = e.z + w1 + d2, x13 = e.w + w1 + d3;
+                        const uint32_t m = min(min(min(x00, x01), min(x02, x03)), min(min(x10, x11), min(x12, x13)));
+                        if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
+                            const uint32_t e0 = 2 * (p + i);
+                            uint32_t q0 = s0[tl], q1 = s1[tl], q2 = s2[tl], q3 = s3[tl];
+                            if (x00 == 0) q0 = (q0 == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (x10 == 0) q0 = (q0 == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            if (x01 == 0) q1 = (q1 == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (x11 == 0) q1 = (q1 == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            if (x02 == 0) q2 = (q2 == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (x12 == 0) q2 = (q2 == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            if (x03 == 0) q3 = (q3 == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (x13 == 0) q3 = (q3 == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            s0[tl] = q0;
+                            s1[tl] = q1;
+                            s2[tl] = q2;
+                            s3[tl] = q3;
+                        }
+                    }
+                    cur = nxt;
+                }
+            }
+        }
+        if (k + 1 < nK) __syncthreads();  // drains chunk k + 1's DMAs and orders the buffers
+    }
+    if (!active) return;
+#pragma unroll
+    for (uint32_t h = 0; h < 4; ++h) {
+        const uint32_t r = r0 + h;
+        if (r >= n) continue;
+        const uint32_t s = nodes[r];
+        uint32_t o[V5_TW];
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; ++j) {
+            const uint32_t t = t0 + j;
+            const uint32_t nd = h == 0 ? nd0[j] : h == 1 ? nd1[j] : h == 2 ? nd2[j] : nd3[j];
+            const uint32_t st = h == 0 ? s0[j] : h == 1 ? s1[j] : h == 2 ? s2[j] : s3[j];
+            o[j] = (t >= V || t == s || (inf_check && nd == 0u - KeyOps<uint32_t>::INF)) ? PRED_NONE : st;
+        }
+        uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; j += 4) out[j / 4] = make_uint4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,
