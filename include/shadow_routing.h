@@ -143,7 +143,8 @@ void srg_destroy(srg_ctx* ctx);
                                      lane over LDS-staged rows (v_readlane / s_load entry reads); 2 = entries
                                      grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches
                                      broadcast with v_readlane; 10 = four sources per lane (ds_read_b128
-                                     of 1-KB rows, 256-source workgroups; measured slower) */
+                                     of 1-KB rows, 256-source workgroups; measured slower); 11 = variant 5
+                                     with one hit test per 4-pair group (measured the same) */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) / 16 (one workgroup per CU) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;

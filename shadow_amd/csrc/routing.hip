@@ -1505,7 +1505,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // pair-lane LDS scans (9x: timing experiments); u64 keys run variant 5 on the keys' low words
     // (tight_sparse.hip.h: exact together with the loss pass's multi-predecessor check)
     const bool v5lo = sizeof(K) == 8 && c.scan_u64_low;
-    const bool v5 = (sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 10) || c.scan_variant >= 91)) || v5lo;
+    const bool v5 = (sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 11) || c.scan_variant >= 91)) || v5lo;
     const bool v10 = v5 && c.scan_variant == 10;  // four sources per lane: 256-source blocks
     const uint32_t SB = v10 ? V10_SB : V5_SB;
     const size_t npad = v5 ? ((size_t)nloc + SB - 1) / SB * SB : ((size_t)nloc + 63) / 64 * 64;
@@ -1677,7 +1677,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                     if (v10) set_lds(tight_v10, 2 * V5_UC * V10_SB * 4);
                     auto scan5 = v5lo ? tight_v5
                                  : c.scan_variant == 6 ? tight_v6 : c.scan_variant == 7 ? tight_v7<0> : c.scan_variant == 8 ? tight_v7<1>
-                                 : c.scan_variant == 91 ? tight_v7<0, 1> : c.scan_variant == 92 ? tight_v7<0, 2> : tight_v5;
+                                 : c.scan_variant == 91 ? tight_v7<0, 1> : c.scan_variant == 92 ? tight_v7<0, 2>
+                                 : c.scan_variant == 11 ? tight_v11 : tight_v5;
                     // host entry: the scan runs in source-block groups, each group's loss rows folded
                     // right after it and shipped while later groups scan (loss rows on a second
                     // stream beside the next group's scan were starved of CUs: 24.7 ms vs 20.8)
@@ -2784,7 +2785,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_packed = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_VARIANT:
-            if (!((value >= 0 && value <= 10) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
+            if (!((value >= 0 && value <= 11) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
             ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:

@@ -1082,6 +1082,134 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
     }
 }
 
+// Variant 11: variant 5 with one hit test per 4-pair group.  v5's ISA checks each pair with its
+// own v_cmp -> vcc -> s_cbranch (a VALU -> SALU round trip per pair that serialises the four
+// independent pairs of a group); here the four pairs' slacks are computed first and one ballot
+// of their min guards the (per-pair) state updates.
+__global__ void __launch_bounds__(512, 4) tight_v11(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+                                                    const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
+                                                    uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
+                                                    const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
+                                                    uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
+    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t r0 = c * V5_SB + 2 * lane;  // this lane's two sources (columns of DST)
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(DST, dst_bytes);
+    const uint32_t t0 = b * V5_TT + wave * V5_TW;
+    const bool active = t0 < NT;  // a wave past the targets still stages and syncs
+    v16u_v5 ndl, ndh, stl, sth;
+#pragma unroll
+    for (uint32_t j = 0; j < V5_TW; ++j) {
+        uint32_t dl = 0, dh = 0;
+        if (active) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ((t0 + j) * (uint32_t)npad + r0) * 4u, 0, 0);
+            dl = v[0];
+            dh = v[1];
+        }
+        ndl[j] = 0u - dl;
+        ndh[j] = 0u - dh;
+        stl[j] = PRED_NONE;
+        sth[j] = PRED_NONE;
+    }
+    // staging: 512 threads x 16 B = 16 rows per pass, 4 passes per 64-row chunk
+    const uint32_t srow = tid >> 5, scol = (tid & 31) * 4;
+    uint4 sv[4];
+    auto stage_load = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t u = k * V5_UC + srow + 16 * i;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (u * (uint32_t)npad + c * V5_SB + scol) * 4u, 0, 0);
+            sv[i] = make_uint4(v[0], v[1], v[2], v[3]);  // rows past DST read 0 (range-checked)
+        }
+    };
+    auto stage_store = [&](uint32_t buf) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4*>(&rows[buf * (V5_UC * V5_SB) + (srow + 16 * i) * V5_SB + scol]) = sv[i];
+    };
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows);
+    for (uint32_t k = 0; k < nK; ++k) {
+        if (k + 1 < nK) stage_load(k + 1);  // issue early, write after the chunk
+        if (active) {
+            const size_t q = ((size_t)b * nK + k) * V5_WAVES + wave;
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q]);
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q + 1]);
+            const uint32_t vb = (k & 1u) * (V5_UC * V5_SB * 4u) + lane * 8u;
+            if (p0 < p1) {
+                V5Grp cur = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)p0);
+                for (uint32_t p = p0; p < p1; p += 4) {
+                    const V5Grp nxt = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p + 4));
+                    uint2 A[8];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        A[2 * i] = *reinterpret_cast<const uint2*>(lds + vb + (cur.v[4 * i] & 0xFFFFu));
+                        A[2 * i + 1] = *reinterpret_cast<const uint2*>(lds + vb + cur.v[4 * i + 2]);
+                    }
+                    // all four pairs' slacks first (independent chains), one hit test per group
+                    uint32_t X[4][4], mg = 0xFFFFFFFFu;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        const uint32_t tl = cur.v[4 * i] >> 16;
+                        const uint32_t dl = ndl[tl], dh = ndh[tl];
+                        const uint32_t w0 = cur.v[4 * i + 1], w1 = cur.v[4 * i + 3];
+                        X[i][0] = A[2 * i].x + w0 + dl;
+                        X[i][1] = A[2 * i].y + w0 + dh;
+                        X[i][2] = A[2 * i + 1].x + w1 + dl;
+                        X[i][3] = A[2 * i + 1].y + w1 + dh;
+                        mg = min(mg, min(min(X[i][0], X[i][1]), min(X[i][2], X[i][3])));
+                    }
+                    if (__builtin_expect(__ballot(mg == 0) != 0, 0)) {
+#pragma unroll
+                        for (uint32_t i = 0; i < 4; ++i) {
+                            const uint32_t m = min(min(X[i][0], X[i][1]), min(X[i][2], X[i][3]));
+                            if (__ballot(m == 0) == 0) continue;
+                            const uint32_t tl = cur.v[4 * i] >> 16;
+                            const uint32_t e0 = 2 * (p + i);
+                            uint32_t sl = stl[tl], sh = sth[tl];
+                            if (X[i][0] == 0) sl = (sl == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (X[i][2] == 0) sl = (sl == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            if (X[i][1] == 0) sh = (sh == PRED_NONE) ? e0 : PRED_MULTI;
+                            if (X[i][3] == 0) sh = (sh == PRED_NONE) ? e0 + 1 : PRED_MULTI;
+                            stl[tl] = sl;
+                            sth[tl] = sh;
+                        }
+                    }
+                    cur = nxt;
+                }
+            }
+        }
+        if (k + 1 < nK) {
+            stage_store((k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
+            __syncthreads();
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t r = r0 + h;
+        if (r >= n) continue;
+        const uint32_t s = nodes[r];
+        uint32_t o[V5_TW];
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; ++j) {
+            const uint32_t t = t0 + j;
+            const uint32_t nd = h ? ndh[j] : ndl[j];
+            const uint32_t st = h ? sth[j] : stl[j];
+            o[j] = (t >= V || t == s || (inf_check && nd == 0u - KeyOps<uint32_t>::INF)) ? PRED_NONE : st;
+        }
+        uint4* out = reinterpret_cast<uint4*>(PRED + (size_t)r * ldp + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < V5_TW; j += 4) out[j / 4] = make_uint4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+}
+
 // Variant 6: variant 5 with the record stream in VECTOR registers.  v5's 4-pair s_load groups
 // cost one scalar-cache round trip per group that no other work covers (the s_waitcnt for a
 // scalar load also drains every LDS read): 58 % of its wave cycles were waits

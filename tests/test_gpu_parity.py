@@ -110,7 +110,7 @@ def test_fw_kernels_match_oracle(router, packed, kw):
     r.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 def test_scan_variants_match_oracle(variant):
     """All u32 tight-scan kernels: vector entry batches + readlane, scalar entry loads, target runs
     (the default), LDS-staged u-chunks (one or two sources per lane)."""
@@ -157,7 +157,7 @@ def test_fw_symmetric_matches_general(V):
         assert_parity(out[1], lat, loss)
 
 
-@pytest.mark.parametrize("variant", [2, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [2, 5, 6, 7, 8, 9, 10, 11])
 def test_scan_variants_ragged_sources(variant):
     """Several 128-source blocks, target tiles and u-chunks, with n and V off every block size and
     a used-node subset in random order (lanes past n, targets past V, sentinel pairs)."""
@@ -179,7 +179,7 @@ def test_scan_v5_equals_v2_full_c3():
     g = synth.atlas_like(10000, seed=10000)
     nodes = np.arange(10000, dtype=np.uint32)
     out = []
-    for v in (2, 5, 6, 9, 10):
+    for v in (2, 5, 6, 9, 10, 11):
         r = Router(0)
         r.set_option(N.SRG_OPT_SCAN_VARIANT, v)
         t = r.compute_shortest_paths(g, nodes)
