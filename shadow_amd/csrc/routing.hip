@@ -219,6 +219,8 @@ __global__ void k_w_key(uint64_t E, const uint32_t* __restrict__ src, const uint
 // 64x64 tiles: (undirected) KW = min(KW, KW^T), then split into W (latency), WL (loss bits)
 // and D (= W with a zero diagonal).  grid = (nb64, nb64) over the upper triangle incl. diagonal
 // blocks when undirected (each block pair handled once), all blocks when directed.
+// WL_ONLY: only WL is written (late loss: W and D were split from latency-only keys before FW)
+template <bool WL_ONLY = false>
 __global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __restrict__ KW, size_t ld, int directed,
                                                  uint32_t* __restrict__ W, uint32_t* __restrict__ WL,
                                                  uint32_t* __restrict__ D) {
@@ -235,9 +237,11 @@ __global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __res
         unsigned long long k = KW[i * ld + j];
         if (!directed) k = min(k, tb[tx][r]);
         const uint32_t w = min((uint32_t)(k >> 32), KeyOps<uint32_t>::INF);  // no edge / >= INF -> INF
-        W[i * ld + j] = w;
         WL[i * ld + j] = (uint32_t)k;
-        D[i * ld + j] = i == j ? 0u : w;
+        if (!WL_ONLY) {
+            W[i * ld + j] = w;
+            D[i * ld + j] = i == j ? 0u : w;
+        }
         if (!directed && bi != bj) tb[tx][r] = k;  // the mirrored element, written below
     }
     if (!directed && bi != bj) {
@@ -246,9 +250,11 @@ __global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __res
             const size_t i = bj * 64 + r, j = bi * 64 + tx;
             const unsigned long long k = tb[r][tx];
             const uint32_t w = min((uint32_t)(k >> 32), KeyOps<uint32_t>::INF);
-            W[i * ld + j] = w;
             WL[i * ld + j] = (uint32_t)k;
-            D[i * ld + j] = w;
+            if (!WL_ONLY) {
+                W[i * ld + j] = w;
+                D[i * ld + j] = w;
+            }
         }
     }
 }
@@ -557,9 +563,8 @@ struct srg_ctx {
     int scan_u64_low = 1;            // u64 keys: pair-lane scan on the keys' low words (SRG_OPT_SCAN_U64_LOW; 0 = generic u64 scan)
     DevBuf b_DST2;                   // its low-word DST
     int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
-    int wl_grid = 0;                 // its WL build's workgroups (0 = 64; env SRG_WL_GRID, experiments)
     hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
-    hipEvent_t ev_build = nullptr, ev_wl = nullptr, ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr;
+    hipEvent_t ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr;
     void* h_lring = nullptr;         // pinned ring of the late loss H2D
     hipEvent_t ev_lring[3] = {nullptr, nullptr, nullptr};
     int edge_shard = -1;             // host entry, multi-rank: ship 1/N of the edges, allgatherv the rest (SRG_OPT_EDGE_SHARD)
@@ -603,7 +608,7 @@ struct srg_ctx {
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_build, ev_wl, ev_ledges, ev_lin, ev_ldone})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
             if (e) (void)hipEventDestroy(e);
@@ -631,43 +636,14 @@ struct LateLoss {
     hipEvent_t ev_done = nullptr;  // the losses and the self-loop losses are on the device
     bool joined = false, applied = false;
     std::string err;
-    // Work that `th` queues on `ls` after the last chunk (the main thread must not block on the
-    // ring while it launches FW): handed over once by give(), or nothing when join() comes first.
-    std::mutex mu;
-    std::condition_variable cv;
-    std::function<void()> post;
-    bool post_set = false;
-    void give(std::function<void()> f) {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            post = std::move(f);
-            post_set = true;
-        }
-        cv.notify_all();
-    }
-    std::function<void()> take() {  // called by `th`
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return post_set; });
-        return post;
-    }
     void join() {
         if (!joined) {
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                post_set = true;  // no work handed over: release the helper
-            }
-            cv.notify_all();
             if (th.joinable()) th.join();
             joined = true;
         }
         if (!err.empty()) fail(SRG_ERR_HIP, "loss H2D: " + err);
     }
     ~LateLoss() {  // no DMA into the ring or the device losses may outlive the call
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            post_set = true;
-        }
-        cv.notify_all();
         if (th.joinable()) th.join();
         if (ls) (void)hipStreamSynchronize(ls);
     }
@@ -686,21 +662,16 @@ struct DevGraph {
     LateLoss* late = nullptr;   // non-null: `loss` is still in flight (loss_arrive before reading it)
 };
 
-// the self-loop losses, then ev_done, on stream s (after the loss chunks)
-void self_loss_done(const DevGraph& g, float* self_loss, hipStream_t s) {
-    if (g.E) k_self_loss<<<grid_for(g.E), kThreads, 0, s>>>(g.E, g.src, g.dst, g.loss, g.V, self_loss);
-    HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(g.late->ev_done, s));
-}
-
 // Make `s` wait until g.loss (and the self-loop losses) are on the device.
 void loss_arrive(const DevGraph& g, float* self_loss, hipStream_t s) {
     LateLoss* L = g.late;
     if (!L) return;
-    L->join();  // every command of the helper is queued (ev_in / ev_done recorded)
+    L->join();  // every loss chunk is queued and ev_in recorded
     if (!L->applied) {
         HIP_CHECK(hipStreamWaitEvent(s, L->ev_in, 0));
-        self_loss_done(g, self_loss, s);
+        if (g.E) k_self_loss<<<grid_for(g.E), kThreads, 0, s>>>(g.E, g.src, g.dst, g.loss, g.V, self_loss);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(L->ev_done, s));
         L->applied = true;
     } else {
         HIP_CHECK(hipStreamWaitEvent(s, L->ev_done, 0));
@@ -1281,7 +1252,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     K* W = (K*)c.b_W.get(VV * sizeof(K));
     uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
     K* D = (K*)c.b_D.get(VV * sizeof(K));
-    bool wl_late = false;  // WL is being built on c.loss_stream (late loss): st waits ev_wl before reading it
+    bool wl_late = false;  // late loss: WL is built after FW, once the losses have landed
     if constexpr (sizeof(K) == 4) {
         // packed (latency, loss) keys: one atomic pass, then a tiled symmetrize + split pass
         static_assert(T % 64 == 0, "tile");
@@ -1290,30 +1261,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         wl_late = g.late && !g.late->applied;
         if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, wl_late ? nullptr : g.loss, KW, Vp);
         const unsigned nb64 = (unsigned)(Vp / 64);
-        k_w_split<<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, (uint32_t*)W, WL, (uint32_t*)D);
-        if (wl_late) {
-            // W is final: the loss side builds WL (min loss among the min-latency parallel
-            // edges, as k_w_split would) beside FW, which reads only D
-            // (queued by the loss helper thread after its last chunk)
-            hipStream_t ls = c.loss_stream;
-            HIP_CHECK(hipEventRecord(c.ev_build, st));
-            hipEvent_t ev_build = c.ev_build, ev_wl = c.ev_wl;
-            float* selfloss = P.selfloss;
-            const DevGraph gg = g;
-            const unsigned wl_grid = c.wl_grid ? (unsigned)c.wl_grid : 64u;
-            g.late->applied = true;
-            g.late->give([=]() {
-                HIP_CHECK(hipStreamWaitEvent(ls, ev_build, 0));
-                self_loss_done(gg, selfloss, ls);
-                // narrow grids: these run beside the FW tiles and should take few CU slots
-                k_fill<uint32_t><<<wl_grid, kThreads, 0, ls>>>(WL, VV, 0xFFFFFFFFu);
-                if (gg.E)
-                    k_w_loss<K><<<wl_grid, kThreads, 0, ls>>>(gg.E, gg.src, gg.dst, gg.lat, gg.loss, gg.directed, W,
-                                                              WL, Vp);
-                HIP_CHECK(hipGetLastError());
-                HIP_CHECK(hipEventRecord(ev_wl, ls));
-            });
-        }
+        k_w_split<false><<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, (uint32_t*)W, WL, (uint32_t*)D);
     } else {
         loss_arrive(g, P.selfloss, st);
         k_fill<K><<<grid_for(VV), kThreads, 0, st>>>(W, VV, KeyOps<K>::INF);
@@ -1359,8 +1307,21 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
     if (wl_late) {
-        g.late->join();
-        HIP_CHECK(hipStreamWaitEvent(st, c.ev_wl, 0));
+        // WL = min loss among the min-latency parallel edges (what k_w_split gives), from the
+        // losses that crossed PCIe during FW.  Built here, after FW, rather than beside it: on a
+        // narrow grid beside the FW tiles it cost the bulk launches 5 % (0.242 -> 0.255 ms,
+        // FW +0.8 ms, profiles/r02g) for about the same total.
+        // The packed-key pass again, now with the losses (its buffer is free until the scan
+        // writes PRED), splitting out WL only: 0.8 ms where k_w_loss's random W reads took 2.3.
+        loss_arrive(g, P.selfloss, st);
+        if constexpr (sizeof(K) == 4) {
+            unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
+            HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, st));
+            if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, KW, Vp);
+            const unsigned nb64 = (unsigned)(Vp / 64);
+            k_w_split<true><<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, nullptr, WL, nullptr);
+            HIP_CHECK(hipGetLastError());
+        }
     }
     if (prof_n && stats) {
         double sum = 0;
@@ -2486,7 +2447,6 @@ void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream
                 HIP_CHECK(hipEventRecord(c.ev_lring[b], c.loss_stream));
             }
             HIP_CHECK(hipEventRecord(L.ev_in, c.loss_stream));
-            if (auto post = L.take()) post();
         } catch (const Failure& f) {
             L.err = f.msg;
         } catch (const std::exception& e) {
@@ -2734,8 +2694,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
         // serialise the W build and FW behind the loss DMAs (measured: build 1.0 -> 3.6 ms)
         c->loss_stream = c->d2h_stream;
-        if (const char* e = std::getenv("SRG_WL_GRID")) c->wl_grid = std::max(0, std::atoi(e));
-        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_build, &c->ev_wl, &c->ev_ledges})
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     });
     if (rc != SRG_OK) {
