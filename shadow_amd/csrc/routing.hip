@@ -564,7 +564,7 @@ struct srg_ctx {
     DevBuf b_DST2;                   // its low-word DST
     int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
     hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
-    hipEvent_t ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr;
+    hipEvent_t ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr, ev_wlate = nullptr;
     void* h_lring = nullptr;         // pinned ring of the late loss H2D
     hipEvent_t ev_lring[3] = {nullptr, nullptr, nullptr};
     int edge_shard = -1;             // host entry, multi-rank: ship 1/N of the edges, allgatherv the rest (SRG_OPT_EDGE_SHARD)
@@ -608,7 +608,7 @@ struct srg_ctx {
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
             if (e) (void)hipEventDestroy(e);
@@ -1313,15 +1313,19 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         // FW +0.8 ms, profiles/r02g) for about the same total.
         // The packed-key pass again, now with the losses (its buffer is free until the scan
         // writes PRED), splitting out WL only: 0.8 ms where k_w_loss's random W reads took 2.3.
-        loss_arrive(g, P.selfloss, st);
+        // It runs on the (idle) FW lookahead stream beside the certification, extract and
+        // essential-entry count, which read W and D only; st waits for it before the entry fill.
+        hipStream_t ax = c.aux_stream;  // st is synchronised (tm.lap): FW is complete
+        loss_arrive(g, P.selfloss, ax);
         if constexpr (sizeof(K) == 4) {
             unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
-            HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, st));
-            if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, KW, Vp);
+            HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, ax));
+            if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, ax>>>(g.E, g.src, g.dst, g.lat, g.loss, KW, Vp);
             const unsigned nb64 = (unsigned)(Vp / 64);
-            k_w_split<true><<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, nullptr, WL, nullptr);
+            k_w_split<true><<<dim3(nb64, nb64), 256, 0, ax>>>(KW, Vp, g.directed, nullptr, WL, nullptr);
             HIP_CHECK(hipGetLastError());
         }
+        HIP_CHECK(hipEventRecord(c.ev_wlate, ax));
     }
     if (prof_n && stats) {
         double sum = 0;
@@ -1398,7 +1402,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         // a used pair at INF: unreachable -- unless some path could reach 2^31-1 ns, in which case
         // the u64 keys decide (the u32 FW work is redone)
         const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (V > 1 ? V - 1 : 1);
-        if (bound >= KeyOps<uint32_t>::INF) return false;
+        if (bound >= KeyOps<uint32_t>::INF) {
+            if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));  // the u64 rerun rewrites WL
+            return false;
+        }
         fail(SRG_ERR_UNREACHABLE,
              "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
              "from another used node)");
@@ -1570,6 +1577,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         }
     }
     n_ess = E_ess;
+    if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));  // WL (late loss) before the entry fill
     const bool sparse = (double)E_ess <= c.sparse_threshold * (double)V * (double)V &&
                         E_layout + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
     if (sparse) {
@@ -2125,6 +2133,7 @@ bool choose_sparse(const srg_ctx& c, const DevGraph& g) {
 
 void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
                     float* out_loss, hipStream_t st, srg_stats* stats, HostSink* sink = nullptr) {
+    HIP_CHECK(hipStreamSynchronize(c.aux_stream));  // nothing of an aborted call still writes WL / PRED
     if (g.V == 0) {
         if (n) fail(SRG_ERR_ARG, "nodes given for an empty graph");
         return;
@@ -2694,7 +2703,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
         // serialise the W build and FW behind the loss DMAs (measured: build 1.0 -> 3.6 ms)
         c->loss_stream = c->d2h_stream;
-        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges})
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     });
     if (rc != SRG_OK) {
