@@ -532,6 +532,9 @@ def main():
                        "parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single",
                        **({"output": "row-distributed (each rank holds its sources' rows)" if not args.gather
                            else "gathered (every rank holds the whole table)"} if strong else {}),
+                       **({"edge_list": "sharded (1/N over each PCIe link, exchanged between GPUs)"
+                           if (args.edge_shard == 1 or (args.edge_shard in (None, -1) and world >= 4))
+                           else "whole list over each PCIe link"} if strong and args.entry == "host" else {}),
                        **({"fallback": fallback} if fallback else {}),
                        "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
             "apsp_wall_ms": round(ms_per_step, 3),
