@@ -1651,11 +1651,34 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                     // host entry: the scan runs in source-block groups, each group's loss rows folded
                     // right after it and shipped while later groups scan (loss rows on a second
                     // stream beside the next group's scan were starved of CUs: 24.7 ms vs 20.8)
-                    const uint32_t ng = interleave ? std::min<uint32_t>(scan_groups, nbS5) : 1u;
+                    uint32_t ng = interleave ? std::min<uint32_t>(scan_groups, nbS5) : 1u;
+                    // experiments: explicit group bounds in source blocks ("24,56"), env SRG_SCAN_CUTS
+                    std::vector<uint32_t> cuts_env;
+                    if (const char* e = interleave ? std::getenv("SRG_SCAN_CUTS") : nullptr) {
+                        for (const char* q = e; *q;) {
+                            char* end = nullptr;
+                            const unsigned long x = std::strtoul(q, &end, 10);
+                            if (end == q) break;
+                            if (x > 0 && x < nbS5 && (cuts_env.empty() || x > cuts_env.back())) cuts_env.push_back((uint32_t)x);
+                            q = *end ? end + 1 : end;
+                        }
+                        if (!cuts_env.empty()) ng = (uint32_t)cuts_env.size() + 1;
+                    }
                     for (uint32_t gi = 0; gi < ng; ++gi) {
                         // group bounds on multiples of 8 source blocks: every XCD gets the same
                         // number of blocks per launch (20 blocks = 3/3/3/3/2/2/2/2 ran 33 % long)
-                        auto cut = [&](uint32_t q) { return q == ng ? nbS5 : std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8); };
+                        auto cut = [&](uint32_t q) {
+                            if (q == 0) return 0u;
+                            if (q == ng) return nbS5;
+                            if (!cuts_env.empty()) return cuts_env[q - 1];
+                            // three groups: half, then all but the last partial 8 blocks, so the
+                            // loss rows left to ship after the last fold are few (C3 40 / 32 / 7
+                            // blocks: exposed D2H 1.8 -> 0.8 ms, scan + tail -0.6 ms vs thirds,
+                            // profiles/r02i/scan_cuts.txt)
+                            const uint32_t half = std::min(nbS5, (nbS5 / 2 + 4) / 8 * 8), last = (nbS5 - 1) / 8 * 8;
+                            if (ng == 3 && half > 0 && last > half) return q == 1 ? half : last;
+                            return std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8);
+                        };
                         const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                         if (c1 == c0) continue;
                         if (v10)
