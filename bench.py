@@ -252,28 +252,20 @@ def main():
     ap.add_argument("--sparse-delta-div", type=int, default=None,
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
     ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
-    ap.add_argument("--sparse-lane-masks", type=int, default=None, help="sparse: 1 = lane-masked pulls")
     ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
     ap.add_argument("--chain-prio", type=int, default=None, help="dense: 0 = FW chain kernels at normal wave priority")
-    ap.add_argument("--sparse-split-labels", type=int, default=None, help="sparse: 1 = u32 latency + loss arrays")
-    ap.add_argument("--d2h-mode", type=int, default=None,
-                    help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync, N >= 2 = copy kernel of N workgroups")
-    ap.add_argument("--sparse-relabel", type=int, default=None, help="sparse: 1 = degree-dealt vertex ids (default), 0 = given ids")
-    ap.add_argument("--p1-threads", type=int, default=None, help="symmetric FW pivot closure threads (512/1024)")
+    ap.add_argument("--d2h-mode", type=int, default=None, help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync")
     ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")
     ap.add_argument("--late-loss", type=int, default=None,
                     help="host entry: 1 = edge losses shipped beside the W build and FW (default), 0 = with the edges")
     ap.add_argument("--edge-shard", type=int, default=None,
                     help="host entry, N > 1: 1 = each rank ships 1/N of the edges and the ranks exchange them, "
                          "0 = every rank ships all, -1 = auto (default: on from 4 ranks)")
-    ap.add_argument("--chain-cus", type=int, default=None, help="symmetric FW: CUs reserved for the chain (0 = none)")
-    ap.add_argument("--fw-fold", type=int, default=None, help="symmetric FW: 1 = add,add,min3; 0 = lshl_add_u64,min3")
     ap.add_argument("--scan-groups", type=int, default=None, help="host entry: scan launches interleaved with the loss (0 = auto)")
     ap.add_argument("--loss-chunks", type=int, default=None, help="dense: k_loss_rows launches (0 = auto)")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
-    ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs, KC 16, 3 waves/SIMD; 1 = packed, KC 32; 0 = add + min3")
-    ap.add_argument("--scan-variant", type=int, default=None, help="u32 tight scan kernel (0 readlane, 1 scalar)")
+    ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs; 0 = add + min3")
     ap.add_argument("--simulate-rank", type=str, default=None,
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
                          "(outputs invalid; prints a diagnostic line, never the bench result)")
@@ -356,38 +348,24 @@ def main():
         router.set_option(N.SRG_OPT_SPARSE_DELTA_ALL, args.sparse_delta_all)
     if args.sparse_delta_div is not None:
         router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, args.sparse_delta_div)
-    if args.sparse_lane_masks is not None:
-        router.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, args.sparse_lane_masks)
     if args.fw_symmetric is not None:
         router.set_option(N.SRG_OPT_FW_SYMMETRIC, args.fw_symmetric)
     if args.chain_prio is not None:
         router.set_option(N.SRG_OPT_CHAIN_PRIO, args.chain_prio)
-    if args.sparse_split_labels is not None:
-        router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, args.sparse_split_labels)
     if args.sparse_wgs is not None:
         router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
-    if args.sparse_relabel is not None:
-        router.set_option(N.SRG_OPT_SPARSE_RELABEL, args.sparse_relabel)
-    if args.p1_threads is not None:
-        router.set_option(N.SRG_OPT_P1_THREADS, args.p1_threads)
     if args.h2d_codec is not None:
         router.set_option(N.SRG_OPT_H2D_CODEC, args.h2d_codec)
     if args.late_loss is not None:
         router.set_option(N.SRG_OPT_LATE_LOSS, args.late_loss)
     if args.edge_shard is not None:
         router.set_option(N.SRG_OPT_EDGE_SHARD, args.edge_shard)
-    if args.chain_cus is not None:
-        router.set_option(N.SRG_OPT_CHAIN_CUS, args.chain_cus)
-    if args.fw_fold is not None:
-        router.set_option(N.SRG_OPT_FW_FOLD, args.fw_fold)
     if args.scan_groups is not None:
         router.set_option(N.SRG_OPT_SCAN_GROUPS, args.scan_groups)
     if args.loss_chunks is not None:
         router.set_option(N.SRG_OPT_LOSS_CHUNKS, args.loss_chunks)
     if args.d2h_mode is not None:
         router.set_option(N.SRG_OPT_D2H_MODE, args.d2h_mode)
-    if args.scan_variant is not None:
-        router.set_option(N.SRG_OPT_SCAN_VARIANT, args.scan_variant)
     if args.simulate_rank:
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)
@@ -452,12 +430,8 @@ def main():
         dev_ms = (time.perf_counter() - t1) * 1e3 / 2
     wkey = (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "") + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
-            f"w{args.sparse_wgs or 2}" + (f":lm{args.sparse_lane_masks}" if args.sparse_lane_masks else "")
-            + (f":sl{args.sparse_split_labels}" if args.sparse_split_labels else "")
+            f"w{args.sparse_wgs or 2}"
             + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
-            + (f":fold{args.fw_fold}" if args.fw_fold else "") + (f":cus{args.chain_cus}" if args.chain_cus else "")
-            + (f":p1t{args.p1_threads}" if args.p1_threads and args.p1_threads != 512 else "")
-            + (":relabel" if args.sparse_relabel else "")
             + (f":n{world}" if world > 1 else "") + (f":sim{args.simulate_rank}" if args.simulate_rank else ""))
     roofline = None
     if agg.get("prof_launches") and kind == 3:
@@ -497,7 +471,7 @@ def main():
                     "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
                     "ops_per_relaxation": OPS_PER_RELAX.get(kind, 2.0), "relax_per_s": round(relax / (avg_ms * 1e-3), 1),
                     "traffic_source": tsrc, "workload_key": wkey}
-        if kind == 0 and args.fw_packed and not args.fw_fold:
+        if kind == 0 and args.fw_packed:
             # v_min* issue at half rate on gfx950: the pair-packed relaxation pair (v_lshl_add_u64 +
             # v_min3_u32) measured 0.187 wave-instr/SIMD/cycle = 2 relaxations per 10.7 cycles per
             # wave = 0.748 of the 2-op lane peak (profiles/r01_valu_rate_microbench.txt)

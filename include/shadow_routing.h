@@ -39,8 +39,11 @@ extern "C" {
 #define SRG_ERR_UNREACHABLE 4   /* assert_eq!(paths.len(), nodes.len().pow(2)) panics   mod.rs:219 */
 #define SRG_ERR_LATENCY_RANGE 5 /* latency.convert(Nano).unwrap() overflow (mod.rs:336), or a used
                                    pair with no path below 2^62 ns on a graph whose worst-case path
-                                   sum reaches 2^62 (unreachable, or a sum the reference's u64 would
-                                   wrap); a graph whose used pairs all have paths below 2^62 ns
+                                   sum reaches 2^62.  The u64 keys hold distances below 2^62 only (an
+                                   edge of >= 2^62 ns counts as absent), so such a pair may be
+                                   unreachable OR have a shortest path in [2^62, 2^64) that the
+                                   reference would return (e.g. one 2^63 ns edge) -- a documented
+                                   deviation; a graph whose used pairs all have paths below 2^62 ns
                                    succeeds whatever its edge latencies */
 #define SRG_ERR_HIP 6           /* HIP runtime failure (no device, launch failure) */
 #define SRG_ERR_OOM 7           /* device allocation failed */
@@ -132,19 +135,9 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SIMULATE_RANK 6   /* TIMING AID ONLY: value = nranks*1000 + rank runs this rank's share
                                      with every collective elided -- outputs are NOT valid; 0 detaches */
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
-#define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles: 1 = two relaxations per 64-bit add of
-                                     packed key pairs + v_min3, 32-deep k-chunks, operand prefetch;
-                                     2 (default) = the same with 16-deep k-chunks and no operand prefetch (3 waves
-                                     per SIMD); 3 = 16-deep with prefetch; 0 = one add per relaxation */
-#define SRG_OPT_SCAN_VARIANT 9    /* u32 tight-predecessor scan: 5 (default) = two sources per lane over
-                                     LDS-staged rows (ds_read_b64) with a 4-pair scalar record stream; 6 = the
-                                     same with the records in vector registers (v_readlane); 7 = the records staged
-                                     in LDS with the rows (no scalar loads in the loop); 4 / 3 = one source per
-                                     lane over LDS-staged rows (v_readlane / s_load entry reads); 2 = entries
-                                     grouped by target, 1 = scalar (s_load) entry reads, 0 = vector entry batches
-                                     broadcast with v_readlane; 10 = four sources per lane (ds_read_b128
-                                     of 1-KB rows, 256-source workgroups; measured slower); 11 = variant 5
-                                     with one hit test per 4-pair group (measured the same) */
+#define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles (directed graphs / multi-rank): 2 (default) = two
+                                     relaxations per 64-bit add of packed key pairs + v_min3, 16-deep k-chunks;
+                                     0 = one add per relaxation */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) / 16 (one workgroup per CU) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
@@ -153,33 +146,20 @@ void srg_destroy(srg_ctx* ctx);
                                         below the bucket bound, 0 (default) = when any is */
 #define SRG_OPT_SPARSE_GLOBAL_BITMAPS 14 /* sparse: 1 = keep the per-batch vertex bitmaps in global memory
                                         (automatic when 5V/8 bytes do not fit the LDS budget) */
-#define SRG_OPT_SPARSE_LANE_MASKS 15 /* sparse: 1 = pull only the lanes whose label of the arc's source
-                                        changed since its last push (per-vertex 64-bit lane masks) */
 #define SRG_OPT_FW_SYMMETRIC 17     /* dense u32: 1 (default) = for an undirected graph on one rank, update only
                                        the FW tiles I <= J (D stays symmetric) and mirror at the end */
 #define SRG_OPT_CHAIN_PRIO 18       /* dense: 1 (default) = the FW lookahead chain kernels raise their wave priority */
 #define SRG_OPT_D2H_MODE 20         /* host entry: how finished rows are shipped into the page-locked caller
                                      * arrays while kernels run: 1 (default) = an SDMA engine, 0 =
-                                     * hipMemcpyAsync, N >= 2 = a copy kernel of N workgroups */
+                                     * hipMemcpyAsync (a full-chip blit kernel: slows the overlapped kernels) */
 #define SRG_OPT_LOSS_CHUNKS 21       /* dense: k_loss_rows launches (row chunks); 0 (default) = 8 when the host
                                      * entry ships rows early, else 1 */
-#define SRG_OPT_SCAN_GROUPS 22       /* host entry, u32 scan variants 5/6: source-block groups the scan is
+#define SRG_OPT_SCAN_GROUPS 22       /* host entry: source-block groups the tight scan is
                                      * launched in, each group's loss rows folded and shipped while
                                      * later groups scan; 0 (default) = 3, 1 = scan, then loss */
-#define SRG_OPT_FW_FOLD 23           /* symmetric u32 FW: instructions of a k-pair's two relaxations, 0 (default) =
-                                     * v_lshl_add_u64 + v_min3_u32, 1 = two v_add_u32 + v_min3_u32 (slower) */
-#define SRG_OPT_CHAIN_CUS 24         /* symmetric u32 FW: CUs reserved for the lookahead chain through CU-masked
-                                     * streams (n evenly spaced CU ids; -n = the lowest n ids); 0 = none */
 #define SRG_OPT_H2D_CODEC 25         /* host entry: 1 (default) = the edge list crosses PCIe narrowed (u16
                                      * endpoints, u32 latencies; 12 instead of 20 B per edge) when every
                                      * endpoint < 65536 and latency < 2^32, widened on the device; 0 = plain */
-#define SRG_OPT_P1_THREADS 26        /* symmetric u32 FW: threads of the pivot-closure workgroup, 512 (default) / 1024 */
-#define SRG_OPT_SPARSE_RELABEL 27    /* sparse: 1 = vertices dealt over the 64-vertex windows in descending
-                                     * in-degree order (balances the waves' sweep work; measured no gain on
-                                     * C4); 0 (default) = given ids */
-#define SRG_OPT_SCAN_U64_LOW 28      /* u64 keys: 1 (default) = the pair-lane LDS scan (variant 5) on the keys'
-                                     * low 32 bits, exact with the loss pass's multi-predecessor check;
-                                     * 0 = the generic u64 scan */
 #define SRG_OPT_EDGE_SHARD 29        /* host entry, multi-rank: 1 = each rank ships 1/N of the edge list over
                                      * its own PCIe link and the ranks exchange the slices over the GPU
                                      * links (allgatherv); 0 = every rank ships the whole list; -1 (default)
@@ -187,9 +167,6 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_LATE_LOSS 30         /* host entry: 1 (default) = the edge losses cross PCIe after the endpoints
                                      * and latencies, on their own stream beside the W build and FW (which
                                      * need no loss); 0 = with them */
-#define SRG_OPT_CHAIN_SPLIT 19     /* dense symmetric FW: split-K factor 1 (default)/2/4/8 of the line launches */
-#define SRG_OPT_SPARSE_SPLIT_LABELS 16 /* sparse: 1 = u32 latency and u32 loss label arrays; a pull loads a
-                                          source's loss only where its candidate latency can still win */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).

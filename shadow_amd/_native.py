@@ -36,26 +36,17 @@ SRG_OPT_SPARSE_LOCALITY = 5
 SRG_OPT_SIMULATE_RANK = 6
 SRG_OPT_FW_TILE = 7
 SRG_OPT_FW_PACKED = 8
-SRG_OPT_SCAN_VARIANT = 9
 SRG_OPT_SPARSE_GROUP = 10
 SRG_OPT_SPARSE_WGS_PER_CU = 11
 SRG_OPT_SPARSE_DELTA_DIV = 12
 SRG_OPT_SPARSE_DELTA_ALL = 13
 SRG_OPT_SPARSE_GLOBAL_BITMAPS = 14
-SRG_OPT_SPARSE_LANE_MASKS = 15
-SRG_OPT_SPARSE_SPLIT_LABELS = 16
 SRG_OPT_FW_SYMMETRIC = 17
 SRG_OPT_CHAIN_PRIO = 18
-SRG_OPT_CHAIN_SPLIT = 19
 SRG_OPT_D2H_MODE = 20
 SRG_OPT_LOSS_CHUNKS = 21
 SRG_OPT_SCAN_GROUPS = 22
-SRG_OPT_FW_FOLD = 23
-SRG_OPT_CHAIN_CUS = 24
 SRG_OPT_H2D_CODEC = 25
-SRG_OPT_P1_THREADS = 26
-SRG_OPT_SPARSE_RELABEL = 27
-SRG_OPT_SCAN_U64_LOW = 28
 SRG_OPT_EDGE_SHARD = 29
 SRG_OPT_LATE_LOSS = 30
 SRG_ALGO_AUTO = 0

@@ -118,8 +118,6 @@ struct P1Geo {
     __device__ __forceinline__ static int col(int tx, int b) { return b < HC ? tx * HC + b : T / 2 + tx * HC + (b - HC); }
 };
 
-// NTH = 1024 (SRG_OPT_P1_THREADS): twice the waves, half the elements per thread -- a larger share
-// of the issue slots of the CU it shares with the bulk tiles of the symmetric FW.
 template <class K, int T, int NTH = 512>
 __global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, int kb, int prio) {
     // prio: the chain runs beside the bulk tiles; a raised wave priority wins the VALU issue
@@ -327,19 +325,14 @@ __device__ __forceinline__ int tile_kept(int base, int idx, int x0, int x1) {
 template <class K, int T, int KC, int PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J);
 
-// PK (tile variant, SRG_OPT_FW_PACKED): 0 = add + min3 (any key); u32 keys only, the
-// pair-packed tile below (fw_tile_pk):
-//   1 = KC 32, next k-pair's operands read from LDS while the current one is folded (2 waves/SIMD)
-//   2 = KC 16, no operand prefetch: register budget for 3 waves per SIMD (latency hidden by
-//       the other waves instead), LDS 33 KB per workgroup
-//   3 = KC 16 with the operand prefetch
-//   4 = KC 16, no prefetch, register budget for 4 waves per SIMD (<= 128 VGPRs)
+// PK (tile variant, SRG_OPT_FW_PACKED): 0 = add + min3 (any key); 2 = u32 keys only, the
+// pair-packed tile below (fw_tile_pk) with 16-deep k-chunks and a register budget for 3 waves
+// per SIMD (the other waves hide the LDS latency; LDS 33 KB per workgroup).  Variants with
+// 32-deep chunks or an operand prefetch measured slower and were removed.
 template <int PK>
-constexpr int pk_kc() { return (PK >= 2) ? 16 : 32; }
+constexpr int pk_kc() { return PK ? 16 : 32; }
 template <int PK>
-constexpr bool pk_prefetch() { return PK == 1 || PK == 3; }
-template <int PK>
-constexpr int pk_min_waves() { return PK == 2 ? 3 : PK == 4 ? 4 : 1; }  // waves per SIMD budgeted for
+constexpr int pk_min_waves() { return PK ? 3 : 1; }  // waves per SIMD budgeted for
 
 template <class K, int T, int KC, int PK>
 __global__ void __launch_bounds__(256, pk_min_waves<PK>()) fw_product(K* __restrict__ D, size_t ld, int kb, TileSet ts) {
@@ -449,7 +442,7 @@ constexpr size_t pk_lds_bytes() {
     return (size_t)2 * KC * (T + 2) * sizeof(u64p);  // double-buffered Ap + Bp
 }
 
-template <int T, int KC, bool PF>
+template <int T, int KC>
 __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
     using S = PkStage<T, KC>;
     constexpr int M = T / 16;
@@ -513,23 +506,12 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
                     c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         };
-        if constexpr (PF) {
-            // operands of k-pair kp+1 are read from LDS while kp is folded (two register sets)
-            u64p ap[2][M], bp[2][M];
-            rd(0, ap[0], bp[0]);
+        // one register set: the other resident waves hide the LDS latency
 #pragma unroll
-            for (int kp = 0; kp < KC / 2; ++kp) {
-                if (kp + 1 < KC / 2) rd(kp + 1, ap[(kp + 1) & 1], bp[(kp + 1) & 1]);
-                fold(ap[kp & 1], bp[kp & 1]);
-            }
-        } else {
-            // one register set: the other resident waves hide the LDS latency
-#pragma unroll
-            for (int kp = 0; kp < KC / 2; ++kp) {
-                u64p ap[M], bp[M];
-                rd(kp, ap, bp);
-                fold(ap, bp);
-            }
+        for (int kp = 0; kp < KC / 2; ++kp) {
+            u64p ap[M], bp[M];
+            rd(kp, ap, bp);
+            fold(ap, bp);
         }
         if (ch + 1 < ch1) {  // write late into the other buffer
             u64p* An = lds + ((ch + 1 - ch0) & 1) * BUF;
@@ -650,13 +632,10 @@ __device__ __forceinline__ void sym_store(const SymOp<T, KC>& o, u64p* __restric
     }
 }
 
-// one stored tile C = (I, J), I <= J, relaxed through pivot block kb (k-pair LDS image as fw_tile_pk).
-// FOLD (SRG_OPT_FW_FOLD) picks the instructions of the two relaxations of one k-pair:
-//   0 = one v_lshl_add_u64 over the packed pairs + v_min3_u32
-//   1 = two v_add_u32 over the 32-bit halves + v_min3_u32: the VALU microbenchmark rates (add 0.40,
-//       min3 0.25, lshl_add_u64 0.195 wave-instr/SIMD/cycle) predicted it faster; in the tile it is
-//       slower (C3 bulk launch 0.304 vs 0.242 ms, profiles/r02c/fw_fold.txt), so 0 stays default
-template <int T, int KC, int FOLD = 0>
+// one stored tile C = (I, J), I <= J, relaxed through pivot block kb (k-pair LDS image as fw_tile_pk):
+// one v_lshl_add_u64 over the packed pairs + v_min3_u32 per two relaxations (two v_add_u32 +
+// v_min3_u32 measured slower in the tile: C3 bulk launch 0.304 vs 0.242 ms, profiles/r02c/fw_fold.txt)
+template <int T, int KC>
 __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
     using S = SymOp<T, KC>;
     constexpr int M = T / 16;
@@ -720,14 +699,8 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b) {
-                    if constexpr (FOLD == 1) {
-                        const uint32_t lo = (uint32_t)ap[a] + (uint32_t)bp[b];
-                        const uint32_t hi = (uint32_t)(ap[a] >> 32) + (uint32_t)(bp[b] >> 32);
-                        c[a][b] = KeyOps<uint32_t>::min3(c[a][b], lo, hi);
-                    } else {
-                        const u64p s = add_pairs(ap[a], bp[b]);
-                        c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
-                    }
+                    const u64p s = add_pairs(ap[a], bp[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         }
         if (ch + 1 < ch1) {  // write late into the other buffer
@@ -755,12 +728,12 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
     }
 }
 
-template <int T, int KC, int FOLD = 0>
+template <int T, int KC>
 __global__ void __launch_bounds__(256, 3) fw_product_sym(uint32_t* __restrict__ D, size_t ld, int kb, SymSet s, int prio) {
     int I, J;
     if (!sym_tile(s, (int)blockIdx.x, I, J)) return;  // whole workgroup
     if (prio) __builtin_amdgcn_s_setprio(3);  // chain (line) launches: see fw_phase1
-    fw_tile_sym<T, KC, FOLD>(D, ld, kb, I, J);
+    fw_tile_sym<T, KC>(D, ld, kb, I, J);
 }
 
 // lower triangle <- transpose of the upper one, 64 x 64 blocks (bi > bj) through LDS
@@ -779,7 +752,7 @@ template <class K, int T, int KC, int PK>
 __device__ __forceinline__ void fw_tile(K* __restrict__ D, size_t ld, int kb, int I, int J) {
     if constexpr (PK != 0) {
         static_assert(sizeof(K) == 4, "pair-packed tiles need u32 keys");
-        fw_tile_pk<T, KC, pk_prefetch<PK>()>(reinterpret_cast<uint32_t*>(D), ld, kb, I, J);
+        fw_tile_pk<T, KC>(reinterpret_cast<uint32_t*>(D), ld, kb, I, J);
         return;
     }
     using G = Geo<K, T>;

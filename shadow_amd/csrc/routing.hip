@@ -543,15 +543,12 @@ struct srg_ctx {
     bool sparse_delta_all = false;   // sparse: bucket test over every dropped lane (else any lane)
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
-    bool sparse_lane_masks = false;      // sparse: lane-masked pulls (SRG_OPT_SPARSE_LANE_MASKS)
-    bool sparse_split_labels = false;    // sparse: u32 latency + u32 loss label arrays (SRG_OPT_SPARSE_SPLIT_LABELS)
-    DevBuf b_lmask;
     int fw_tile = 0;                 // 0 = auto, 64 or 128
-    int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 1..3 pair-packed
-    int chain_split = 1;             // split-K of the symmetric FW's line launches (SRG_OPT_CHAIN_SPLIT)
+    int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 2 pair-packed
     int chain_prio = 1;              // FW lookahead chain kernels at raised wave priority (SRG_OPT_CHAIN_PRIO)
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
-    int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync, >= 2 = copy kernel of that many workgroups (SRG_OPT_D2H_MODE)
+    int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync (SRG_OPT_D2H_MODE)
+    DevBuf b_DST2;                   // low words of the u64-key DST (the scan input)
     SdmaAgents sdma;
     int h2d_codec = 1;               // host entry: narrowed edge list over PCIe (SRG_OPT_H2D_CODEC)
     HostPool* pool = nullptr;        // its host workers
@@ -560,8 +557,6 @@ struct srg_ctx {
     hipEvent_t ev_ring[3] = {nullptr, nullptr, nullptr};
     DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
     size_t own_row0 = 0, own_row1 = ~(size_t)0;  // multi-rank without output exchange: the output rows this rank filled
-    int scan_u64_low = 1;            // u64 keys: pair-lane scan on the keys' low words (SRG_OPT_SCAN_U64_LOW; 0 = generic u64 scan)
-    DevBuf b_DST2;                   // its low-word DST
     int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
     hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
     hipEvent_t ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr, ev_wlate = nullptr;
@@ -570,16 +565,8 @@ struct srg_ctx {
     int edge_shard = -1;             // host entry, multi-rank: ship 1/N of the edges, allgatherv the rest (SRG_OPT_EDGE_SHARD)
     const uint32_t* sim_edges = nullptr;  // simulated rank: the edge list whose other slices are resident
     size_t sim_E = 0;
-    int sparse_relabel = 0;          // sparse: degree-dealt vertex ids (SRG_OPT_SPARSE_RELABEL; measured no gain on C4)
-    DevBuf b_perm, b_rsrc, b_rdst, b_rslat, b_rsloss, b_rcols;  // its relabeled copies
-    int chain_cus = 0;               // symmetric FW: CUs reserved for the lookahead chain (0 = none; < 0: the lowest -n CU ids) (SRG_OPT_CHAIN_CUS)
-    int cu_streams_for = 0;          // chain_cus the two CU-masked streams below were made for
-    hipStream_t cu_bulk = nullptr, cu_chain = nullptr;
-    int p1_threads = 512;            // symmetric FW pivot closure workgroup size, 512 / 1024 (SRG_OPT_P1_THREADS)
-    int fw_fold = 0;                 // symmetric FW: 0 = v_lshl_add_u64 + v_min3 per k-pair, 1 = two v_add_u32 + v_min3 (SRG_OPT_FW_FOLD; 1 measured 0.304 vs 0.242 ms per bulk launch)
     int scan_groups = 0;             // host entry: v5 scan launches interleaved with the loss rows (0 = auto: 3) (SRG_OPT_SCAN_GROUPS)
     int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
-    int scan_variant = 5;            // u32 tight scan: 0 = vector batches + v_readlane, 1 = scalar entry loads, 2 = target runs, 3/4 = LDS u-chunks (one source per lane), 5 (default) / 6 = LDS u-chunks, two sources per lane (scalar / vector record stream)
     srg::Comm* comm = nullptr;       // null = single GPU
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
@@ -604,7 +591,7 @@ struct srg_ctx {
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
                           &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst,
-                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered, &b_lmask})
+                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
@@ -613,13 +600,13 @@ struct srg_ctx {
         for (hipEvent_t e : ev_lring)
             if (e) (void)hipEventDestroy(e);
         if (h_lring) (void)hipHostFree(h_lring);
-        for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream, cu_bulk, cu_chain})
+        for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream})
             if (s) (void)hipStreamDestroy(s);
         delete pool;
         for (hipEvent_t e : ev_ring)
             if (e) (void)hipEventDestroy(e);
         if (h_ring) (void)hipHostFree(h_ring);
-        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_DST2, &b_perm, &b_rsrc, &b_rdst, &b_rslat, &b_rsloss, &b_rcols})
+        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_DST2})
             b->release();
     }
 };
@@ -767,38 +754,6 @@ struct Timer {
     }
 };
 
-// Device -> host copy by a narrow kernel (SRG_OPT_D2H_MODE >= 2: that many workgroups), kept as
-// a measured alternative: its posted PCIe writes still slowed the streaming kernels it overlapped
-// (profiles/r02c/d2h_probe.txt), so the default ships rows on an SDMA engine instead.
-__global__ void __launch_bounds__(256) k_copy_to_host(const unsigned char* __restrict__ src,
-                                                     unsigned char* __restrict__ dst, size_t bytes) {
-    const size_t nt = (size_t)gridDim.x * blockDim.x, tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    size_t done = 0;
-    if ((((uintptr_t)src ^ (uintptr_t)dst) & 15) == 0) {
-        const size_t head = (16 - ((uintptr_t)src & 15)) & 15;  // bytes before the first 16-B boundary
-        if (head < bytes) {
-            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            const v4u* s = reinterpret_cast<const v4u*>(src + head);
-            v4u* d = reinterpret_cast<v4u*>(dst + head);
-            const size_t n16 = (bytes - head) / 16;
-            size_t i = tid;
-            for (; i + 3 * nt < n16; i += 4 * nt) {
-                const v4u a = __builtin_nontemporal_load(&s[i]), b = __builtin_nontemporal_load(&s[i + nt]);
-                const v4u c = __builtin_nontemporal_load(&s[i + 2 * nt]), e = __builtin_nontemporal_load(&s[i + 3 * nt]);
-                d[i] = a;
-                d[i + nt] = b;
-                d[i + 2 * nt] = c;
-                d[i + 3 * nt] = e;
-            }
-            for (; i < n16; i += nt) d[i] = s[i];
-            for (size_t k = tid; k < head; k += nt) dst[k] = src[k];
-            done = head + n16 * 16;
-        }
-    }
-    for (size_t k = done + tid; k < bytes; k += nt) dst[k] = src[k];  // unaligned remainder (rare)
-}
-
-
 // Host entry output sink: the caller's n x n host arrays.  Finished output rows are copied
 // while later kernels run (latency rows right after FW, loss rows per chunk of k_loss_rows),
 // so the 1.2 GB C3 table mostly leaves during the scan and loss pass.  The caller's (pageable)
@@ -813,7 +768,7 @@ __global__ void __launch_bounds__(256) k_copy_to_host(const unsigned char* __res
 struct HostSink {
     uint64_t* lat = nullptr;
     float* loss = nullptr;
-    void* lat_view = nullptr;   // device views of the mapped host arrays (copy kernel)
+    void* lat_view = nullptr;   // device views of the mapped host arrays (SDMA destinations)
     void* loss_view = nullptr;
     int mode = 1;
     const SdmaAgents* sdma = nullptr;
@@ -896,12 +851,7 @@ struct HostSink {
         }
         HIP_CHECK(hipEventRecord(ev, st));
         HIP_CHECK(hipStreamWaitEvent(cs, ev, 0));
-        if (mode >= 2 && view) {
-            k_copy_to_host<<<mode, 256, 0, cs>>>(src, (unsigned char*)view + off, bytes);
-            HIP_CHECK(hipGetLastError());
-        } else {
-            HIP_CHECK(hipMemcpyAsync((unsigned char*)host + off, src, bytes, hipMemcpyDeviceToHost, cs));
-        }
+        HIP_CHECK(hipMemcpyAsync((unsigned char*)host + off, src, bytes, hipMemcpyDeviceToHost, cs));
         early_bytes += bytes;
     }
     // wait for every copy; throws on a failed one
@@ -1149,13 +1099,13 @@ __global__ void k_low_words(const uint64_t* __restrict__ x, size_t n, uint32_t* 
 // fw_tile_sym), then the lower triangle is mirrored.  The chain of pivot k1 updates line k1
 // (row k1 = column k1^T) w.r.t. kb, closes k1, and updates line k1 w.r.t. k1; the bulk of kb
 // is every stored tile off the lines kb and k1.
-template <int T, int FOLD>
+template <int T>
 void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
                     int& prof_n) {
     constexpr int KCS = 16;
     const int nb = pl.nb;
     const size_t lds = pk_lds_bytes<T, KCS>();
-    set_lds(fw_product_sym<T, KCS, FOLD>, lds);
+    set_lds(fw_product_sym<T, KCS>, lds);
     const bool prof = c.profiling && nb > 2;
     if (prof) {
         while (c.prof_events.size() < (size_t)2 * nb) {
@@ -1164,50 +1114,17 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
             c.prof_events.push_back(e);
         }
     }
-    hipStream_t aux = c.aux_stream;
-    // SRG_OPT_CHAIN_CUS: the chain (pivot closure + line launches) gets CUs of its own through two
-    // CU-masked streams, so its single-workgroup closure does not queue behind, or share a CU with,
-    // the bulk tiles (beside them it took ~170 us instead of ~70)
-    hipStream_t bulk = st;
-    if (c.chain_cus != 0) {
-        if (c.cu_streams_for != c.chain_cus) {
-            for (hipStream_t* x : {&c.cu_bulk, &c.cu_chain})
-                if (*x) {
-                    HIP_CHECK(hipStreamDestroy(*x));
-                    *x = nullptr;
-                }
-            int ncu = 256;
-            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device));
-            const int r = std::min(std::abs(c.chain_cus), ncu / 2);
-            std::vector<uint32_t> mb((ncu + 31) / 32, 0u), mc((ncu + 31) / 32, 0u);
-            for (int i = 0; i < ncu; ++i) {
-                const bool chain = c.chain_cus > 0 ? (i % (ncu / r) == 0 && i / (ncu / r) < r) : i < r;
-                (chain ? mc : mb)[i / 32] |= 1u << (i % 32);
-            }
-            HIP_CHECK(hipExtStreamCreateWithCUMask(&c.cu_bulk, (uint32_t)mb.size(), mb.data()));
-            HIP_CHECK(hipExtStreamCreateWithCUMask(&c.cu_chain, (uint32_t)mc.size(), mc.data()));
-            c.cu_streams_for = c.chain_cus;
-        }
-        bulk = c.cu_bulk;
-        aux = c.cu_chain;
-        HIP_CHECK(hipEventRecord(c.ev_b, st));
-        HIP_CHECK(hipStreamWaitEvent(bulk, c.ev_b, 0));
-    }
-    // line launches sit on the critical chain: split-K so that ~nb x split workgroups share a tile
-    const int lsplit = std::max(1, std::min(c.chain_split, T / KCS));
+    hipStream_t aux = c.aux_stream, bulk = st;
     auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
-        fw_product_sym<T, KCS, FOLD><<<dim3(nb, 1, lsplit), 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
+        fw_product_sym<T, KCS><<<nb, 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
     };
-    auto phase1 = [&](int k, hipStream_t s) {
-        if (c.p1_threads == 1024) fw_phase1<uint32_t, T, 1024><<<1, 1024, 0, s>>>(D, Vp, k, c.chain_prio);
-        else fw_phase1<uint32_t, T><<<1, 512, 0, s>>>(D, Vp, k, c.chain_prio);
-    };
+    auto phase1 = [&](int k, hipStream_t s) { fw_phase1<uint32_t, T><<<1, 512, 0, s>>>(D, Vp, k, c.chain_prio); };
     phase1(0, bulk);
     if (nb > 1) line(0, 0, 0, -1, bulk);
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
         if (k1 >= nb) {
-            if (nb > 1) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
+            if (nb > 1) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
             break;
         }
         HIP_CHECK(hipEventRecord(c.ev_a, bulk));
@@ -1219,17 +1136,13 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
         const int m = nb - 2;  // lines kb and k1 excluded
         const bool timed = prof && m > 0;
         if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], bulk));
-        if (m > 0) fw_product_sym<T, KCS, FOLD><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
+        if (m > 0) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
         if (timed) {
             HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], bulk));
             prof_relax += (uint64_t)m * (m + 1) / 2 * T * T * T;
             ++prof_n;
         }
         HIP_CHECK(hipStreamWaitEvent(bulk, c.ev_d, 0));
-    }
-    if (bulk != st) {
-        HIP_CHECK(hipEventRecord(c.ev_b, bulk));
-        HIP_CHECK(hipStreamWaitEvent(st, c.ev_b, 0));
     }
     const unsigned nb64 = (unsigned)(Vp / 64);
     k_sym_mirror<uint32_t><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
@@ -1290,17 +1203,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const bool sym_fw = sizeof(K) == 4 && T == 128 && c.fw_symmetric && !g.directed && !multi && c.fw_packed != 0;
     if (sym_fw) {
         if constexpr (sizeof(K) == 4 && T == 128) {
-            if (c.fw_fold == 1) fw_blocked_sym<T, 1>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
-            else fw_blocked_sym<T, 0>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
+            fw_blocked_sym<T>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
         }
     } else if constexpr (sizeof(K) == 4) {
-        switch (c.fw_packed) {
-            case 0: fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n); break;
-            case 2: fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n); break;
-            case 3: fw_blocked<K, T, 3>(c, pl, D, Vp, st, prof_relax, prof_n); break;
-            case 4: fw_blocked<K, T, 4>(c, pl, D, Vp, st, prof_relax, prof_n); break;
-            default: fw_blocked<K, T, 1>(c, pl, D, Vp, st, prof_relax, prof_n); break;
-        }
+        if (c.fw_packed) fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n);
+        else fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
     } else {
         fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
     }
@@ -1451,7 +1358,6 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     HIP_CHECK(hipMemsetAsync(multi_cnt, 0, 8, st));
     // essential bitmask of the own rows, then all-gathered (V^2/8 bytes)
     const uint32_t nw64 = (V + 63) / 64;
-    const uint32_t nbT = 2 * nw64;
     unsigned long long* ess = (unsigned long long*)c.b_ess.get((size_t)V * nw64 * 8);
     if (pl.u1 > pl.u0)
         k_ess_mask<K><<<grid_for((size_t)(pl.u1 - pl.u0) * nw64 * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, pl.u0,
@@ -1470,33 +1376,20 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    // pair-lane LDS scans (9x: timing experiments); u64 keys run variant 5 on the keys' low words
-    // (tight_sparse.hip.h: exact together with the loss pass's multi-predecessor check)
-    const bool v5lo = sizeof(K) == 8 && c.scan_u64_low;
-    const bool v5 = (sizeof(K) == 4 && ((c.scan_variant >= 5 && c.scan_variant <= 11) || c.scan_variant >= 91)) || v5lo;
-    const bool v10 = v5 && c.scan_variant == 10;  // four sources per lane: 256-source blocks
-    const uint32_t SB = v10 ? V10_SB : V5_SB;
-    const size_t npad = v5 ? ((size_t)nloc + SB - 1) / SB * SB : ((size_t)nloc + 63) / 64 * 64;
+    // pair-lane LDS scan (tight_v5); u64 keys run it on the keys' low words (exact together with
+    // the loss pass's multi-predecessor check, tight_sparse.hip.h)
+    const bool v5lo = sizeof(K) == 8;
+    const uint32_t SB = V5_SB;
+    const size_t npad = ((size_t)nloc + SB - 1) / SB * SB;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
-    const uint32_t NT = nw64 * 64;  // == nbT * TB targets
-    // LDS-staged scan (SRG_OPT_SCAN_VARIANT 3, default): entries by (target tile, u-chunk, target)
-    const bool lds = sizeof(K) == 4 && (c.scan_variant == 3 || c.scan_variant == 4);
-    const uint32_t nK = (V + LS_UC - 1) / LS_UC, nbTT = (NT + LS_TT - 1) / LS_TT;
-    const size_t NQ3 = (size_t)nbTT * nK * LS_TT;
-    uint32_t *ls_cnt = nullptr, *ls_nr = nullptr, *ls_roff = nullptr;
-    // 32-target blocks (variants 0/1) and target runs (variant 2)
-    const bool runs = sizeof(K) == 4 && c.scan_variant == 2;
-    uint32_t *ecnt = nullptr, *eoff = nullptr, *eblk = nullptr, *roff = nullptr;
-    const size_t NQ = (size_t)nbT * V;
-    uint64_t E_ess = 0, E_layout = 0;
-    size_t tbytes = 0;
+    const uint32_t NT = nw64 * 64;
     const uint32_t nK5 = (V + V5_UC - 1) / V5_UC, nbTT5 = (NT + V5_TT - 1) / V5_TT;
     const size_t NG5 = (size_t)nbTT5 * nK5 * V5_WAVES;
-    uint32_t *v5_cnt = nullptr, *v5_goff = nullptr;
-    if (v5) {
-        v5_cnt = (uint32_t*)c.b_ecnt.get((size_t)nbTT5 * nK5 * V5_TT * 4);
+    uint32_t* v5_cnt = (uint32_t*)c.b_ecnt.get((size_t)nbTT5 * nK5 * V5_TT * 4);
+    uint32_t* v5_goff = (uint32_t*)c.b_eoff.get((NG5 + 1) * 4);
+    uint64_t E_ess = 0, E_layout = 0;
+    {
         uint32_t* v5_glen = (uint32_t*)c.b_rlen.get((NG5 + 1) * 4);
-        v5_goff = (uint32_t*)c.b_eoff.get((NG5 + 1) * 4);
         HIP_CHECK(hipMemsetAsync(v5_cnt, 0, (size_t)nbTT5 * nK5 * V5_TT * 4, st));
         HIP_CHECK(hipMemsetAsync(v5_glen, 0, (NG5 + 1) * 4, st));
         const size_t nwaves = (size_t)nw64 * nK5;
@@ -1505,76 +1398,16 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         size_t ta = 0, tc = 0;
         HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), st));
         HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, v5_glen, v5_goff, (int)(NG5 + 1), st));
-        tbytes = std::max(ta, tc);
+        const size_t tbytes = std::max(ta, tc);
         void* tmp = c.b_scantmp.get(tbytes);
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, v5_glen, v5_goff, (int)(NG5 + 1), st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, ta, indeg, cscoff, (int)(NT + 1), st));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tc, v5_glen, v5_goff, (int)(NG5 + 1), st));
         uint32_t tail[2];
         HIP_CHECK(hipMemcpyAsync(&tail[0], cscoff + NT, 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipMemcpyAsync(&tail[1], v5_goff + NG5, 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         E_ess = tail[0];
         E_layout = 2ull * tail[1];
-    } else if (lds) {
-        ls_cnt = (uint32_t*)c.b_ecnt.get(NQ3 * 4);
-        ls_nr = (uint32_t*)c.b_gblk.get(NQ3 * 4);
-        uint32_t* ls_rlen = (uint32_t*)c.b_rlen.get((NQ3 + 1) * 4);
-        ls_roff = (uint32_t*)c.b_eoff.get((NQ3 + 1) * 4);
-        HIP_CHECK(hipMemsetAsync(ls_cnt, 0, NQ3 * 4, st));  // target windows past nw64 stay empty
-        HIP_CHECK(hipMemsetAsync(ls_nr, 0, NQ3 * 4, st));
-        HIP_CHECK(hipMemsetAsync(ls_rlen, 0, (NQ3 + 1) * 4, st));
-        const size_t nwaves = (size_t)nw64 * nK;
-        k_ls_count<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, V, nw64, nK, ls_cnt, ls_nr, ls_rlen,
-                                                                            indeg);
-        HIP_CHECK(hipGetLastError());
-        size_t ta = 0, tc = 0;
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, ls_rlen, ls_roff, (int)(NQ3 + 1), st));
-        tbytes = std::max(ta, tc);
-        void* tmp = c.b_scantmp.get(tbytes);
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ls_rlen, ls_roff, (int)(NQ3 + 1), st));
-        uint32_t tail[2];
-        HIP_CHECK(hipMemcpyAsync(&tail[0], cscoff + NT, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(&tail[1], ls_roff + NQ3, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        E_ess = tail[0];
-        E_layout = tail[1];
-    } else {
-        ecnt = (uint32_t*)c.b_ecnt.get(NQ * 4);
-        eoff = (uint32_t*)c.b_eoff.get(NQ * 4);
-        eblk = (uint32_t*)c.b_gblk.get(((size_t)nbT + 1) * 4);
-        k_ess_count<<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(ess, V, nw64, ecnt, indeg);
-        HIP_CHECK(hipGetLastError());
-        size_t tb0 = 0, tb2 = 0;
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb0, ecnt, eoff, (int)NQ, st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, indeg, cscoff, (int)(nw64 * 64 + 1), st));
-        tbytes = std::max(tb0, tb2);
-        void* tmp = c.b_scantmp.get(tbytes);
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, ecnt, eoff, (int)NQ, st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tbytes, indeg, cscoff, (int)(nw64 * 64 + 1), st));
-        k_ess_blocks<<<1, 1, 0, st>>>(eoff, ecnt, V, nbT, eblk);
-        uint32_t tail[3];
-        HIP_CHECK(hipMemcpyAsync(&tail[0], eoff + NQ - 1, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(&tail[1], ecnt + NQ - 1, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(&tail[2], eblk + nbT, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        E_ess = (uint64_t)tail[0] + tail[1];
-        E_layout = tail[2];  // padded entry count (blocks rounded up to 64)
-        // run layout (entries grouped by target, variant 2): run offsets from indeg
-        if (runs) {
-            uint32_t* rlen = (uint32_t*)c.b_rlen.get(((size_t)NT + 1) * 4);
-            roff = (uint32_t*)c.b_roff.get(((size_t)NT + 1) * 4);
-            k_run_len<<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, V, NT, rlen);
-            size_t tb3 = 0;
-            HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, rlen, roff, (int)(NT + 1), st));
-            void* tmp3 = c.b_scantmp.get(std::max(tb3, tbytes));
-            HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp3, tb3, rlen, roff, (int)(NT + 1), st));
-            uint32_t tot = 0;
-            HIP_CHECK(hipMemcpyAsync(&tot, roff + NT, 4, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            E_layout = tot;
-        }
     }
     n_ess = E_ess;
     if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));  // WL (late loss) before the entry fill
@@ -1584,42 +1417,23 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         scan_kind = SRG_SCAN_SPARSE;
         const size_t Eb = E_layout + 256;
         uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
-        uint32_t* ent_ro = v5 ? nullptr : (uint32_t*)c.b_entkey.get(Eb * 4);  // v5: pair records instead
         K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
-        uint32_t* ent_tl = (uint32_t*)c.b_grpu.get(Eb * 4);
         uint32_t* ent_u = (uint32_t*)c.b_grpe.get(Eb * 4);
         float* ent_b = (float*)c.b_entb.get(Eb * 4);
         uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
-        if (v5) {
-            HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
-            uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
+        HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+        uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
+        {
             const size_t nwaves = (size_t)nw64 * nK5;
             k_v5_fill<K><<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK5, v5_cnt,
                                                                                   v5_goff, cscoff, cscfill, rec, ent_w,
                                                                                   ent_u, ent_b, cscent);
-        } else if (lds) {
-            if constexpr (sizeof(K) == 4) {
-                const size_t nwaves = (size_t)nw64 * nK;
-                k_ls_fill<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK, ls_cnt,
-                                                                                   ls_roff, cscoff, ent_ro, ent_w,
-                                                                                   ent_u, ent_b, cscent);
-            }
-        } else {
-            HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
-            k_ess_fill<K><<<grid_for((size_t)nw64 * V * 64, 256 * 64), 256, 0, st>>>(
-                ess, W, WL, Vp, V, nw64, std::max<size_t>(npad, 64), eoff, eblk, cscoff, cscfill, ent_ro, ent_w,
-                ent_tl, ent_u, ent_b, cscent, roff);
-            if (runs)
-                k_run_pad<K><<<grid_for((size_t)NT + 1), kThreads, 0, st>>>(indeg, roff, V, NT, ent_ro, ent_w,
-                                                                              ent_tl, ent_u, ent_b);
-            else
-                k_ess_pad<K><<<nbT + 1, 64, 0, st>>>(eoff, ecnt, eblk, V, nbT, ent_ro, ent_w, ent_tl, ent_u, ent_b);
         }
         HIP_CHECK(hipGetLastError());
-        // host entry, one rank, v5/v6 scan, per-row LDS loss: scan groups interleaved with the loss
+        // host entry, one rank, per-row LDS loss: scan groups interleaved with the loss rows
         const size_t lds_rows = loss_rows_lds(V);
         const uint32_t scan_groups = c.scan_groups ? (uint32_t)c.scan_groups : 3u;
-        const bool interleave = v5 && sink_rows && lds_rows <= 150 * 1024 && scan_groups > 1;
+        const bool interleave = sink_rows && lds_rows <= 150 * 1024 && scan_groups > 1;
         if (interleave) {
             set_lds(k_loss_rows<K>, lds_rows);
             HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
@@ -1628,7 +1442,6 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             const uint32_t nbS = (uint32_t)(npad / 64);
             K* DST = (K*)c.b_DST.get(dst_bytes);
             k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
-            const uint32_t nblk = 8u * nbT * ((nbS + 7) / 8);
             // the scan's DST: the keys themselves (u32), or their low words (u64 keys)
             const uint32_t* DSTs = (const uint32_t*)DST;
             uint32_t dsts_bytes = (uint32_t)std::min<size_t>(dst_bytes, 0xFFFFFFFFull);
@@ -1640,114 +1453,45 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 dsts_bytes = (uint32_t)(cnt * 4);
             }
             const uint32_t inf_check = v5lo ? 0u : 1u;
-            if (v5) {
-                {
-                    const uint32_t nbS5 = (uint32_t)(npad / SB);
-                    if (v10) set_lds(tight_v10, 2 * V5_UC * V10_SB * 4);
-                    auto scan5 = v5lo ? tight_v5
-                                 : c.scan_variant == 6 ? tight_v6 : c.scan_variant == 7 ? tight_v7<0> : c.scan_variant == 8 ? tight_v7<1>
-                                 : c.scan_variant == 91 ? tight_v7<0, 1> : c.scan_variant == 92 ? tight_v7<0, 2>
-                                 : c.scan_variant == 11 ? tight_v11 : tight_v5;
-                    // host entry: the scan runs in source-block groups, each group's loss rows folded
-                    // right after it and shipped while later groups scan (loss rows on a second
-                    // stream beside the next group's scan were starved of CUs: 24.7 ms vs 20.8)
-                    uint32_t ng = interleave ? std::min<uint32_t>(scan_groups, nbS5) : 1u;
-                    // experiments: explicit group bounds in source blocks ("24,56"), env SRG_SCAN_CUTS
-                    std::vector<uint32_t> cuts_env;
-                    if (const char* e = interleave ? std::getenv("SRG_SCAN_CUTS") : nullptr) {
-                        for (const char* q = e; *q;) {
-                            char* end = nullptr;
-                            const unsigned long x = std::strtoul(q, &end, 10);
-                            if (end == q) break;
-                            if (x > 0 && x < nbS5 && (cuts_env.empty() || x > cuts_env.back())) cuts_env.push_back((uint32_t)x);
-                            q = *end ? end + 1 : end;
-                        }
-                        if (!cuts_env.empty()) ng = (uint32_t)cuts_env.size() + 1;
-                    }
-                    for (uint32_t gi = 0; gi < ng; ++gi) {
-                        // group bounds on multiples of 8 source blocks: every XCD gets the same
-                        // number of blocks per launch (20 blocks = 3/3/3/3/2/2/2/2 ran 33 % long)
-                        auto cut = [&](uint32_t q) {
-                            if (q == 0) return 0u;
-                            if (q == ng) return nbS5;
-                            if (!cuts_env.empty()) return cuts_env[q - 1];
-                            // three groups: half, then all but the last partial 8 blocks, so the
-                            // loss rows left to ship after the last fold are few (C3 40 / 32 / 7
-                            // blocks: exposed D2H 1.8 -> 0.8 ms, scan + tail -0.6 ms vs thirds,
-                            // profiles/r02i/scan_cuts.txt)
-                            const uint32_t half = std::min(nbS5, (nbS5 / 2 + 4) / 8 * 8), last = (nbS5 - 1) / 8 * 8;
-                            if (ng == 3 && half > 0 && last > half) return q == 1 ? half : last;
-                            return std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8);
-                        };
-                        const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
-                        if (c1 == c0) continue;
-                        if (v10)
-                            tight_v10<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 2 * V5_UC * V10_SB * 4, st>>>(
-                                DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
-                                v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
-                        else if (c.scan_variant == 9 && !v5lo)
-                            tight_v9<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
-                                DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
-                                v5_goff, (const uint32_t*)c.b_entkey.get(0), v5_cnt, PRED, Vp, inf_check);
-                        else
-                            scan5<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
-                                DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0,
-                                v5_goff, (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
-                        HIP_CHECK(hipGetLastError());
-                        if (interleave) {
-                            const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);
-                            if (r1 <= r0) continue;
-                            k_loss_rows<K><<<r1 - r0, 1024, lds_rows, st>>>(
-                                PRED, Vp, V, lnodes, nloc, ent_u, ent_b, ent_w, DST, npad, cscoff, cscent, P.selfloss,
-                                nodes, n, lpos, out_loss, &P.flags->changed, r0);
-                            HIP_CHECK(hipGetLastError());
-                            sink->send_rows(st, out_loss, sink->loss, r0, r1 - r0, 4);
-                        }
-                    }
+            const uint32_t nbS5 = (uint32_t)(npad / SB);
+            // host entry: the scan runs in source-block groups, each group's loss rows folded right
+            // after it and shipped while later groups scan (loss rows on a second stream beside the
+            // next group's scan were starved of CUs: 24.7 ms vs 20.8)
+            const uint32_t ng = interleave ? std::min<uint32_t>(scan_groups, nbS5) : 1u;
+            for (uint32_t gi = 0; gi < ng; ++gi) {
+                // group bounds on multiples of 8 source blocks: every XCD gets the same number of
+                // blocks per launch (20 blocks = 3/3/3/3/2/2/2/2 ran 33 % long)
+                auto cut = [&](uint32_t q) {
+                    if (q == 0) return 0u;
+                    if (q == ng) return nbS5;
+                    // three groups: half, then all but the last partial 8 blocks, so the loss rows
+                    // left to ship after the last fold are few (C3 40 / 32 / 7 blocks: exposed D2H
+                    // 1.8 -> 0.8 ms, scan + tail -0.6 ms vs thirds, profiles/r02i/scan_cuts.txt)
+                    const uint32_t half = std::min(nbS5, (nbS5 / 2 + 4) / 8 * 8), last = (nbS5 - 1) / 8 * 8;
+                    if (ng == 3 && half > 0 && last > half) return q == 1 ? half : last;
+                    return std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8);
+                };
+                const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
+                if (c1 == c0) continue;
+                tight_v5<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                    DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0, v5_goff,
+                    (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
+                HIP_CHECK(hipGetLastError());
+                if (interleave) {
+                    const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);
+                    if (r1 <= r0) continue;
+                    k_loss_rows<K><<<r1 - r0, 1024, lds_rows, st>>>(PRED, Vp, V, lnodes, nloc, ent_u, ent_b, ent_w,
+                                                                   DST, npad, cscoff, cscent, P.selfloss, nodes, n,
+                                                                   lpos, out_loss, &P.flags->changed, r0);
+                    HIP_CHECK(hipGetLastError());
+                    sink->send_rows(st, out_loss, sink->loss, r0, r1 - r0, 4);
                 }
-            } else if constexpr (sizeof(K) == 4) {
-                if (lds) {
-                    auto kern = c.scan_variant == 4 ? tight_lds_u32_rl : tight_lds_u32;
-                    kern<<<8u * nbTT * ((nbS + 7) / 8), LS_WAVES * 64, 0, st>>>(
-                        (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, (uint32_t)Vp, nbTT, nbS, nK,
-                        ls_nr, ls_roff, ent_ro, (const uint32_t*)ent_w, PRED, Vp);
-                } else if (runs) {
-                    constexpr uint32_t TBR = 8;
-                    const uint32_t nbR = NT / TBR;
-                    tight_sparse_u32_runs<TBR><<<8u * nbR * ((nbS + 7) / 8), 64, 0, st>>>(
-                        (const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbR, nbS, roff, ent_ro,
-                        (const uint32_t*)ent_w, ent_tl, PRED, Vp);
-                } else {
-                    auto scan = c.scan_variant ? tight_sparse_u32_s : tight_sparse_u32;
-                    scan<<<nblk, 64, 0, st>>>((const uint32_t*)DST, npad, (uint32_t)dst_bytes, lnodes, nloc, V, nbT, nbS,
-                                              eblk, ent_ro, (const uint32_t*)ent_w, ent_tl, PRED, Vp);
-                }
-            } else {
-                tight_sparse<K><<<nblk, 64, 0, st>>>(DST, npad, lnodes, nloc, V, nbT, nbS, eblk, ent_u, ent_w, ent_tl,
-                                                      PRED, Vp);
             }
-            HIP_CHECK(hipGetLastError());
             k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
             HIP_CHECK(hipGetLastError());
-            if (const char* dbg = std::getenv("SRG_DEBUG_PRED")) {
-                // debugging aid: the tight predecessor VERTEX per (used row, target), -1 none, -2 multi
-                std::vector<uint32_t> pr((size_t)nloc * Vp), eu(E_layout + 256);
-                HIP_CHECK(hipMemcpyAsync(pr.data(), PRED, pr.size() * 4, hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipMemcpyAsync(eu.data(), ent_u, eu.size() * 4, hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipStreamSynchronize(st));
-                if (FILE* f = std::fopen(dbg, "wb")) {
-                    for (uint32_t r = 0; r < nloc; ++r)
-                        for (uint32_t t = 0; t < V; ++t) {
-                            const uint32_t p = pr[(size_t)r * Vp + t];
-                            const int32_t u = p == PRED_NONE ? -1 : p == PRED_MULTI ? -2 : (int32_t)eu[p];
-                            std::fwrite(&u, 4, 1, f);
-                        }
-                    std::fclose(f);
-                }
-            }
             ms_scan = tm.lap();
             if (interleave) {  // loss rows already folded and shipped, group by group
-                if (sink_rows) sink->loss_sent = true;
+                sink->loss_sent = true;
                 uint32_t sw = 0;
                 HIP_CHECK(hipMemcpyAsync(&sw, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipStreamSynchronize(st));
@@ -1870,24 +1614,6 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
 // Rank r routes the used sources at positions [r*n/G, (r+1)*n/G) (contiguous output rows).
 // Returns false when a used pair came out saturated/unreachable and the graph's latencies
 // could exceed the u32 keys: the caller then decides on the dense u64 path.
-// sparse relabeling: edges, self-loop data and output columns in the new vertex ids
-__global__ void k_relabel(uint64_t E, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ src,
-                          const uint32_t* __restrict__ dst, uint32_t* __restrict__ rsrc, uint32_t* __restrict__ rdst,
-                          uint32_t V, const uint64_t* __restrict__ slat, const float* __restrict__ sloss,
-                          uint64_t* __restrict__ rslat, float* __restrict__ rsloss, uint32_t n,
-                          const uint32_t* __restrict__ nodes, uint32_t* __restrict__ rcols) {
-    const size_t nt = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < E; i += nt) {
-        rsrc[i] = perm[src[i]];
-        rdst[i] = perm[dst[i]];
-    }
-    for (size_t v = blockIdx.x * (size_t)blockDim.x + threadIdx.x; v < V; v += nt) {
-        rslat[perm[v]] = slat[v];
-        rsloss[perm[v]] = sloss[v];
-    }
-    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += nt) rcols[j] = perm[nodes[j]];
-}
-
 bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
                 float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats) {
     const uint32_t V = g.V;
@@ -1896,56 +1622,11 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     Timer tm(st);
     uint32_t* off = (uint32_t*)c.b_indeg.get(((size_t)V + 1) * 4);
     uint32_t* cur = (uint32_t*)c.b_cscfill.get(((size_t)V + 1) * 4);
-    // Vertex relabeling (SRG_OPT_SPARSE_RELABEL): a wave owns every 16th 64-vertex window for a
-    // whole sweep, so the windows' in-degree sums are its work.  Generated or real graphs often
-    // number their hubs first (Barabasi-Albert: window 0 holds 26x the mean in-degree sum, the
-    // wave that owns it 1.42x the mean): vertices are dealt round-robin over the windows in
-    // descending in-degree order (windows within 2.3x of the mean, waves within 1.02x).  Labels,
-    // self-loop data and output columns are read through the new ids; outputs keep their order.
-    // Measured on C4: 303 vs 302 ms without it -- the kernel is bound by its label traffic
-    // (1.28 TB per launch at ~4.2 TB/s), not by the waves' balance -- so it is off by default.
     const uint32_t* esrc = g.src;
     const uint32_t* edst = g.dst;
     const uint64_t* selflat = P.selflat;
     const float* selfloss = P.selfloss;
     const uint32_t* cols = nodes;
-    std::vector<uint32_t> perm;
-    if (c.sparse_relabel && V > 64 && g.E) {
-        HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
-        k_csr_count<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.directed, cur);
-        std::vector<uint32_t> hdeg(V);
-        HIP_CHECK(hipMemcpyAsync(hdeg.data(), cur, (size_t)V * 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        std::vector<uint32_t> rank(V);
-        for (uint32_t v = 0; v < V; ++v) rank[v] = v;
-        std::stable_sort(rank.begin(), rank.end(), [&](uint32_t x, uint32_t y) { return hdeg[x] > hdeg[y]; });
-        const uint32_t nw = (V + 63) / 64;
-        perm.assign(V, 0);
-        uint32_t r = 0;
-        for (uint32_t sl = 0; sl < 64; ++sl)
-            for (uint32_t w = 0; w < nw; ++w) {
-                const uint32_t id = w * 64 + sl;
-                if (id < V) perm[rank[r++]] = id;
-            }
-        uint32_t* d_perm = (uint32_t*)c.b_perm.get((size_t)V * 4);
-        uint32_t* rsrc = (uint32_t*)c.b_rsrc.get(g.E * 4);
-        uint32_t* rdst = (uint32_t*)c.b_rdst.get(g.E * 4);
-        uint64_t* rslat = (uint64_t*)c.b_rslat.get((size_t)V * 8);
-        float* rsloss = (float*)c.b_rsloss.get((size_t)V * 4);
-        uint32_t* rcols = (uint32_t*)c.b_rcols.get(std::max<size_t>(n, 1) * 4);
-        HIP_CHECK(hipMemcpyAsync(d_perm, perm.data(), (size_t)V * 4, hipMemcpyHostToDevice, st));
-        k_relabel<<<grid_for(std::max<size_t>(g.E, V)), kThreads, 0, st>>>(g.E, d_perm, g.src, g.dst, rsrc, rdst, V,
-                                                                          P.selflat, P.selfloss, rslat, rsloss, n,
-                                                                          nodes, rcols);
-        HIP_CHECK(hipGetLastError());
-        esrc = rsrc;
-        edst = rdst;
-        selflat = rslat;
-        selfloss = rsloss;
-        cols = rcols;
-        HIP_CHECK(hipStreamSynchronize(st));  // perm (host vector) stays alive; the copy is done
-    }
-    auto vid = [&](uint32_t v) { return perm.empty() ? v : perm[v]; };
     // CSR of in-arcs
     HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
     if (g.E) k_csr_count<<<grid_for(g.E), kThreads, 0, st>>>(g.E, esrc, edst, g.directed, cur);
@@ -2023,11 +1704,11 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     for (uint32_t i = 0; i < nloc; ++i) loc[i] = p0 + i;
     if (c.sparse_locality)
         std::stable_sort(loc.begin(), loc.end(),
-                         [&](uint32_t x, uint32_t y) { return order[vid(P.nodes_h[x])] < order[vid(P.nodes_h[y])]; });
+                         [&](uint32_t x, uint32_t y) { return order[P.nodes_h[x]] < order[P.nodes_h[y]]; });
     std::vector<uint32_t> bsrc((size_t)std::max<uint32_t>(nbatch, 1) * 64), brow(bsrc.size());
     for (uint32_t i = 0; i < (uint32_t)bsrc.size(); ++i) {
         const bool real = i < nloc;
-        bsrc[i] = vid(P.nodes_h[real ? loc[i] : (nloc ? loc[0] : 0)]);
+        bsrc[i] = P.nodes_h[real ? loc[i] : (nloc ? loc[0] : 0)];
         brow[i] = real ? loc[i] : 0xFFFFFFFFu;
     }
     uint32_t* d_bsrc = (uint32_t*)c.b_lnodes.get(bsrc.size() * 4);
@@ -2046,7 +1727,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     // label slots (V x 64 x 8 B per resident batch) within about half of the free HBM
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t slot_bytes = (size_t)V * 64 * 8 + (c.sparse_lane_masks ? (size_t)V * 3 * 8 : 0);
+    const size_t slot_bytes = (size_t)V * 64 * 8;
     grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
     const uint32_t nwv = (V + 63) / 64;
     const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
@@ -2056,25 +1737,20 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
     if (nbatch) {
         unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
-        unsigned long long* lm =
-            c.sparse_lane_masks ? (unsigned long long*)c.b_lmask.get((size_t)grid * V * 3 * 8) : nullptr;
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
-        auto kern = c.sparse_split_labels
-                        ? (gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true, true> : k_sparse_bf<SP_G, true, true>)
-                                 : (c.sparse_group == 4 ? k_sparse_bf<4, false, true> : k_sparse_bf<SP_G, false, true>))
-                        : (gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true, false> : k_sparse_bf<SP_G, true, false>)
-                                 : (c.sparse_group == 4 ? k_sparse_bf<4, false, false> : k_sparse_bf<SP_G, false, false>));
-        if (c.sparse_wgs_per_cu == 1 && !c.sparse_split_labels) {  // 128-VGPR budget (no spills)
-            kern = gbits ? (c.sparse_group == 16 ? k_sparse_bf<16, true, false, 4>
-                            : c.sparse_group == 4 ? k_sparse_bf<4, true, false, 4> : k_sparse_bf<SP_G, true, false, 4>)
-                         : (c.sparse_group == 16 ? k_sparse_bf<16, false, false, 4>
-                            : c.sparse_group == 4 ? k_sparse_bf<4, false, false, 4> : k_sparse_bf<SP_G, false, false, 4>);
+        auto kern = gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true> : k_sparse_bf<SP_G, true>)
+                          : (c.sparse_group == 4 ? k_sparse_bf<4, false> : k_sparse_bf<SP_G, false>);
+        if (c.sparse_wgs_per_cu == 1) {  // 128-VGPR budget (no spills)
+            kern = gbits ? (c.sparse_group == 16 ? k_sparse_bf<16, true, 4>
+                            : c.sparse_group == 4 ? k_sparse_bf<4, true, 4> : k_sparse_bf<SP_G, true, 4>)
+                         : (c.sparse_group == 16 ? k_sparse_bf<16, false, 4>
+                            : c.sparse_group == 4 ? k_sparse_bf<4, false, 4> : k_sparse_bf<SP_G, false, 4>);
         }
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
-                     selflat, selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb, lm};
+                     selflat, selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.es.max_lat / (unsigned long long)c.sparse_delta_div);
@@ -2101,9 +1777,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     const double ms_sssp = tm.lap();
     if (std::getenv("SRG_DEBUG_SPARSE")) {
         const unsigned long long ev = (unsigned long long)hfl[2] | (unsigned long long)hfl[3] << 32;
-        const unsigned long long ll = (unsigned long long)hfl[6] | (unsigned long long)hfl[7] << 32;
-        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu, arc lanes loaded %llu\n",
-                     nbatch, grid, hfl[1], ev, ll);
+        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu\n", nbatch, grid,
+                     hfl[1], ev);
     }
     if (hfl[0]) {
         // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
@@ -2772,12 +2447,8 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
         case SRG_OPT_FW_PACKED:
-            if (!(value == 0 || value == 1 || value == 2 || value == 3 || value == 4)) return SRG_ERR_ARG;
+            if (value != 0 && value != 2) return SRG_ERR_ARG;
             ctx->fw_packed = (int)value;
-            return SRG_OK;
-        case SRG_OPT_SCAN_VARIANT:
-            if (!((value >= 0 && value <= 11) || value == 91 || value == 92) || value != (int)value) return SRG_ERR_ARG;
-            ctx->scan_variant = (int)value;
             return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
             if (value != 4 && value != 8 && value != 16) return SRG_ERR_ARG;  // 16: one workgroup per CU only
@@ -2797,21 +2468,11 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SPARSE_GLOBAL_BITMAPS:
             ctx->sparse_global_bitmaps = value != 0.0;
             return SRG_OK;
-        case SRG_OPT_SPARSE_LANE_MASKS:
-            ctx->sparse_lane_masks = value != 0.0;
-            return SRG_OK;
-        case SRG_OPT_SPARSE_SPLIT_LABELS:
-            ctx->sparse_split_labels = value != 0.0;
-            return SRG_OK;
         case SRG_OPT_FW_SYMMETRIC:
             ctx->fw_symmetric = value != 0.0;
             return SRG_OK;
         case SRG_OPT_CHAIN_PRIO:
             ctx->chain_prio = value != 0.0 ? 1 : 0;
-            return SRG_OK;
-        case SRG_OPT_SCAN_U64_LOW:
-            if (value != 0 && value != 1) return SRG_ERR_ARG;
-            ctx->scan_u64_low = (int)value;
             return SRG_OK;
         case SRG_OPT_LATE_LOSS:
             if (value != 0 && value != 1) return SRG_ERR_ARG;
@@ -2821,25 +2482,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1 && value != -1) return SRG_ERR_ARG;
             ctx->edge_shard = (int)value;
             return SRG_OK;
-        case SRG_OPT_SPARSE_RELABEL:
-            if (value != 0 && value != 1) return SRG_ERR_ARG;
-            ctx->sparse_relabel = (int)value;
-            return SRG_OK;
-        case SRG_OPT_P1_THREADS:
-            if (value != 512 && value != 1024) return SRG_ERR_ARG;
-            ctx->p1_threads = (int)value;
-            return SRG_OK;
         case SRG_OPT_H2D_CODEC:
             if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->h2d_codec = (int)value;
-            return SRG_OK;
-        case SRG_OPT_CHAIN_CUS:
-            if (value < -128 || value > 128 || value != (int)value) return SRG_ERR_ARG;
-            ctx->chain_cus = (int)value;
-            return SRG_OK;
-        case SRG_OPT_FW_FOLD:
-            if (value != 0 && value != 1) return SRG_ERR_ARG;
-            ctx->fw_fold = (int)value;
             return SRG_OK;
         case SRG_OPT_SCAN_GROUPS:
             if (value < 0 || value > 1024) return SRG_ERR_ARG;
@@ -2850,12 +2495,8 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->loss_chunks = (int)value;
             return SRG_OK;
         case SRG_OPT_D2H_MODE:
-            if (value < 0 || value > 1024) return SRG_ERR_ARG;
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->d2h_mode = (int)value;
-            return SRG_OK;
-        case SRG_OPT_CHAIN_SPLIT:
-            if (!(value == 1 || value == 2 || value == 4 || value == 8)) return SRG_ERR_ARG;
-            ctx->chain_split = (int)value;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;

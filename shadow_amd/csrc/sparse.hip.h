@@ -36,10 +36,10 @@ constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_CAP = 128;            // active-arc list entries per wave
 constexpr int SP_G = 8;                // label rows in flight per wave (default; SRG_OPT_SPARSE_GROUP)
 constexpr size_t sp_scratch_bytes() {
-    return (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4
+    return (size_t)SP_WAVES * (128 + 3 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 3 * SP_CAP) * 4
                                                                    : (size_t)64 * 65 * 8;
 }
-static_assert(sp_scratch_bytes() >= (size_t)SP_WAVES * (128 + 5 * SP_CAP) * 4, "per-wave scratch");
+static_assert(sp_scratch_bytes() >= (size_t)SP_WAVES * (128 + 3 * SP_CAP) * 4, "per-wave scratch");
 constexpr uint32_t SP_OWN = 0xFFFFFFFFu;  // w_b tag of a list entry that is a vertex's own row (b is never NaN)
 
 __device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, uint32_t w, float b) {
@@ -126,9 +126,6 @@ struct SparseArgs {
     uint32_t delta;              // bucket width in ns (0xFFFFFFFF = one bucket: plain Bellman-Ford)
     uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
-    unsigned long long* lmask;   // [gridDim.x][3][V] per-vertex lane masks (null = whole-row pulls): two
-                                 // sweep-parity buffers of "lanes changed since the last push" and the
-                                 // accumulator of lanes dropped but not yet pushed
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
@@ -142,26 +139,16 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
     return __builtin_nontemporal_load(p);
 }
 
-// Lane masks (a.lmask): a pull of arc (u, t) only needs the lanes whose label of u changed since
-// u was last pushed -- the other lanes already relaxed (u, t) with their current label of u when
-// it last changed (same argument as the vertex-level fprev skip, per lane).  The masked lanes
-// issue no memory request, so a row pull reads only the 128-B lines that hold changed lanes.
-//
 // Vertex bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
 // pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
 // sweep (the out-neighbours of changed vertices, pushed when a vertex changes).  A sweep
 // only visits marked vertices, 64 per wave step (one bitmap word pair).  The five bitmaps take
 // 5 V / 8 bytes: in LDS up to V ~ 190k (GB = false), beyond that in a per-workgroup global
 // slice (GB = true; the same accesses, separated by the same barriers, L2-resident).
-// Split labels (SPL): the slot holds a u32 latency array and a u32 loss-bits array instead of
-// packed u64 labels.  A pull reads the 256-B latency row; the source's loss is loaded (lane-
-// masked) only in lanes whose candidate latency does not exceed the target's latency at the
-// start of its group -- every other candidate loses the lexicographic min on latency alone.
-// The fold itself is unchanged (u64 keys rebuilt in registers), so the fixpoint is the same.
 // WPE = waves per SIMD the register budget is sized for: 8 (two 1024-thread workgroups per CU,
 // <= 64 VGPRs: the kernel spills ~90 B per lane to scratch) or 4 (one workgroup per CU, <= 128
 // VGPRs, no spills; SRG_OPT_SPARSE_WGS_PER_CU = 1).
-template <int G, bool GB, bool SPL, int WPE = 8>
+template <int G, bool GB, int WPE = 8>
 __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
@@ -174,37 +161,18 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
     unsigned long long* pend = mnext + nw;  // changed, but above the bucket bound: not pushed yet
     __shared__ uint32_t s_batch, s_changed, s_pend;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (5 x SP_CAP);
+    // per-wave scratch: vertex prefix/offsets (64 + 64) and the active-arc list (3 x SP_CAP);
     // the output transpose tile [64][65] u64 reuses the same region after convergence
     uint32_t* scratch = GB ? reinterpret_cast<uint32_t*>(smem_raw) : reinterpret_cast<uint32_t*>(pend + nw);
-    uint32_t* w_st = scratch + wave * (128 + 5 * SP_CAP);  // stride = sp_scratch_bytes() / SP_WAVES
+    uint32_t* w_st = scratch + wave * (128 + 3 * SP_CAP);  // stride = sp_scratch_bytes() / SP_WAVES
     uint32_t* w_lo = w_st + 64;
     uint32_t* w_u = w_lo + 64;
     uint32_t* w_w = w_u + SP_CAP;   // arc weight, or the window index of an own-row entry
     uint32_t* w_b = w_w + SP_CAP;   // 1 - arc loss, or SP_OWN
-    uint32_t* w_ml = w_b + SP_CAP;  // lane mask of the arc's source vertex (lanes 0-31 / 32-63)
-    uint32_t* w_mh = w_ml + SP_CAP;
-    const bool LM = a.lmask != nullptr;
-    unsigned long long* cmX = LM ? a.lmask + (size_t)blockIdx.x * 3 * V : nullptr;  // [2][V] by sweep parity
-    unsigned long long* cmP = LM ? cmX + 2 * (size_t)V : nullptr;                  // dropped, not yet pushed
-    unsigned long long lanes_loaded = 0;
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
     unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
-    uint32_t* Llat = reinterpret_cast<uint32_t*>(L);  // SPL: [V][64] latency, then [V][64] loss bits
-    uint32_t* Lls = Llat + (size_t)V * 64;
-    auto ld32 = [](const uint32_t* p) { return __builtin_nontemporal_load(p); };
-    auto st_label = [&](size_t idx, unsigned long long v) {
-        if constexpr (SPL) {
-            Llat[idx] = (uint32_t)(v >> 32);
-            Lls[idx] = (uint32_t)v;
-        } else {
-            L[idx] = v;
-        }
-    };
-    auto ld_full = [&](size_t idx) -> unsigned long long {
-        if constexpr (SPL) return ((unsigned long long)ld32(&Llat[idx]) << 32) | ld32(&Lls[idx]);
-        else return ld_label(&L[idx]);
-    };
+    auto st_label = [&](size_t idx, unsigned long long v) { L[idx] = v; };
+    auto ld_full = [&](size_t idx) -> unsigned long long { return ld_label(&L[idx]); };
     uint32_t max_sweeps = 0;
     unsigned long long evals = 0;
     uint32_t saturated = 0;  // a finite label + arc reached 2^32-1: INF may then mean "too long", not unreachable
@@ -235,15 +203,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
             pend[w] = 0;
         }
         if (threadIdx.x == 0) s_pend = 0;
-        uint32_t par = 0;  // sweep parity: pulls read cmX[par], pushes write cmX[par ^ 1]
-        if (LM) {
-            for (uint32_t v = threadIdx.x; v < V; v += SP_THREADS) cmP[v] = 0;
-            for (uint32_t q = wave; q < 64; q += SP_WAVES) {
-                const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)my_src, q);
-                const unsigned long long m = __ballot(my_src == sv);
-                if (lane == 0) cmX[sv] = m;
-            }
-        }
         // bucket bound (delta-stepping): a changed vertex is pushed to its out-neighbours only
         // once some lane's new latency is below the bound; the others wait in `pend` until the
         // bucket is exhausted and the bound moves on.  Any push order reaches the same unique
@@ -301,52 +260,9 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                     unsigned long long best = 0, old = 0;
                     for (uint32_t j0 = 0; j0 < cnt; j0 += G) {
                         unsigned long long row[G];
-                        if constexpr (SPL) {
-                            uint32_t rl[G], rs[G];
 #pragma unroll
-                            for (int q = 0; q < G; ++q)
-                                if (j0 + q < cnt) {
-                                    const uint32_t e = j0 + q;
-                                    const bool own = w_b[e] == SP_OWN;
-                                    bool need = true;
-                                    if (LM && !own) need = ((lane < 32 ? w_ml[e] : w_mh[e]) >> (lane & 31)) & 1u;
-                                    if (LM) lanes_loaded += need ? 1u : 0u;
-                                    const size_t idx = (size_t)w_u[e] * 64 + lane;
-                                    rl[q] = need ? ld32(&Llat[idx]) : 0xFFFFFFFFu;
-                                    rs[q] = own ? ld32(&Lls[idx]) : 0u;
-                                }
-                            // a candidate can only win if its latency is <= the target's latency at
-                            // the start of its group (best <= old): load the source's loss there only
-                            uint32_t olat = (uint32_t)(old >> 32);
-#pragma unroll
-                            for (int q = 0; q < G; ++q)
-                                if (j0 + q < cnt) {
-                                    const uint32_t e = j0 + q;
-                                    if (w_b[e] == SP_OWN) {
-                                        olat = rl[q];
-                                    } else if (rl[q] != 0xFFFFFFFFu) {
-                                        const uint32_t cl = __builtin_elementwise_add_sat(rl[q], w_w[e]);
-                                        saturated |= cl == 0xFFFFFFFFu;
-                                        if (cl != 0xFFFFFFFFu && cl <= olat)
-                                            rs[q] = ld32(&Lls[(size_t)w_u[e] * 64 + lane]);
-                                        else
-                                            rl[q] = 0xFFFFFFFFu;  // cannot win: an INF row in the fold
-                                    }
-                                }
-#pragma unroll
-                            for (int q = 0; q < G; ++q)
-                                row[q] = rl[q] == 0xFFFFFFFFu ? LBL_INF : ((unsigned long long)rl[q] << 32) | rs[q];
-                        } else {
-#pragma unroll
-                            for (int q = 0; q < G; ++q)
-                                if (j0 + q < cnt) {
-                                    bool need = true;
-                                    if (LM && w_b[j0 + q] != SP_OWN)
-                                        need = ((lane < 32 ? w_ml[j0 + q] : w_mh[j0 + q]) >> (lane & 31)) & 1u;
-                                    if (LM) lanes_loaded += need ? 1u : 0u;
-                                    row[q] = need ? ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]) : LBL_INF;
-                                }
-                        }
+                        for (int q = 0; q < G; ++q)
+                            if (j0 + q < cnt) row[q] = ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]);
 #pragma unroll
                         for (int q = 0; q < G; ++q) {
                             const uint32_t e = j0 + q;
@@ -357,7 +273,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                                     const unsigned long long dm = __ballot(best < old);
                                     if (dm) {
                                         if (best < old) st_label((size_t)(w * 64 + cur) * 64 + lane, best);
-                                        if (LM && lane == 0) atomicOr(&cmP[w * 64 + cur], dm);
                                         if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
                                             changed |= 1ull << cur;
                                         else
@@ -369,7 +284,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                             } else {
                                 const unsigned long long c =
                                     row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(tagb));
-                                if constexpr (!SPL) saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
+                                saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
                                 best = c < best ? c : best;
                                 ++evals;
                             }
@@ -379,7 +294,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                         const unsigned long long dm = __ballot(best < old);
                         if (dm) {
                             if (best < old) st_label((size_t)(w * 64 + cur) * 64 + lane, best);
-                            if (LM && lane == 0) atomicOr(&cmP[w * 64 + cur], dm);
                             if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
                                 changed |= 1ull << cur;
                             else
@@ -417,11 +331,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                         if (!(vi & 0x80000000u)) {
                             w_w[pos] = a.in_w[k];
                             w_b[pos] = __float_as_uint(a.in_b[k]);
-                            if (LM) {
-                                const unsigned long long mk = __builtin_nontemporal_load(&cmX[par * (size_t)V + u]);
-                                w_ml[pos] = (uint32_t)mk;
-                                w_mh[pos] = (uint32_t)(mk >> 32);
-                            }
                         } else {
                             w_w[pos] = k;  // window index of the vertex
                             w_b[pos] = SP_OWN;
@@ -462,11 +371,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                 // (4) mark the out-neighbours of the changed vertices for the next sweep
                 if (changed) {
                     if (lane == 0) atomicOr(&fcur[w], changed);
-                    if (LM) {  // their lanes changed since the last push -> the next sweep's pull masks
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if ((changed >> lane) & 1ull)
-                            cmX[(par ^ 1u) * (size_t)V + vl] = atomicExch(&cmP[vl], 0ull);
-                    }
                     chg = 1;
                     const bool ch = (changed >> lane) & 1ull;
                     uint32_t olo = lo, ohi = hi;
@@ -506,7 +410,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
             __syncthreads();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             ++sweeps;
-            par ^= 1u;
             const bool more = s_changed != 0;
             for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
                 fprev[w] = fcur[w];
@@ -534,7 +437,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                         const uint32_t b = (uint32_t)__builtin_ctzll(mk);
                         mk &= mk - 1;
                         push_out(w * 64 + b);
-                        if (LM && lane == 0) cmX[par * (size_t)V + w * 64 + b] = atomicExch(&cmP[w * 64 + b], 0ull);
                     }
                 }
                 __syncthreads();
@@ -581,11 +483,6 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
     if (threadIdx.x == 0) atomicMax(&a.flags[1], max_sweeps);
     if (__ballot(saturated) && lane == 0) atomicOr(&a.flags[5], 1u);
     if (lane == 0 && evals) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[2]), evals);
-    if (LM) {  // lanes actually loaded by arc pulls (diagnostics: flags[6..7])
-        unsigned long long tot = lanes_loaded;
-        for (int o = 32; o; o >>= 1) tot += __shfl_xor(tot, o, 64);
-        if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[6]), tot);
-    }
 }
 
 }  // namespace srg

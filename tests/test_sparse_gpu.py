@@ -34,28 +34,6 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[5]], ids=lambda k: f"V{k['V']}_s{k['seed']}")
-def test_bf_relabel_vs_oracle(bf_router, kw):
-    """The sparse path with degree-dealt vertex ids (SRG_OPT_SPARSE_RELABEL 1) against the oracle
-    (every other sparse test runs the default given ids)."""
-    kw = dict(kw)
-    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
-    g = synth.random_graph(V, dens, seed, **kw)
-    nodes = list(range(V))
-    bf_router.set_option(N.SRG_OPT_SPARSE_RELABEL, 1)
-    try:
-        lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
-    except oracle.OracleError as e:
-        with pytest.raises(NetGraphError) as ei:
-            bf_router.compute_shortest_paths(g, nodes)
-        assert ei.value.code == e.code
-        return
-    t = bf_router.compute_shortest_paths(g, nodes)
-    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
-    assert np.array_equal(t.latency_ns, lat)
-    assert bits_equal(t.packet_loss, loss)
-
-
 @pytest.mark.parametrize("kw", CASES, ids=lambda k: f"V{k['V']}_s{k['seed']}")
 def test_bf_random_vs_oracle(bf_router, kw):
     kw = dict(kw)
@@ -104,57 +82,6 @@ def test_bf_delta_buckets(bf_router, kw, div, all_lanes):
     t = bf_router.compute_shortest_paths(g, nodes)
     assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
-
-
-@pytest.mark.parametrize("lm,sl", [(1, 0), (0, 1), (1, 1)], ids=["lanemask", "split", "both"])
-@pytest.mark.parametrize("div", [0, 1, 4])
-@pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], dict(V=1000, density=0.01, seed=207, lat_hi=100, parallel=0.1)],
-                         ids=lambda k: f"V{k['V']}_s{k['seed']}")
-def test_bf_lane_masks(bf_router, kw, div, lm, sl):
-    """Lane-masked pulls (only the lanes whose label of the arc's source changed since its last
-    push are loaded) and split latency / loss labels (a source's loss is loaded only where its
-    candidate latency can still win) reach the same fixpoint bit for bit, with and without
-    delta buckets."""
-    bf_router.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, lm)
-    bf_router.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, sl)
-    bf_router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, div)
-    kw = dict(kw)
-    V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
-    g = synth.random_graph(V, dens, seed, **kw)
-    nodes = list(range(V))
-    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
-    t = bf_router.compute_shortest_paths(g, nodes)
-    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
-    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
-
-
-def test_bf_variants_c4_equal():
-    """C4 at full size: whole-row pulls, lane-masked pulls and split labels, with and without the
-    degree-dealt vertex relabeling, give identical 2.5e9-pair tables."""
-    import torch
-    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
-    V = 50000
-    dev = torch.device("cuda", 0)
-    e = synth.barabasi_albert(V, 4, seed=V)
-    dg = DeviceGraph(e)
-    nodes_t = torch.arange(V, dtype=torch.int32, device=dev)
-    ref = None
-    ol = torch.empty((V, V), dtype=torch.int64, device=dev)
-    os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
-    for lm, sl, rl in ((0, 0, 1), (1, 0, 1), (0, 1, 1), (1, 1, 1), (0, 0, 0)):
-        r = Router(0)
-        r.set_option(N.SRG_OPT_SPARSE_LANE_MASKS, lm)
-        r.set_option(N.SRG_OPT_SPARSE_SPLIT_LABELS, sl)
-        r.set_option(N.SRG_OPT_SPARSE_RELABEL, rl)
-        st = compute_shortest_paths_device(r, dg, nodes_t, ol, os_)
-        torch.cuda.synchronize()
-        assert st["path_kind"] == N.SRG_PATH_SPARSE_U32
-        if ref is None:
-            ref = (ol.clone(), os_.view(torch.int32).clone())
-        else:
-            assert torch.equal(ol, ref[0]), f"latency differs (lane masks {lm}, split {sl})"
-            assert torch.equal(os_.view(torch.int32), ref[1]), f"loss differs (lane masks {lm}, split {sl})"
-        r.close()
 
 
 @pytest.mark.parametrize("kw", [CASES[1], CASES[2], CASES[3], CASES[5]], ids=lambda k: f"V{k['V']}_s{k['seed']}")
