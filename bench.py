@@ -222,6 +222,241 @@ def init_strong_router(local, dev):
     return router, None
 
 
+def make_edges(args):
+    """The synthetic graph of the selected config (BASELINE.json configs; SURVEY §8d generators)."""
+    from shadow_amd import synth
+    V = args.vertices
+    seed = args.seed if args.seed is not None else V
+    if args.graph == "atlas":
+        edges = synth.atlas_like(V, seed=seed)
+        cname = {10000: "C3", 4096: "C2"}.get(V, "atlas")
+        gdesc = f"{cname} atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph"
+    elif args.graph == "complete":
+        seed = args.seed if args.seed is not None else 1001
+        edges = synth.complete_random(V, seed=seed)
+        gdesc = f"C1 complete_random({V}, seed={seed}): complete undirected graph, random latency/loss"
+    else:
+        edges = synth.barabasi_albert(V, 4, seed=seed)
+        gdesc = f"C4 barabasi_albert({V}, m=4, seed={seed}): sparse undirected graph"
+    if args.lat_scale != 1:
+        import numpy as np
+        edges.latency_ns = edges.latency_ns * np.uint64(args.lat_scale)
+        gdesc += f", latencies x{args.lat_scale}"
+    return edges, gdesc, seed
+
+
+def apply_options(router, args):
+    """Bench flags -> srg_set_option (Router and MultiRouter alike)."""
+    from shadow_amd import _native as N
+    if args.no_locality:
+        router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
+    if args.fw_tile:
+        router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
+    router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
+    for flag, opt in (("sparse_group", "SPARSE_GROUP"), ("sparse_delta_all", "SPARSE_DELTA_ALL"),
+                      ("sparse_delta_div", "SPARSE_DELTA_DIV"), ("fw_symmetric", "FW_SYMMETRIC"),
+                      ("chain_prio", "CHAIN_PRIO"), ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
+                      ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
+                      ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE")):
+        v = getattr(args, flag)
+        if v is not None:
+            router.set_option(getattr(N, "SRG_OPT_" + opt), v)
+
+
+def workload_key(args, V, seed, world):
+    return (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "")
+            + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
+            f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
+            f"w{args.sparse_wgs or 2}"
+            + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
+            + (f":n{world}" if world > 1 else "") + (f":sim{args.simulate_rank}" if args.simulate_rank else ""))
+
+
+def roofline_for(agg, kind, args, edges, V, wkey, sym):
+    """The dominant kernel's roofline from the HIP-event launch times the library recorded:
+    dense = the FW bulk tile kernel (VALU), sparse = k_sparse_bf (HBM)."""
+    if not agg.get("prof_launches"):
+        return None
+    avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
+    if kind == 3:
+        # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
+        # (SURVEY §8d): arcs*16 + (V+1)*4 + V*12
+        arcs = int(((edges.src != edges.dst).sum()) * (1 if edges.directed else 2))
+        per_src = arcs * 16 + (V + 1) * 4 + V * 12
+        srcs = agg["prof_relaxations"] / agg["prof_launches"]
+        achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = load_traffic("k_sparse_bf", wkey)
+        return {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford, delta-stepping buckets)",
+                "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
+                "bytes_per_source": per_src, "sources_per_launch": int(srcs), "traffic_source": tsrc,
+                # measured HBM bytes per launch over this run's launch time: the real HBM rate
+                "traffic_GBps": round(traffic / (avg_ms * 1e-3) / 1e9, 1) if traffic else None,
+                "workload_key": wkey}
+    relax = agg["prof_relaxations"] / agg["prof_launches"]
+    achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
+    traffic, tsrc = load_traffic("fw_product", wkey)
+    if sym:
+        kname = "fw_bulk_lb<128,16> (FW phase 3 over the stored tiles I <= J, operands from the pivot's line buffer, pair-packed)"
+    elif kind == 0:
+        kname = ("fw_product<u32,128,16,2> (FW phase 3, pair-packed, non-lookahead tiles)" if args.fw_packed else
+                 "fw_product<u32,128,32,0> (FW phase 3, add + min3, non-lookahead tiles)")
+    else:
+        kname = "fw_product<u64,64,32,0> (FW phase 3)"
+    r = {"bound": "valu", "kernel": kname, "achieved": round(achieved, 3),
+         "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
+         "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
+         "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
+         "ops_per_relaxation": OPS_PER_RELAX.get(kind, 2.0), "relax_per_s": round(relax / (avg_ms * 1e-3), 1),
+         "traffic_source": tsrc, "workload_key": wkey}
+    if kind == 0 and args.fw_packed:
+        # v_min* issue at half rate on gfx950: the pair-packed relaxation pair (v_lshl_add_u64 +
+        # v_min3_u32) measured 0.187 wave-instr/SIMD/cycle = 2 relaxations per 10.7 cycles per
+        # wave = 0.748 of the 2-op lane peak (profiles/r01_valu_rate_microbench.txt)
+        r["instruction_mix_ceiling_frac"] = 0.748
+        r["frac_of_mix_ceiling"] = round(achieved / VALU_PEAK_TOPS / 0.748, 4)
+    return r
+
+
+def verify_rows(edges, table_lat, table_loss, V, k=4, seed=4242):
+    """k seeded rows of the benchmarked table against the oracle (outside the timed region)."""
+    import numpy as np
+    import oracle
+    rows = np.random.default_rng(seed).choice(V, size=k, replace=False).tolist()
+    dense = edges.num_edges * 8 > V * V
+    lat, loss = oracle.compute_shortest_paths(edges.as_tuple(), list(range(V)), rows=rows, mode=2 if dense else 1,
+                                              nthreads=cpu_info()["threads"])
+    ok = np.array_equal(table_lat[rows], lat) and np.array_equal(table_loss[rows].view(np.uint32), loss.view(np.uint32))
+    return {"rows": rows, "bit_exact": bool(ok)}
+
+
+def cold_call(make, args, edges, V):
+    """srg_create (or srg_multi_create) + the first srg_compute_shortest_paths on freshly
+    allocated, never-touched output arrays -- what Shadow's one call per simulation pays
+    (sim_config.rs:137-141; the Rust binding's vec![0u64; n*n] is lazily zeroed memory)."""
+    import numpy as np
+    t0 = time.perf_counter()
+    router = make()
+    apply_options(router, args)
+    lat = np.empty((V, V), dtype=np.uint64)   # not pre-faulted
+    loss = np.empty((V, V), dtype=np.float32)
+    router.compute_shortest_paths(edges, np.arange(V, dtype=np.uint32), lat, loss)
+    ms = (time.perf_counter() - t0) * 1e3
+    del lat, loss
+    return router, ms
+
+
+def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg, extra):
+    n = args.steps
+    brk = ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")
+    entry_desc = ("host entry srg_compute_shortest_paths: host edge list in, host n x n table out "
+                  "(H2D + kernels + D2H in the step)" if args.entry == "host" else
+                  "device entry srg_compute_shortest_paths_device: edge list resident in HBM, table left in HBM")
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "source-SSSPs/s", "n_gpus": world, "steps": n,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+        "dtype": "u64+f32" if kind == 1 else "u32+f32", "data": "synthetic",
+        "config": {"workload": f"{gdesc}, all {V} nodes used, {entry_desc}", "entry": args.entry, "vertices": V,
+                   "edges": int(edges.num_edges), "global_batch": V,
+                   "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind)), **extra_cfg},
+        "apsp_wall_ms": round(ms_per_step, 3),
+        "ms_h2d": round(agg.get("ms_h2d", 0) / n, 3), "ms_d2h": round(agg.get("ms_d2h", 0) / n, 3),
+        "d2h_overlapped_GB": round(agg.get("d2h_overlapped_bytes", 0) / n / 1e9, 3),
+        "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
+        "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
+        "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
+        "roofline": roofline, "cpu_baseline": cpu, **extra,
+    }
+    print(json.dumps(line), flush=True)
+
+
+def run_steps(step, args, label):
+    s = None
+    for i in range(args.warmup):
+        s = step()
+        log(f"[{label}] warmup {i}: {s['ms_total']:.2f} ms (h2d {s['ms_h2d']:.2f}, build {s['ms_build']:.2f}, "
+            f"fw/bf {s['ms_fw']:.2f}, scan {s['ms_scan']:.2f}, loss {s['ms_loss']:.2f}, exchange {s['ms_exchange']:.2f}, "
+            f"d2h {s['ms_d2h']:.2f}; kind {s['path_kind']}, ess {s['essential_edges']}, local {s['local_sources']})")
+    return s
+
+
+def bench_multi(args):
+    """--gpus N without a launcher: ONE process drives N GPUs through srg_multi (Shadow's one-process
+    model, manager.rs:301-324): one RoutingInfo per step, the whole n x n table in one host array,
+    every GPU shipping its own sources' rows over its own PCIe link."""
+    import numpy as np
+    import torch
+    from shadow_amd import MultiRouter
+    from shadow_amd import _native as N
+    G = args.gpus
+    have = torch.cuda.device_count()
+    if have < G:
+        print(f"bench.py --gpus {G}: only {have} HIP device(s) visible; refusing to run {G} ranks on fewer GPUs",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.entry != "host":
+        print("bench.py --gpus N (one process): only the host entry is supported", file=sys.stderr, flush=True)
+        sys.exit(2)
+    edges, gdesc, seed = make_edges(args)
+    V = args.vertices
+    log(f"[multi{G}] generated {gdesc}: {edges.num_edges} edges")
+    router, cold_ms = cold_call(lambda: MultiRouter(list(range(G))), args, edges, V)
+    log(f"[multi{G}] cold call (srg_multi_create + first call, unfaulted outputs): {cold_ms:.1f} ms")
+    h_nodes = np.arange(V, dtype=np.uint32)
+    h_lat = np.zeros((V, V), dtype=np.uint64)
+    h_loss = np.zeros((V, V), dtype=np.float32)
+    h_lat.fill(0)  # fault the pages in once: the caller's Vecs are already allocated
+    h_loss.fill(0)
+
+    def step():
+        return router.compute_shortest_paths(edges, h_nodes, h_lat, h_loss).stats
+
+    s = run_steps(step, args, f"multi{G}")
+    router.set_option(N.SRG_OPT_PROFILING, 0 if args.no_profile else 1)
+    for d in range(G):
+        torch.cuda.synchronize(d)
+    agg = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = step()
+        for k, v in s.items():
+            if isinstance(v, (int, float)):
+                agg[k] = agg.get(k, 0) + v
+    elapsed = time.perf_counter() - t0
+    ms = elapsed * 1e3 / args.steps
+    kind = s["path_kind"]
+    ver = verify_rows(edges, h_lat, h_loss, V) if not args.no_verify else None
+    roof = roofline_for(agg, kind, args, edges, V, workload_key(args, V, seed, G), kind == 0 and args.fw_packed
+                        and args.fw_symmetric != 0 and not edges.directed)
+    emit(args, V, gdesc, edges, kind, G, G and V * args.steps / elapsed, ms, agg, s, roof, None,
+         {"parallelism": f"multi{G} (one process, srg_multi: in-process group, pull collectives over xGMI)",
+          "output": "full table in one host array (each GPU writes its sources' rows over its own PCIe link)",
+          "cold_call_ms": round(cold_ms, 1)},
+         {"verified_rows": ver})
+
+
+def shared_table(V, rank, tag):
+    """The n x n output as ONE host table shared by every rank's process (POSIX shm): each GPU
+    writes its own sources' rows into it over its own PCIe link, so rank 0 ends with the whole
+    RoutingInfo in its address space."""
+    import mmap
+    import numpy as np
+    import torch.distributed as dist
+    path = f"/dev/shm/srg_bench_{tag}"
+    nbytes = V * V * 12
+    if rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(nbytes)
+    dist.barrier()
+    fd = os.open(path, os.O_RDWR)
+    mm = mmap.mmap(fd, nbytes)
+    os.close(fd)
+    lat = np.frombuffer(mm, dtype=np.uint64, count=V * V).reshape(V, V)
+    loss = np.frombuffer(mm, dtype=np.float32, count=V * V, offset=V * V * 8).reshape(V, V)
+    return path, mm, lat, loss
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,6 +470,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="skip the 4 oracle rows checked after the timed steps")
     ap.add_argument("--graph", choices=["atlas", "complete", "ba", "events"], default="atlas",
                     help="atlas = C3 (headline; C2 with --vertices 4096), complete = C1, ba = C4, "
                          "events = C5 stretch (10^7 packet events)")
@@ -244,7 +480,6 @@ def main():
                     help="host = srg_compute_shortest_paths (host edge list in, host table out: H2D + D2H "
                          "included); device = srg_compute_shortest_paths_device (inputs/outputs in HBM)")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
-    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the output-row exchange (the default)")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: every rank ends with the whole table (RCCL row exchange; host entry: all rows D2H)")
     ap.add_argument("--sparse-group", type=int, default=None, help="sparse: label rows in flight per wave (4/8)")
@@ -282,6 +517,7 @@ def main():
         # benchmarked device-resident by default (a host copy of it is 0.5 s of PCIe alone).
         args.entry = "device" if args.graph == "ba" else "host"
 
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -289,6 +525,8 @@ def main():
         return bench_events(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1:
+        return bench_multi(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -296,33 +534,15 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from shadow_amd import Router, synth
+    from shadow_amd import Router
     from shadow_amd import _native as N
     from shadow_amd.device import DeviceGraph, compute_shortest_paths_device, set_profiling
 
     V = args.vertices
-    seed = args.seed if args.seed is not None else V
     t0 = time.time()
-    if args.graph == "atlas":
-        edges = synth.atlas_like(V, seed=seed)
-        cname = {10000: "C3", 4096: "C2"}.get(V, "atlas")
-        gdesc = f"{cname} atlas_like({V}, seed={seed}): complete undirected GML-equivalent graph"
-    elif args.graph == "complete":
-        seed = args.seed if args.seed is not None else 1001
-        edges = synth.complete_random(V, seed=seed)
-        gdesc = f"C1 complete_random({V}, seed={seed}): complete undirected graph, random latency/loss"
-    else:
-        edges = synth.barabasi_albert(V, 4, seed=seed)
-        gdesc = f"C4 barabasi_albert({V}, m=4, seed={seed}): sparse undirected graph"
-    if args.lat_scale != 1:
-        import numpy as np
-        edges.latency_ns = edges.latency_ns * np.uint64(args.lat_scale)
-        gdesc += f", latencies x{args.lat_scale}"
+    edges, gdesc, seed = make_edges(args)
     log(f"[rank {rank}] generated {gdesc}: {edges.num_edges} edges in {time.time()-t0:.1f}s")
-    dg = DeviceGraph(edges, dev)
-    nodes = torch.arange(V, dtype=torch.int32, device=dev)
-    out_lat = torch.empty((V, V), dtype=torch.int64, device=dev)
-    out_loss = torch.empty((V, V), dtype=torch.float32, device=dev)
+    cold_ms = None
     strong = world > 1 and not args.replicas
     fallback = None
     if strong:
@@ -330,69 +550,49 @@ def main():
         if router is None:
             log(f"[rank {rank}] multi-rank build unavailable ({fallback}): running independent replicas")
             strong = False
-        elif not args.gather:
-            # the row-distributed table: each rank's output holds the rows of the sources it
-            # routes (the layout one Shadow process driving N GPUs through an in-process rank
-            # group, srg_comm_init_local, writes into its single array); --gather replicates it
-            router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
+        else:
+            apply_options(router, args)
+            if not args.gather:
+                # each rank routes the sources at positions [n r/N, n (r+1)/N) and writes those rows
+                # into the ONE host table all ranks share (shared_table); --gather instead runs the
+                # RCCL row exchange so that every rank's own array holds the whole table
+                router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
     if not strong:
-        router = Router(local)
-    if args.no_locality:
-        router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
-    if args.fw_tile:
-        router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
-    router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
-    if args.sparse_group is not None:
-        router.set_option(N.SRG_OPT_SPARSE_GROUP, args.sparse_group)
-    if args.sparse_delta_all is not None:
-        router.set_option(N.SRG_OPT_SPARSE_DELTA_ALL, args.sparse_delta_all)
-    if args.sparse_delta_div is not None:
-        router.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, args.sparse_delta_div)
-    if args.fw_symmetric is not None:
-        router.set_option(N.SRG_OPT_FW_SYMMETRIC, args.fw_symmetric)
-    if args.chain_prio is not None:
-        router.set_option(N.SRG_OPT_CHAIN_PRIO, args.chain_prio)
-    if args.sparse_wgs is not None:
-        router.set_option(N.SRG_OPT_SPARSE_WGS_PER_CU, args.sparse_wgs)
-    if args.h2d_codec is not None:
-        router.set_option(N.SRG_OPT_H2D_CODEC, args.h2d_codec)
-    if args.late_loss is not None:
-        router.set_option(N.SRG_OPT_LATE_LOSS, args.late_loss)
-    if args.edge_shard is not None:
-        router.set_option(N.SRG_OPT_EDGE_SHARD, args.edge_shard)
-    if args.scan_groups is not None:
-        router.set_option(N.SRG_OPT_SCAN_GROUPS, args.scan_groups)
-    if args.loss_chunks is not None:
-        router.set_option(N.SRG_OPT_LOSS_CHUNKS, args.loss_chunks)
-    if args.d2h_mode is not None:
-        router.set_option(N.SRG_OPT_D2H_MODE, args.d2h_mode)
+        if args.entry == "host" and not args.simulate_rank:
+            router, cold_ms = cold_call(lambda: Router(local), args, edges, V)
+            log(f"[rank {rank}] cold call (srg_create + first call, unfaulted outputs): {cold_ms:.1f} ms")
+        else:
+            router = Router(local)
+            apply_options(router, args)
     if args.simulate_rank:
         sg, sr = (int(x) for x in args.simulate_rank.split(":"))
         router.set_option(N.SRG_OPT_SIMULATE_RANK, sg * 1000 + sr)
         if not args.gather:  # as the N > 1 default: this rank's rows only
             router.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
-
+    dg = DeviceGraph(edges, dev)
+    nodes = torch.arange(V, dtype=torch.int32, device=dev)
+    shm = None
     if args.entry == "host":
-        import numpy as np
         h_nodes = np.arange(V, dtype=np.uint32)
-        h_lat = np.empty((V, V), dtype=np.uint64)
-        h_loss = np.empty((V, V), dtype=np.float32)
+        if strong and not args.gather:
+            shm = shared_table(V, rank, os.environ.get("MASTER_PORT", "0"))
+            h_lat, h_loss = shm[2], shm[3]
+        else:
+            h_lat = np.empty((V, V), dtype=np.uint64)
+            h_loss = np.empty((V, V), dtype=np.float32)
         h_lat.fill(0)  # fault the pages in once: the caller's Vecs are already allocated
         h_loss.fill(0)
 
         def step():
             return router.compute_shortest_paths(edges, h_nodes, h_lat, h_loss).stats
     else:
+        out_lat = torch.empty((V, V), dtype=torch.int64, device=dev)
+        out_loss = torch.empty((V, V), dtype=torch.float32, device=dev)
+
         def step():
             return compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
 
-    for i in range(args.warmup):
-        s = step()
-        log(f"[rank {rank}] warmup {i}: {s['ms_total']:.2f} ms (build {s['ms_build']:.2f}, fw/bf {s['ms_fw']:.2f}, "
-            f"scan {s['ms_scan']:.2f}, loss {s['ms_loss']:.2f}, extract {s['ms_extract']:.2f}, "
-            f"exchange {s['ms_exchange']:.2f}; rounds {s['loss_rounds']}, multi {s['multi_pred_pairs']}, "
-            f"kind {s['path_kind']}, ess {s['essential_edges']} ({s['essential_edges'] / V / V:.3f} of V^2), "
-            f"scan_kind {s['scan_kind']}, relax {s['relaxations']}, local {s['local_sources']})")
+    s = run_steps(step, args, f"rank {rank}")
     set_profiling(router, not args.no_profile)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -414,6 +614,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        for k in ("prof_launches", "prof_kernel_ms", "prof_relaxations"):  # the dominant kernel over all ranks
+            t = torch.tensor([float(agg.get(k, 0))], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            agg[k] = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
     value = (1 if strong else world) * V * args.steps / elapsed
 
@@ -422,106 +626,61 @@ def main():
     # alone, reported beside the host-entry headline
     dev_ms = None
     if args.entry == "host" and world == 1 and not args.simulate_rank:
+        ol = torch.empty((V, V), dtype=torch.int64, device=dev)
+        os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         for _ in range(2):
-            compute_shortest_paths_device(router, dg, nodes, out_lat, out_loss)
+            compute_shortest_paths_device(router, dg, nodes, ol, os_)
         torch.cuda.synchronize(dev)
         dev_ms = (time.perf_counter() - t1) * 1e3 / 2
-    wkey = (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "") + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
-            f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
-            f"w{args.sparse_wgs or 2}"
-            + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
-            + (f":n{world}" if world > 1 else "") + (f":sim{args.simulate_rank}" if args.simulate_rank else ""))
-    roofline = None
-    if agg.get("prof_launches") and kind == 3:
-        # sparse: HBM-bound; algorithmic bytes per source = one CSR sweep + one result row
-        # (SURVEY §8d): arcs*16 + (V+1)*4 + V*12
-        arcs = int(((edges.src != edges.dst).sum()) * (1 if edges.directed else 2))
-        per_src = arcs * 16 + (V + 1) * 4 + V * 12
-        avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
-        srcs = agg["prof_relaxations"] / agg["prof_launches"]
-        achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic("k_sparse_bf", wkey)
-        roofline = {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford, delta-stepping buckets)",
-                    "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                    "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
-                    "bytes_per_source": per_src, "sources_per_launch": int(srcs), "traffic_source": tsrc,
-                    # measured HBM bytes per launch over this run's launch time: the real HBM rate
-                    "traffic_GBps": round(traffic / (avg_ms * 1e-3) / 1e9, 1) if traffic else None,
-                    "workload_key": wkey}
-    elif agg.get("prof_launches"):
-        avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]
-        relax = agg["prof_relaxations"] / agg["prof_launches"]
-        achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
-        traffic, tsrc = load_traffic("fw_product", wkey)
-        sym = (kind == 0 and args.fw_packed and args.fw_symmetric != 0 and not edges.directed and world == 1
-               and not args.simulate_rank)
-        if sym:
-            kname = "fw_product_sym<128,16> (FW phase 3 over the stored tiles I <= J of the symmetric D, pair-packed)"
-        elif kind == 0:
-            kname = (f"fw_product<u32,128,{16 if args.fw_packed >= 2 else 32},{args.fw_packed}> (FW phase 3, pair-packed, "
-                     "non-lookahead tiles)" if args.fw_packed else
-                     "fw_product<u32,128,32,0> (FW phase 3, add + min3, non-lookahead tiles)")
-        else:
-            kname = "fw_product<u64,64,32,0> (FW phase 3)"
-        roofline = {"bound": "valu", "kernel": kname, "achieved": round(achieved, 3),
-                    "peak": round(VALU_PEAK_TOPS, 3), "unit": "TOP/s (int32 VALU lane-ops)",
-                    "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
-                    "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
-                    "ops_per_relaxation": OPS_PER_RELAX.get(kind, 2.0), "relax_per_s": round(relax / (avg_ms * 1e-3), 1),
-                    "traffic_source": tsrc, "workload_key": wkey}
-        if kind == 0 and args.fw_packed:
-            # v_min* issue at half rate on gfx950: the pair-packed relaxation pair (v_lshl_add_u64 +
-            # v_min3_u32) measured 0.187 wave-instr/SIMD/cycle = 2 relaxations per 10.7 cycles per
-            # wave = 0.748 of the 2-op lane peak (profiles/r01_valu_rate_microbench.txt)
-            roofline["instruction_mix_ceiling_frac"] = 0.748
-            roofline["frac_of_mix_ceiling"] = round(achieved / VALU_PEAK_TOPS / 0.748, 4)
+        del ol, os_
+    wkey = workload_key(args, V, seed, world)
+    sym = (kind == 0 and args.fw_packed and args.fw_symmetric != 0 and not edges.directed)
+    roofline = roofline_for(agg, kind, args, edges, V, wkey, sym)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and not args.simulate_rank:
-        cpu = cpu_baselines(edges, args.cpu_seconds, gdesc.split(":")[0])
-
-    brk = ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")
     if args.simulate_rank:
         n = args.steps
-        print(json.dumps({"diagnostic": "simulated rank (collectives elided, outputs invalid)",
+        brk = ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")
+        print(json.dumps({"diagnostic": "simulated rank (no data exchanged, outputs invalid; every collective costs "
+                                        "the modelled xGMI time, comm.hip ModelComm)",
                           "simulate_rank": args.simulate_rank, "ms_per_step": round(ms_per_step, 3),
+                          "model": {"coll_us": float(os.environ.get("SRG_SIM_COLL_US", 15)),
+                                    "link_GBps": float(os.environ.get("SRG_SIM_LINK_GBPS", 64))},
                           "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
                           "roofline": roofline}), flush=True)
         return
-    if rank == 0:
-        n = args.steps
-        entry_desc = ("host entry srg_compute_shortest_paths: host edge list in, host n x n table out "
-                      "(H2D + kernels + D2H in the step)" if args.entry == "host" else
-                      "device entry srg_compute_shortest_paths_device: edge list resident in HBM, table left in HBM")
-        line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "source-SSSPs/s", "n_gpus": world, "steps": n,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "strong" if strong else "weak", "vs_baseline": None,
-            "dtype": "u64+f32" if kind == 1 else "u32+f32",
-            "data": "synthetic",
-            "config": {"workload": f"{gdesc}, all {V} nodes used, {entry_desc}",
-                       "entry": args.entry, "vertices": V, "edges": int(edges.num_edges), "global_batch": V,
-                       "parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single",
-                       **({"output": "row-distributed (each rank holds its sources' rows)" if not args.gather
-                           else "gathered (every rank holds the whole table)"} if strong else {}),
-                       **({"edge_list": "sharded (1/N over each PCIe link, exchanged between GPUs)"
-                           if (args.edge_shard == 1 or (args.edge_shard in (None, -1) and world >= 4))
-                           else "whole list over each PCIe link"} if strong and args.entry == "host" else {}),
-                       **({"fallback": fallback} if fallback else {}),
-                       "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind))},
-            "apsp_wall_ms": round(ms_per_step, 3),
-            "ms_h2d": round(agg.get("ms_h2d", 0) / n, 3), "ms_d2h": round(agg.get("ms_d2h", 0) / n, 3),
-            "d2h_overlapped_GB": round(agg.get("d2h_overlapped_bytes", 0) / n / 1e9, 3),
-            "device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None,
-            "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
-            "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
-            "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
-            "roofline": roofline, "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baselines(edges, args.cpu_seconds, gdesc.split(":")[0])
+    ver = None
     if world > 1:
+        dist.barrier()  # every rank's rows are in the shared table
+    if rank == 0 and args.entry == "host" and not args.no_verify:
+        ver = verify_rows(edges, h_lat, h_loss, V)
+    if rank == 0:
+        extra_cfg = {"parallelism": (f"rowblock{world}+rccl" if strong else f"replicas{world}") if world > 1 else "single"}
+        if strong:
+            extra_cfg["output"] = ("full table in one host array: POSIX shm shared by the N processes, each GPU "
+                                   "writing its sources' rows over its own PCIe link" if not args.gather
+                                   else "gathered (every rank's own array holds the whole table)")
+            if args.entry == "host":
+                extra_cfg["edge_list"] = ("sharded (1/N over each PCIe link, exchanged between GPUs)"
+                                          if (args.edge_shard == 1 or (args.edge_shard in (None, -1) and world >= 4))
+                                          else "whole list over each PCIe link")
+        if fallback:
+            extra_cfg["fallback"] = fallback
+        if cold_ms is not None:
+            extra_cfg["cold_call_ms"] = round(cold_ms, 1)
+        emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg,
+             {"device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None, "verified_rows": ver})
+    if world > 1:
+        dist.barrier()
+        if shm is not None and rank == 0:
+            try:
+                os.unlink(shm[0])
+            except OSError:
+                pass
         dist.destroy_process_group()
 
 

@@ -168,6 +168,8 @@ void srg_destroy(srg_ctx* ctx);
                                      * and latencies, on their own stream beside the W build and FW (which
                                      * need no loss); 0 = with them */
 int srg_set_option(srg_ctx* ctx, int option, double value);
+/* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
+int srg_get_option(srg_ctx* ctx, int option, double* value);
 
 /* Replaces NetworkGraph::compute_shortest_paths (mod.rs:183-228).
  * Host pointers in, host pointers out.  out_* are caller-allocated num_nodes^2.
@@ -207,6 +209,11 @@ typedef struct srg_routing_info srg_routing_info;
 int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
                            int use_shortest_paths, srg_routing_info** out, srg_stats* stats,
                            char* errbuf, size_t errlen);
+/* The same, built by every GPU of an srg_multi (declared below). */
+struct srg_multi;
+int srg_routing_info_build_multi(struct srg_multi* m, const srg_edge_list* graph, const uint32_t* gml_ids,
+                                 uint32_t num_ids, int use_shortest_paths, srg_routing_info** out, srg_stats* stats,
+                                 char* errbuf, size_t errlen);
 void srg_routing_info_free(srg_routing_info* ri);
 uint32_t srg_routing_info_num_nodes(const srg_routing_info* ri);
 /* RoutingInfo::path (mod.rs:444-446): 1 and the path's properties, or 0 (None).              */
@@ -264,6 +271,29 @@ int srg_local_group_create(int nranks, srg_local_group** out);
 void srg_local_group_release(srg_local_group* g);
 int srg_comm_init_local(srg_ctx* ctx, srg_local_group* g, int rank, char* errbuf, size_t errlen);
 int srg_comm_size(srg_ctx* ctx, int* nranks, int* rank);
+
+/* ---- several GPUs behind ONE call (Shadow's one-process model) ------------------------
+ * Shadow builds RoutingInfo once, in one process (sim_config.rs:137-141 -> manager.rs:301-324),
+ * so the drop-in for a multi-GPU node is one object driving N devices: one context per device in
+ * an in-process group (collectives are pull kernels over xGMI, peer access enabled), one worker
+ * thread per rank.  srg_multi_compute_shortest_paths has exactly srg_compute_shortest_paths'
+ * arguments and results: the whole n x n table lands in the caller's two arrays, every GPU
+ * shipping its own sources' rows over its own PCIe link.  stats: wall times of the slowest
+ * rank, counts summed over ranks, nranks = N.  A device may be listed more than once (several
+ * ranks sharing one GPU: how the one-GPU test box exercises this path).                     */
+typedef struct srg_multi srg_multi;
+int srg_multi_create(srg_multi** out, const int* devices, int num_devices, char* errbuf, size_t errlen);
+void srg_multi_destroy(srg_multi* m);
+int srg_multi_size(const srg_multi* m);
+/* srg_set_option on every rank (SRG_OPT_GATHER_OUTPUT and SRG_OPT_SIMULATE_RANK are fixed: ERR_ARG) */
+int srg_multi_set_option(srg_multi* m, int option, double value);
+int srg_multi_compute_shortest_paths(srg_multi* m, const srg_edge_list* graph, const uint32_t* nodes,
+                                     uint32_t num_nodes, uint64_t* out_latency_ns, float* out_packet_loss,
+                                     srg_stats* stats, char* errbuf, size_t errlen);
+/* get_direct_paths (use_shortest_path = false) on the first device: an n^2 gather, no SSSP work */
+int srg_multi_get_direct_paths(srg_multi* m, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
+                               uint64_t* out_latency_ns, float* out_packet_loss, srg_stats* stats, char* errbuf,
+                               size_t errlen);
 
 /* ---- stretch: one round's cross-host packet-event batch ---------------
  * Replaces, for a whole batch at once, the per-packet tail of Worker::send_packet

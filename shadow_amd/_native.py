@@ -148,6 +148,8 @@ EXPORTS = [
     "srg_order_packet_events_device", "srg_routing_info_build", "srg_routing_info_free", "srg_routing_info_num_nodes",
     "srg_routing_info_path", "srg_routing_info_increment_packet_count", "srg_routing_info_packet_count",
     "srg_routing_info_smallest_latency_ns", "srg_routing_info_tables",
+    "srg_multi_create", "srg_multi_destroy", "srg_multi_size", "srg_multi_set_option", "srg_multi_compute_shortest_paths",
+    "srg_multi_get_direct_paths", "srg_routing_info_build_multi", "srg_get_option",
 ]
 
 _lib = None
@@ -244,6 +246,23 @@ def lib():
     L.srg_routing_info_tables.restype = None
     L.srg_routing_info_tables.argtypes = [c.c_void_p, c.POINTER(_u64p), c.POINTER(_f32p), c.POINTER(_u32p),
                                           c.POINTER(c.c_uint32)]
+    L.srg_multi_create.restype = c.c_int
+    L.srg_multi_create.argtypes = [c.POINTER(c.c_void_p), c.c_void_p, c.c_int, c.c_char_p, c.c_size_t]
+    L.srg_multi_destroy.restype = None
+    L.srg_multi_destroy.argtypes = [c.c_void_p]
+    L.srg_multi_size.restype = c.c_int
+    L.srg_multi_size.argtypes = [c.c_void_p]
+    L.srg_multi_set_option.restype = c.c_int
+    L.srg_multi_set_option.argtypes = [c.c_void_p, c.c_int, c.c_double]
+    L.srg_multi_compute_shortest_paths.restype = c.c_int
+    L.srg_multi_compute_shortest_paths.argtypes = host_sig
+    L.srg_multi_get_direct_paths.restype = c.c_int
+    L.srg_multi_get_direct_paths.argtypes = host_sig
+    L.srg_routing_info_build_multi.restype = c.c_int
+    L.srg_routing_info_build_multi.argtypes = [c.c_void_p, c.POINTER(EdgeList), c.c_void_p, c.c_uint32, c.c_int,
+                                               c.POINTER(c.c_void_p), c.POINTER(Stats), c.c_char_p, c.c_size_t]
+    L.srg_get_option.restype = c.c_int
+    L.srg_get_option.argtypes = [c.c_void_p, c.c_int, c.POINTER(c.c_double)]
     L.srg_comm_size.restype = c.c_int
     L.srg_comm_size.argtypes = [c.c_void_p, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     _lib = L

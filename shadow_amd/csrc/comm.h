@@ -17,9 +17,15 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <stdexcept>
 #include <string>
 
 namespace srg {
+
+// a collective failed (RCCL error, or a peer rank of an in-process group failed): SRG_ERR_RCCL
+struct CommError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
 
 struct Comm {
     int rank = 0, nranks = 1;
@@ -35,7 +41,8 @@ struct Comm {
 std::string rccl_unique_id(unsigned char out[128]);
 std::string rccl_create(int nranks, int rank, const unsigned char id[128], int device, Comm** out);
 
-// Timing aid: collectives are no-ops (results invalid), see SRG_OPT_SIMULATE_RANK.
+// Timing aid: collectives move nothing (results invalid) but cost the modelled xGMI time on the
+// stream, see SRG_OPT_SIMULATE_RANK and DESIGN.md §7.
 Comm* null_create(int nranks, int rank);
 
 // In-process group of `nranks` ranks (threads of one process); each rank attaches one context.
@@ -43,5 +50,8 @@ struct LocalGroup;
 LocalGroup* local_group_create(int nranks);
 void local_group_release(LocalGroup* g);  // refcounted: the group and each attached comm
 std::string local_create(LocalGroup* g, int rank, int device, Comm** out);
+// a rank failed outside the collective protocol: every barrier of the group throws until reset
+void local_group_abort(LocalGroup* g);
+void local_group_reset(LocalGroup* g);
 
 }  // namespace srg

@@ -119,7 +119,7 @@ struct P1Geo {
 };
 
 template <class K, int T, int NTH = 512>
-__global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, int kb, int prio) {
+__device__ __forceinline__ void phase1_body(K* __restrict__ base, size_t ld, int prio) {
     // prio: the chain runs beside the bulk tiles; a raised wave priority wins the VALU issue
     // arbitration on the SIMDs it shares with them (MI355X_MICROARCH.md, waves per SIMD)
     if (prio) __builtin_amdgcn_s_setprio(3);
@@ -130,7 +130,6 @@ __global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, i
     __shared__ __attribute__((aligned(16))) K prow[2][R][T];  // prow[.][j][col] = D[k0+j][col]
     __shared__ __attribute__((aligned(16))) K pcol[2][R][T];  // pcol[.][j][row] = D[row][k0+j]
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-    K* base = D + (size_t)kb * T * ld + (size_t)kb * T;
     K c[MR][MC];
 #pragma unroll
     for (int a = 0; a < MR; ++a)
@@ -213,6 +212,17 @@ __global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, i
             for (int e = 0; e < HC; ++e) v.v[e] = c[a][h * HC + e];
             stv<K, HC>(base + (size_t)G::row(ty, a) * ld + G::col(tx, h * HC), v);
         }
+}
+
+template <class K, int T, int NTH = 512>
+__global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, int kb, int prio) {
+    phase1_body<K, T, NTH>(D + (size_t)kb * T * ld + (size_t)kb * T, ld, prio);
+}
+
+// close the T x T tile at `base` (row stride ld): the pivot tile inside a line buffer
+template <class K, int T, int NTH = 512>
+__global__ void __launch_bounds__(NTH) fw_close_at(K* __restrict__ base, size_t ld, int prio) {
+    phase1_body<K, T, NTH>(base, ld, prio);
 }
 
 // Stage a KC x T chunk of A^T (A rows i, columns k0..k0+KC) and of B (rows k0.., cols j)
@@ -538,39 +548,29 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
 }
 
 // ---------------------------------------------------------------------------------------
-// Symmetric FW (undirected graph, one rank).  W is symmetric, and so is D after every FW step
-// (D[i][j] = min(D[i][j], D[i][k] + D[k][j]) maps symmetric to symmetric), so only the tiles
-// (I <= J) are updated; the lower triangle is mirrored once after the last pivot.  Operands:
-//     A = D[I][kb] = tile (I, kb) if I <= kb, else tile (kb, I) read transposed
-//     B = D[kb][J] = tile (kb, J) if kb <= J, else tile (J, kb) read transposed
-// An operand is staged from either layout into the same k-pair LDS image:
+// Symmetric FW over line buffers (undirected graphs; one or several ranks).  W is symmetric, and
+// so is D after every FW step (D[i][j] = min(D[i][j], D[i][k] + D[k][j]) maps symmetric to
+// symmetric), so only the stored tiles (I <= J) of the row-major D are updated; the lower
+// triangle is filled once at the end (mirror, or the multi-rank unpack).
+// Every product reads its operands from the LINE BUFFER of the pivot L: nb tiles of T x T (row
+// stride T), tile j = the stored tile (min(j, L), max(j, L)) -- line L of the triangle (row L
+// and column L).  With that buffer
+//     A = D[I][L] = tile I as stored if I <= L, else tile I read transposed
+//     B = D[L][J] = tile J as stored if J >= L, else tile J read transposed
+// and an operand is staged from either layout into the same k-pair LDS image:
 //   row form  (element (x, k) at base + x*ld + k, 16 B along k)      = A plain / B transposed
 //   col form  (element (x, k) at base + k*ld + x, two k-rows paired)  = A transposed / B plain
-// Tile sets (SymSet): mode 0 = every kept tile I <= J with rows/cols x0, x1 excluded
-// (grid.x = nb(nb+1)/2), mode 1 = the tiles of line L, i.e. (min(L,x), max(L,x)) for x != x0, x1
-// (grid.x = nb).
-struct SymSet {
-    int mode, L, x0, x1, nb;
-};
-
-__device__ __forceinline__ bool sym_tile(const SymSet& s, int idx, int& I, int& J) {
-    if (s.mode == 1) {
-        if (idx == s.x0 || idx == s.x1) return false;
-        I = min(idx, s.L);
-        J = max(idx, s.L);
-        return true;
-    }
-    // idx -> (I, J), I <= J, row I holding nb - I tiles
-    const int m = s.nb;
-    const double b = 2.0 * m + 1.0;
+// The line buffer is the unit of exchange in the multi-rank schedule (one allgather per pivot,
+// routing.hip fw_line_sym), and its tiles are contiguous 64-KB blocks for the bulk's operand reads.
+__device__ __forceinline__ void tri_tile(int nb, int idx, int& I, int& J) {
+    // idx -> (I, J), I <= J, row-major over the upper triangle: row I holds nb - I tiles
+    const double b = 2.0 * nb + 1.0;
     int i = (int)((b - sqrt(b * b - 8.0 * (double)idx)) * 0.5);
-    auto off = [&](int r) { return r * m - r * (r - 1) / 2; };
+    auto off = [&](int r) { return r * nb - r * (r - 1) / 2; };
     while (i > 0 && off(i) > idx) --i;
-    while (i + 1 < m && off(i + 1) <= idx) ++i;
+    while (i + 1 < nb && off(i + 1) <= idx) ++i;
     I = i;
     J = i + (idx - off(i));
-    if (I == s.x0 || I == s.x1 || J == s.x0 || J == s.x1) return false;
-    return true;
 }
 
 template <int T, int KC>
@@ -632,56 +632,49 @@ __device__ __forceinline__ void sym_store(const SymOp<T, KC>& o, u64p* __restric
     }
 }
 
-// one stored tile C = (I, J), I <= J, relaxed through pivot block kb (k-pair LDS image as fw_tile_pk):
-// one v_lshl_add_u64 over the packed pairs + v_min3_u32 per two relaxations (two v_add_u32 +
-// v_min3_u32 measured slower in the tile: C3 bulk launch 0.304 vs 0.242 ms, profiles/r02c/fw_fold.txt)
-template <int T, int KC>
-__device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld, int kb, int I, int J) {
-    using S = SymOp<T, KC>;
-    constexpr int M = T / 16;
-    constexpr int LDA = T + 2;
+// C (TM x TM, row stride ldc) = min(C, A (x) B) with A = TM rows x TK (form acol), B = TK x TM
+// columns (form bcol), both with row stride ldab; C2 (optional) receives a copy of the result.
+// TM = 128: 256 threads x (8 x 8) micro-tiles (the bulk); TM = 64: (4 x 4) micro-tiles (the
+// quadrant launches on the FW critical chain).  One v_lshl_add_u64 over packed k-pairs +
+// v_min3_u32 per two relaxations (two v_add_u32 + v_min3_u32 measured slower in the tile: C3
+// bulk launch 0.304 vs 0.242 ms, profiles/r02c/fw_fold.txt).  Every product reads all of A and
+// B through LDS before C is stored; in-place line updates where A or B overlaps C across
+// workgroups read old or new values of C's row, and both give the same result once the pivot
+// is closed (min over k of C'[x][k] + P[k][y] = min over k of C[x][k] + P[k][y] for P closed).
+template <int TM, int TK, int KC>
+__device__ __forceinline__ void fw_core_lb(uint32_t* __restrict__ C, size_t ldc, const uint32_t* __restrict__ Ab,
+                                           bool acol, const uint32_t* __restrict__ Bb, bool bcol, size_t ldab,
+                                           uint32_t* __restrict__ C2, size_t ldc2) {
+    using S = SymOp<TM, KC>;
+    constexpr int M = TM / 16;
+    constexpr int LDA = TM + 2;
     constexpr int BUF = KC * LDA;
+    constexpr int NCH = TK / KC;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     u64p* lds = reinterpret_cast<u64p*>(smem_raw);
-    uint32_t* C = D + (size_t)I * T * ld + (size_t)J * T;
-    const bool acol = I > kb, bcol = !(J < kb);  // A transposed / B plain read column-form
-    const uint32_t* Ab = acol ? D + (size_t)kb * T * ld + (size_t)I * T : D + (size_t)I * T * ld + (size_t)kb * T;
-    const uint32_t* Bb = bcol ? D + (size_t)kb * T * ld + (size_t)J * T : D + (size_t)J * T * ld + (size_t)kb * T;
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-    // gridDim.z > 1: split-K over the pivot block's k chunks, merged with atomicMin (exact: min
-    // is associative and commutative) -- the short line launches on the FW critical chain
-    constexpr int NCH = T / KC;
-    const int nsplit = (int)gridDim.z;
-    const int ch0 = (int)blockIdx.z * NCH / nsplit, ch1 = ((int)blockIdx.z + 1) * NCH / nsplit;
     S sa, sb;
-    sym_load<T, KC>(sa, Ab, ld, acol, ch0 * KC);
-    sym_load<T, KC>(sb, Bb, ld, bcol, ch0 * KC);
+    sym_load<TM, KC>(sa, Ab, ldab, acol, 0);
+    sym_load<TM, KC>(sb, Bb, ldab, bcol, 0);
     uint32_t c[M][M];
-    if (nsplit == 1) {
 #pragma unroll
-        for (int a = 0; a < M; ++a)
+    for (int a = 0; a < M; ++a)
 #pragma unroll
-            for (int g = 0; g < M / 2; ++g) {
-                VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx);
-                c[a][2 * g] = v.v[0];
-                c[a][2 * g + 1] = v.v[1];
-            }
-    } else {
-#pragma unroll
-        for (int a = 0; a < M; ++a)
-#pragma unroll
-            for (int b = 0; b < M; ++b) c[a][b] = KeyOps<uint32_t>::INF;
-    }
-    sym_store<T, KC>(sa, lds, acol);
-    sym_store<T, KC>(sb, lds + (KC / 2) * LDA, bcol);
+        for (int g = 0; g < M / 2; ++g) {
+            VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ldc + 32 * g + 2 * tx);
+            c[a][2 * g] = v.v[0];
+            c[a][2 * g + 1] = v.v[1];
+        }
+    sym_store<TM, KC>(sa, lds, acol);
+    sym_store<TM, KC>(sb, lds + (KC / 2) * LDA, bcol);
     __syncthreads();
 #pragma unroll 1
-    for (int ch = ch0; ch < ch1; ++ch) {
-        const u64p* Ap = lds + ((ch - ch0) & 1) * BUF;
+    for (int ch = 0; ch < NCH; ++ch) {
+        const u64p* Ap = lds + (ch & 1) * BUF;
         const u64p* Bp = Ap + (KC / 2) * LDA;
-        if (ch + 1 < ch1) {  // issue early
-            sym_load<T, KC>(sa, Ab, ld, acol, (ch + 1) * KC);
-            sym_load<T, KC>(sb, Bb, ld, bcol, (ch + 1) * KC);
+        if (ch + 1 < NCH) {  // issue early
+            sym_load<TM, KC>(sa, Ab, ldab, acol, (ch + 1) * KC);
+            sym_load<TM, KC>(sb, Bb, ldab, bcol, (ch + 1) * KC);
         }
 #pragma unroll
         for (int kp = 0; kp < KC / 2; ++kp) {
@@ -703,37 +696,202 @@ __device__ __forceinline__ void fw_tile_sym(uint32_t* __restrict__ D, size_t ld,
                     c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         }
-        if (ch + 1 < ch1) {  // write late into the other buffer
-            u64p* An = lds + ((ch + 1 - ch0) & 1) * BUF;
-            sym_store<T, KC>(sa, An, acol);
-            sym_store<T, KC>(sb, An + (KC / 2) * LDA, bcol);
+        if (ch + 1 < NCH) {  // write late into the other buffer
+            u64p* An = lds + ((ch + 1) & 1) * BUF;
+            sym_store<TM, KC>(sa, An, acol);
+            sym_store<TM, KC>(sb, An + (KC / 2) * LDA, bcol);
         }
         __syncthreads();
     }
-    if (nsplit == 1) {
 #pragma unroll
-        for (int a = 0; a < M; ++a)
+    for (int a = 0; a < M; ++a)
 #pragma unroll
-            for (int g = 0; g < M / 2; ++g) {
-                VecN<uint32_t, 2> v;
-                v.v[0] = c[a][2 * g];
-                v.v[1] = c[a][2 * g + 1];
-                stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx, v);
-            }
-    } else {
-#pragma unroll
-        for (int a = 0; a < M; ++a)
-#pragma unroll
-            for (int b = 0; b < M; ++b) atomicMin(C + (size_t)pk_rc(ty, a) * ld + pk_rc(tx, b), c[a][b]);
-    }
+        for (int g = 0; g < M / 2; ++g) {
+            VecN<uint32_t, 2> v;
+            v.v[0] = c[a][2 * g];
+            v.v[1] = c[a][2 * g + 1];
+            stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ldc + 32 * g + 2 * tx, v);
+            if (C2) stv<uint32_t, 2>(C2 + (size_t)pk_rc(ty, a) * ldc2 + 32 * g + 2 * tx, v);
+        }
 }
 
 template <int T, int KC>
-__global__ void __launch_bounds__(256, 3) fw_product_sym(uint32_t* __restrict__ D, size_t ld, int kb, SymSet s, int prio) {
+constexpr size_t lb_lds_bytes() { return (size_t)2 * KC * (T + 2) * sizeof(u64p); }
+
+// ---- distribution of the stored tiles over G ranks (routing.hip fw_line_sym) ----------------
+// Tile (I, J), I <= J, belongs to rank (I + J) mod G: every rank holds ~1/G of every row and of
+// every LINE (line L's tile j is (min(j,L), max(j,L)), owner (j + L) mod G), so both the bulk of a
+// pivot and the per-pivot line exchange are balanced.  A line buffer is laid out owner-major so
+// that each rank's tiles of the line are one contiguous segment for the allgather:
+//   slot(j) = base(owner) + (j - j0(owner)) / G,  j0(r) = (r - L) mod G,
+//   count(r) = #{ j < nb : j = j0(r) mod G },  base(r) = sum_{r' < r} count(r')
+struct LineMap {
+    int nb, G;
+    __host__ __device__ int j0(int r, int L) const { return ((r - L) % G + G) % G; }
+    __host__ __device__ int count(int r, int L) const {
+        const int a = j0(r, L);
+        return a < nb ? (nb - 1 - a) / G + 1 : 0;
+    }
+    __host__ __device__ int base(int r, int L) const {
+        int s = 0;
+        for (int q = 0; q < r; ++q) s += count(q, L);
+        return s;
+    }
+    __host__ __device__ int owner(int j, int L) const { return (j + L) % G; }
+    __host__ __device__ int slot(int j, int L) const {
+        const int r = owner(j, L);
+        return base(r, L) + (j - j0(r, L)) / G;
+    }
+};
+
+// Bulk of pivot L: this rank's stored tiles (triangle indices tiles[0 .. gridDim.x)) except
+// those in lines x0, x1 (the pivot's own line, final, and the next pivot's line, updated by the
+// chain).  C in D (row stride ld), operands from line L's buffer.
+template <int T, int KC>
+__global__ void __launch_bounds__(256, 3) fw_bulk_lb(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lb,
+                                                     int L, int x0, int x1, LineMap lm, const int* __restrict__ tiles) {
     int I, J;
-    if (!sym_tile(s, (int)blockIdx.x, I, J)) return;  // whole workgroup
-    if (prio) __builtin_amdgcn_s_setprio(3);  // chain (line) launches: see fw_phase1
-    fw_tile_sym<T, KC>(D, ld, kb, I, J);
+    tri_tile(lm.nb, tiles[blockIdx.x], I, J);
+    if (I == x0 || I == x1 || J == x0 || J == x1) return;  // whole workgroup
+    constexpr size_t TT = (size_t)T * T;
+    fw_core_lb<T, T, KC>(D + (size_t)I * T * ld + (size_t)J * T, ld, lb + lm.slot(I, L) * TT, I > L,
+                         lb + lm.slot(J, L) * TT, J >= L, T, nullptr, 0);
+}
+
+// Line launches of the FW critical chain, one 64 x 64 quadrant of a line tile per workgroup
+// (grid = (tiles, 4)) so that a line takes one quadrant's latency instead of one tile's.
+//   mode 0 (line K1 w.r.t. pivot L, this rank's tiles of line K1: j = j0 + G * blockIdx.x):
+//          C = D tile (min(j,K1), max(j,K1)), operands from line L's buffer lbL; the result
+//          also goes to lbK.  j == L is not updated (that tile, (L, K1), is final in line L):
+//          it is copied from lbL, the same stored tile.
+//   mode 1 (line K1 w.r.t. its own closed pivot, every tile j = blockIdx.x): C = lbK's tile,
+//          operands from lbK; the result also goes to D when this rank owns the tile (rank g),
+//          and the closed pivot tile j == K1 is copied back to D by its owner.
+template <int T>
+__global__ void __launch_bounds__(256, 2) fw_line_lb(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lbL,
+                                                     int L, uint32_t* __restrict__ lbK, int K1, int mode, LineMap lm,
+                                                     int g, int prio) {
+    constexpr int TM = T / 2;
+    constexpr size_t TT = (size_t)T * T;
+    const int j = mode == 0 ? lm.j0(g, K1) + lm.G * (int)blockIdx.x : (int)blockIdx.x;
+    const int q = (int)blockIdx.y, qi = q >> 1, qj = q & 1;
+    const int I = min(j, K1), J = max(j, K1);
+    const bool own = lm.owner(j, K1) == g;
+    uint32_t* Dt = D + (size_t)I * T * ld + (size_t)J * T;
+    uint32_t* Lt = lbK + lm.slot(j, K1) * TT;
+    auto copy_quadrant = [&](const uint32_t* src, size_t lds_, uint32_t* dst, size_t ldd) {
+        src += (size_t)qi * TM * lds_ + qj * TM;
+        dst += (size_t)qi * TM * ldd + qj * TM;
+        for (int e = threadIdx.x; e < TM * TM / 4; e += 256) {
+            const int r = e / (TM / 4), c4 = e % (TM / 4);
+            st16(dst + (size_t)r * ldd + c4 * 4, ld16(src + (size_t)r * lds_ + c4 * 4));
+        }
+    };
+    if (mode == 1 && j == K1) {  // the closed pivot tile itself: back to D on its owner
+        if (own) copy_quadrant(Lt, T, Dt, ld);
+        return;
+    }
+    if (mode == 0 && j == L) {  // the final tile (L, K1) from line L's buffer
+        copy_quadrant(lbL + lm.slot(K1, L) * TT, T, Lt, T);
+        return;
+    }
+    if (prio) __builtin_amdgcn_s_setprio(3);  // the chain runs beside the bulk tiles (see fw_phase1)
+    const uint32_t* lb = mode == 0 ? lbL : lbK;
+    const int P = mode == 0 ? L : K1;
+    const bool acol = I > P, bcol = J >= P;
+    // A rows qi: row form advances rows, col form advances columns (and B likewise for columns qj)
+    const uint32_t* Ab = lb + lm.slot(I, P) * TT + (acol ? (size_t)qi * TM : (size_t)qi * TM * T);
+    const uint32_t* Bb = lb + lm.slot(J, P) * TT + (bcol ? (size_t)qj * TM : (size_t)qj * TM * T);
+    Dt += (size_t)qi * TM * ld + qj * TM;
+    Lt += (size_t)qi * TM * T + qj * TM;
+    if (mode == 0) fw_core_lb<TM, T, 32>(Dt, ld, Ab, acol, Bb, bcol, T, Lt, T);
+    else fw_core_lb<TM, T, 32>(Lt, T, Ab, acol, Bb, bcol, T, own ? Dt : nullptr, ld);
+}
+
+// One squaring step of the pivot-tile closure, Pout = min(Pin, Pin (x) Pin): 16 x 16 outputs per
+// workgroup, grid (T/16, T/16).  Eight steps (ping-pong, the last into the line buffer) close the
+// tile -- paths of up to 2^8 >= T hops inside the block; keys are integers, so any order of the
+// relaxations gives the same closure.  flags[s] records whether step s changed anything; a step
+// after an unchanged one only copies (the tile is closed).  Replaces the one-workgroup closure on
+// the multi-rank critical chain: 64 workgroups per step instead of one CU for 128^3 relaxations.
+template <int T>
+__global__ void __launch_bounds__(256) fw_square(const uint32_t* __restrict__ Pin, uint32_t* __restrict__ Pout,
+                                                 uint32_t* __restrict__ flags, int step, int prio) {
+    if (prio) __builtin_amdgcn_s_setprio(3);
+    __shared__ uint32_t A[16][T + 1];
+    __shared__ uint32_t B[T][17];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int r = blockIdx.y * 16 + ty, c = blockIdx.x * 16 + tx;
+    const uint32_t old = Pin[(size_t)r * T + c];
+    if (step > 0 && __hip_atomic_load(&flags[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        Pout[(size_t)r * T + c] = old;  // converged: keep the ping-pong consistent
+        return;
+    }
+    for (int e = threadIdx.x; e < 16 * T; e += 256) {
+        const int y = e / T, k = e % T;
+        A[y][k] = Pin[(size_t)(blockIdx.y * 16 + y) * T + k];
+        const int kk = e / 16, x = e % 16;
+        B[kk][x] = Pin[(size_t)kk * T + blockIdx.x * 16 + x];
+    }
+    __syncthreads();
+    uint32_t v = old;
+#pragma unroll 8
+    for (int k = 0; k < T; k += 2) v = KeyOps<uint32_t>::min3(v, A[ty][k] + B[k][tx], A[ty][k + 1] + B[k + 1][tx]);
+    Pout[(size_t)r * T + c] = v;
+    if (__ballot(v != old) && (threadIdx.x & 63) == 0) atomicOr(&flags[step], 1u);
+}
+
+// lb[slot(j)] <- stored tile (min(j, L), max(j, L)) of D, j = blockIdx.x
+template <int T>
+__global__ void __launch_bounds__(256) k_pack_line(const uint32_t* __restrict__ D, size_t ld, uint32_t* __restrict__ lb,
+                                                   int L, LineMap lm) {
+    const int j = (int)blockIdx.x, I = min(j, L), J = max(j, L);
+    const uint32_t* src = D + (size_t)I * T * ld + (size_t)J * T;
+    uint32_t* dst = lb + (size_t)lm.slot(j, L) * T * T;
+    for (int e = threadIdx.x; e < T * T / 4; e += 256) {
+        const int r = e / (T / 4), c4 = e % (T / 4);
+        st16(dst + (size_t)r * T + c4 * 4, ld16(src + (size_t)r * ld + c4 * 4));
+    }
+}
+
+// Multi-rank end of FW: every rank packs its own stored tiles (triangle indices tiles[i]) into
+// P[first + i] (T x T each; its segment of the allgather), and after the allgather every rank
+// unpacks every tile t from P[slot[t]] into its row-major D, with the mirror (J, I) = (I, J)^T
+// through 64 x 64 LDS transposes.
+template <int T>
+__global__ void __launch_bounds__(256) k_pack_tiles(const uint32_t* __restrict__ D, size_t ld, int nb,
+                                                    const int* __restrict__ tiles, size_t first, uint32_t* __restrict__ P) {
+    int I, J;
+    tri_tile(nb, tiles[blockIdx.x], I, J);
+    const uint32_t* src = D + (size_t)I * T * ld + (size_t)J * T;
+    uint32_t* dst = P + (first + blockIdx.x) * (size_t)T * T;
+    for (int e = threadIdx.x; e < T * T / 4; e += 256) {
+        const int r = e / (T / 4), c4 = e % (T / 4);
+        st16(dst + (size_t)r * T + c4 * 4, ld16(src + (size_t)r * ld + c4 * 4));
+    }
+}
+
+template <int T>
+__global__ void __launch_bounds__(256) k_unpack_tiles(const uint32_t* __restrict__ P, const int* __restrict__ slot, int nb,
+                                                      uint32_t* __restrict__ D, size_t ld) {
+    int I, J;
+    tri_tile(nb, (int)blockIdx.x, I, J);
+    const uint32_t* src = P + (size_t)slot[blockIdx.x] * T * T;
+    __shared__ uint32_t tile[64][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int sb = 0; sb < (T / 64) * (T / 64); ++sb) {
+        const int bi = sb / (T / 64), bj = sb % (T / 64);
+        for (int r = ty; r < 64; r += 4) {
+            const uint32_t v = src[(size_t)(bi * 64 + r) * T + bj * 64 + tx];
+            tile[r][tx] = v;
+            D[((size_t)I * T + bi * 64 + r) * ld + (size_t)J * T + bj * 64 + tx] = v;
+        }
+        __syncthreads();
+        if (I != J)
+            for (int r = ty; r < 64; r += 4)
+                D[((size_t)J * T + bj * 64 + r) * ld + (size_t)I * T + bi * 64 + tx] = tile[tx][r];
+        __syncthreads();
+    }
 }
 
 // lower triangle <- transpose of the upper one, 64 x 64 blocks (bi > bj) through LDS

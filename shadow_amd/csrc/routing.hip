@@ -364,19 +364,6 @@ __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, 
     if (unreach) atomicOr(&flags->unreachable_used_pair, 1u);
 }
 
-// Row packing for the output exchange when a rank's rows are not one contiguous range:
-// pack: stage[q] = out[pos[q]]  /  unpack: out[pos[q]] = stage[q]   (rows of `row_bytes`)
-__global__ void k_rows_copy(const unsigned char* __restrict__ src, unsigned char* __restrict__ dst,
-                            const uint32_t* __restrict__ pos, uint32_t nrows, size_t row_bytes, int unpack) {
-    const size_t words = row_bytes / 4;
-    for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
-        const size_t sr = unpack ? q : pos[q], dr = unpack ? pos[q] : q;
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(src + sr * row_bytes);
-        uint32_t* b = reinterpret_cast<uint32_t*>(dst + dr * row_bytes);
-        for (size_t w = threadIdx.x; w < words; w += blockDim.x) b[w] = a[w];
-    }
-}
-
 // min over a u64 array (RoutingInfo::get_smallest_latency_ns, mod.rs:474-476: all n^2 entries,
 // diagonal included)
 __global__ void k_min_u64(const uint64_t* __restrict__ a, size_t count, unsigned long long* out) {
@@ -556,7 +543,7 @@ struct srg_ctx {
     size_t h_ring_bytes = 0;
     hipEvent_t ev_ring[3] = {nullptr, nullptr, nullptr};
     DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
-    size_t own_row0 = 0, own_row1 = ~(size_t)0;  // multi-rank without output exchange: the output rows this rank filled
+    size_t own_row0 = 0, own_row1 = ~(size_t)0;  // the output rows this rank routed (multi-rank: [p0, p1))
     int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
     hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
     hipEvent_t ev_ledges = nullptr, ev_lin = nullptr, ev_ldone = nullptr, ev_wlate = nullptr;
@@ -568,6 +555,10 @@ struct srg_ctx {
     int scan_groups = 0;             // host entry: v5 scan launches interleaved with the loss rows (0 = auto: 3) (SRG_OPT_SCAN_GROUPS)
     int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
     srg::Comm* comm = nullptr;       // null = single GPU
+    // srg_multi: the caller's output arrays are page-locked once for every rank (portable); the
+    // host entry then waits for that registration (returns the arrays' device views, false if it
+    // failed) instead of registering them itself
+    std::function<bool(void** views, double* ms)> ext_reg;
     std::vector<hipEvent_t> prof_events;
     hipStream_t stream = nullptr;
     hipStream_t aux_stream = nullptr;   // FW lookahead: phase 1/2 of the next pivot block
@@ -582,7 +573,8 @@ struct srg_ctx {
     DevBuf b_ecnt, b_eoff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu, b_grpe, b_cscent,
         b_gblk, b_DST, b_scantmp, b_ess, b_rlen, b_roff;
     // multi-rank: local sources, their output rows, exchange staging
-    DevBuf b_lnodes, b_lpos, b_allpos, b_stage, b_red, b_outoff, b_outdst;
+    DevBuf b_lnodes, b_lpos, b_red, b_outoff, b_outdst;
+    DevBuf b_ptmp, b_cflags, b_tiles, b_tslot;  // symmetric FW: closure ping-pong + flags, own tiles, packed slots
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -590,7 +582,7 @@ struct srg_ctx {
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
-                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_allpos, &b_stage, &b_red, &b_outoff, &b_outdst,
+                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_ptmp, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst,
                           &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
@@ -891,21 +883,27 @@ struct HostSink {
     }
 };
 
-// ---- distribution plan (DESIGN.md §6) --------------------------------------------------
-// G ranks, 1-D row blocks: rank r owns FW row blocks [r*nb/G, (r+1)*nb/G) (rows of D, and so
-// the D rows of the used sources in them).  Each rank routes the used sources whose vertex it
-// owns; outputs are exchanged row-wise at the end.  G = 1 is the single-GPU case.
+// ---- distribution plan (DESIGN.md §7) --------------------------------------------------
+// G ranks.  FW ownership: the general FW gives rank r the whole rows of the row blocks
+// [blk_lo[r], blk_lo[r+1]); the symmetric FW gives it the stored tiles (I, J) with
+// (I + J) mod G == r (fw_line_sym).  After FW every rank holds the whole D.  Sources: rank r
+// routes the used nodes at positions [p0, p1) = [n r / G, n (r+1) / G) of `nodes`, so its output
+// rows are one contiguous range whatever the node order.
 struct Plan {
     int G = 1, g = 0, nb = 0, rb0 = 0, rb1 = 0;
-    uint32_t u0 = 0, u1 = 0;               // own vertex rows, clipped to [0, V)
-    std::vector<int> blk_lo;               // [G+1] first row block per rank
-    std::vector<uint32_t> lnodes, lpos;    // own used sources (vertex) and their positions in `nodes`
-    std::vector<uint32_t> cnt, first;      // per rank: source count and first row in rank order
-    std::vector<uint32_t> allpos;          // positions of every rank's sources, in rank order
-    bool contiguous = true;                // allpos == 0..n-1 (rows already in rank order)
+    std::vector<int> blk_lo;               // [G+1] first row block per rank (general FW)
+    uint32_t p0 = 0, p1 = 0;               // own sources = nodes[p0 .. p1)
+    std::vector<uint32_t> lnodes, lpos;    // own sources (vertex) and their output rows (p0 ..)
     int owner(int b) const { return (int)(std::upper_bound(blk_lo.begin(), blk_lo.end(), b) - blk_lo.begin()) - 1; }
     bool own(int b) const { return b >= rb0 && b < rb1; }
 };
+
+inline void tri_tile_h(int nb, int idx, int& I, int& J) {  // kernels.hip.h tri_tile, on the host
+    int i = 0;
+    while (i + 1 < nb && (i + 1) * nb - (i + 1) * i / 2 <= idx) ++i;
+    I = i;
+    J = i + (idx - (i * nb - i * (i - 1) / 2));
+}
 
 Plan make_plan(int G, int g, uint32_t V, int T, const std::vector<uint32_t>& nodes_h) {
     Plan p;
@@ -914,26 +912,16 @@ Plan make_plan(int G, int g, uint32_t V, int T, const std::vector<uint32_t>& nod
     p.nb = (int)(((size_t)V + T - 1) / T);
     p.blk_lo.resize(G + 1);
     for (int r = 0; r <= G; ++r) p.blk_lo[r] = (int)((int64_t)r * p.nb / G);
+    p.blk_lo[G] = p.nb;
     p.rb0 = p.blk_lo[g];
     p.rb1 = p.blk_lo[g + 1];
-    p.u0 = std::min<uint32_t>(V, (uint32_t)p.rb0 * T);
-    p.u1 = std::min<uint32_t>(V, (uint32_t)p.rb1 * T);
-    std::vector<std::vector<uint32_t>> per(G);
-    for (uint32_t r = 0; r < nodes_h.size(); ++r) per[p.owner((int)(nodes_h[r] / T))].push_back(r);
-    p.cnt.resize(G);
-    p.first.resize(G);
-    uint32_t acc = 0;
-    for (int r = 0; r < G; ++r) {
-        p.cnt[r] = (uint32_t)per[r].size();
-        p.first[r] = acc;
-        for (uint32_t q : per[r]) {
-            p.contiguous &= (q == acc);
-            p.allpos.push_back(q);
-            ++acc;
-        }
+    const uint64_t n = nodes_h.size();
+    p.p0 = (uint32_t)(n * g / G);
+    p.p1 = (uint32_t)(n * (g + 1) / G);
+    for (uint32_t q = p.p0; q < p.p1; ++q) {
+        p.lnodes.push_back(nodes_h[q]);
+        p.lpos.push_back(q);
     }
-    p.lpos = per[g];
-    for (uint32_t q : p.lpos) p.lnodes.push_back(nodes_h[q]);
     return p;
 }
 
@@ -1094,18 +1082,32 @@ __global__ void k_low_words(const uint64_t* __restrict__ x, size_t n, uint32_t* 
         lo[i] = (uint32_t)x[i];
 }
 
-// Symmetric blocked FW (undirected graph, one rank, u32 pair-packed tiles): the same
-// lookahead schedule as fw_blocked over the stored tiles I <= J only (kernels.hip.h
-// fw_tile_sym), then the lower triangle is mirrored.  The chain of pivot k1 updates line k1
-// (row k1 = column k1^T) w.r.t. kb, closes k1, and updates line k1 w.r.t. k1; the bulk of kb
-// is every stored tile off the lines kb and k1.
+// Symmetric blocked FW over line buffers (undirected graph, u32 pair-packed tiles, one or
+// several ranks; kernels.hip.h fw_core_lb / LineMap).  Tile (I, J) belongs to rank (I + J) mod G.
+// Per pivot kb, with k1 = kb + 1:
+//   chain (aux stream, raised priority), after this rank's bulk of kb - 1:
+//     1. line k1 w.r.t. kb over the rank's own tiles of line k1 -> D and the line buffer LB(k1)
+//     2. (ranks > 1) allgatherv of LB(k1): one contiguous segment per rank (owner-major slots)
+//     3. close the pivot tile (k1, k1) inside LB(k1): eight squaring launches of 64 workgroups
+//        (every rank, redundantly)
+//     4. line k1 w.r.t. k1 over all of LB(k1), own tiles written back to D (every rank)
+//   bulk (main stream): the rank's stored tiles off lines kb and k1 through LB(kb).
+// Line 0 needs no exchange (every rank starts from the same D).  The chain of k1 overlaps the
+// bulk of kb; LB(k1) is written only after the bulk of kb - 1, the last reader of its buffer.
+// At the end the lower triangle is mirrored (one rank) or the ranks' tiles are all-gathered and
+// unpacked with the mirror, so that every rank holds the whole D.  shadow_amd/dist.py line_fw
+// restates this schedule in numpy (tests/test_dist_cpu.py runs it on gloo ranks).
 template <int T>
-void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
-                    int& prof_n) {
+void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
+                 int& prof_n, double& ms_xchg) {
     constexpr int KCS = 16;
-    const int nb = pl.nb;
-    const size_t lds = pk_lds_bytes<T, KCS>();
-    set_lds(fw_product_sym<T, KCS>, lds);
+    const int nb = pl.nb, G = pl.G, g = pl.g;
+    constexpr size_t TT = (size_t)T * T;
+    const bool multi = c.comm && c.comm->nranks > 1;
+    const LineMap lm{nb, G};
+    const size_t lds_bulk = lb_lds_bytes<T, KCS>(), lds_line = lb_lds_bytes<T / 2, 32>();
+    set_lds(fw_bulk_lb<T, KCS>, lds_bulk);
+    set_lds(fw_line_lb<T>, lds_line);
     const bool prof = c.profiling && nb > 2;
     if (prof) {
         while (c.prof_events.size() < (size_t)2 * nb) {
@@ -1114,38 +1116,136 @@ void fw_blocked_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStrea
             c.prof_events.push_back(e);
         }
     }
-    hipStream_t aux = c.aux_stream, bulk = st;
-    auto line = [&](int L, int kb, int x0, int x1, hipStream_t s) {
-        fw_product_sym<T, KCS><<<nb, 256, lds, s>>>(D, Vp, kb, SymSet{1, L, x0, x1, nb}, c.chain_prio);
+    uint32_t* LB[2] = {(uint32_t*)c.b_L0.get(nb * TT * 4), (uint32_t*)c.b_L1.get(nb * TT * 4)};
+    uint32_t* ptmp = (uint32_t*)c.b_ptmp.get(TT * 4);            // closure ping-pong
+    uint32_t* cflags = (uint32_t*)c.b_cflags.get((size_t)nb * 8 * 4);
+    HIP_CHECK(hipMemsetAsync(cflags, 0, (size_t)nb * 8 * 4, st));
+    // this rank's tiles (triangle indices, row-major), and for the final exchange every tile's
+    // slot in the packed buffer (owner-major, each owner's tiles in triangle order)
+    const int ntri = nb * (nb + 1) / 2;
+    std::vector<int> own_h, slot_h(ntri), first(G + 1, 0);
+    for (int t = 0, I = 0; I < nb; ++I)
+        for (int J = I; J < nb; ++J, ++t) {
+            const int r = (I + J) % G;
+            if (r == g) own_h.push_back(t);
+            ++first[r + 1];
+        }
+    for (int r = 0; r < G; ++r) first[r + 1] += first[r];
+    {
+        std::vector<int> fill(first.begin(), first.end() - 1);
+        for (int t = 0, I = 0; I < nb; ++I)
+            for (int J = I; J < nb; ++J, ++t) slot_h[t] = fill[(I + J) % G]++;
+    }
+    const int ntile = (int)own_h.size();
+    int* tiles = (int*)c.b_tiles.get(std::max<size_t>(own_h.size(), 1) * 4);
+    if (ntile) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
+    hipStream_t aux = c.aux_stream, cs = c.comm_stream;
+    const int prio = c.chain_prio;
+    auto close_pivot = [&](uint32_t* lbk, int k, hipStream_t s) {  // eight squarings, ending in the buffer
+        uint32_t* P = lbk + (size_t)lm.slot(k, k) * TT;
+        for (int q = 0; q < 8; ++q)
+            fw_square<T><<<dim3(T / 16, T / 16), 256, 0, s>>>(q % 2 ? ptmp : P, q % 2 ? P : ptmp, cflags + 8 * k, q, prio);
     };
-    auto phase1 = [&](int k, hipStream_t s) { fw_phase1<uint32_t, T><<<1, 512, 0, s>>>(D, Vp, k, c.chain_prio); };
-    phase1(0, bulk);
-    if (nb > 1) line(0, 0, 0, -1, bulk);
+    // line 0: every rank holds the same initial D
+    k_pack_line<T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
+    close_pivot(LB[0], 0, st);
+    if (nb > 1) fw_line_lb<T><<<dim3(nb, 4), 256, lds_line, st>>>(D, Vp, LB[0], 0, LB[0], 0, 1, lm, g, prio);
+    HIP_CHECK(hipGetLastError());
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
-        if (k1 >= nb) {
-            if (nb > 1) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, -1, nb}, 0);
-            break;
+        uint32_t* lbk = LB[kb & 1];
+        if (k1 < nb) {
+            uint32_t* lbn = LB[k1 & 1];
+            HIP_CHECK(hipEventRecord(c.ev_a, st));  // st: bulk of kb - 1 done
+            HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
+            const int mine = lm.count(g, k1);
+            if (mine) fw_line_lb<T><<<dim3(mine, 4), 256, lds_line, aux>>>(D, Vp, lbk, kb, lbn, k1, 0, lm, g, prio);
+            if (multi) {
+                std::vector<size_t> offs(G), lens(G);
+                for (int r = 0; r < G; ++r) {
+                    offs[r] = (size_t)lm.base(r, k1) * TT * 4;
+                    lens[r] = (size_t)lm.count(r, k1) * TT * 4;
+                }
+                HIP_CHECK(hipEventRecord(c.ev_b, aux));
+                HIP_CHECK(hipStreamWaitEvent(cs, c.ev_b, 0));
+                c.comm->allgatherv(lbn, offs.data(), lens.data(), cs);
+                HIP_CHECK(hipEventRecord(c.ev_c, cs));
+                HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
+            }
+            close_pivot(lbn, k1, aux);
+            fw_line_lb<T><<<dim3(nb, 4), 256, lds_line, aux>>>(D, Vp, lbn, k1, lbn, k1, 1, lm, g, prio);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipEventRecord(c.ev_d, aux));
         }
-        HIP_CHECK(hipEventRecord(c.ev_a, bulk));
-        HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
-        line(k1, kb, kb, -1, aux);  // line k1 (incl. tile (k1, k1)) w.r.t. kb
-        phase1(k1, aux);
-        line(k1, k1, k1, -1, aux);  // line k1 w.r.t. its own closed pivot
-        HIP_CHECK(hipEventRecord(c.ev_d, aux));
-        const int m = nb - 2;  // lines kb and k1 excluded
-        const bool timed = prof && m > 0;
-        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], bulk));
-        if (m > 0) fw_product_sym<T, KCS><<<nb * (nb + 1) / 2, 256, lds, bulk>>>(D, Vp, kb, SymSet{0, 0, kb, k1, nb}, 0);
+        // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
+        const bool timed = prof && ntile > 0 && k1 < nb;
+        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
+        if (ntile > 0) fw_bulk_lb<T, KCS><<<ntile, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, tiles);
+        HIP_CHECK(hipGetLastError());
         if (timed) {
-            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], bulk));
-            prof_relax += (uint64_t)m * (m + 1) / 2 * T * T * T;
+            int64_t m = 0;  // relaxations of this launch: own tiles off lines kb and k1
+            for (int t : own_h) {
+                int I, J;
+                tri_tile_h(nb, t, I, J);
+                if (I != kb && I != k1 && J != kb && J != k1) ++m;
+            }
+            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
+            prof_relax += (uint64_t)m * T * T * T;
             ++prof_n;
         }
-        HIP_CHECK(hipStreamWaitEvent(bulk, c.ev_d, 0));
+        if (k1 < nb) HIP_CHECK(hipStreamWaitEvent(st, c.ev_d, 0));
     }
-    const unsigned nb64 = (unsigned)(Vp / 64);
-    k_sym_mirror<uint32_t><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
+    HIP_CHECK(hipGetLastError());
+    if (!multi) {
+        const unsigned nb64 = (unsigned)(Vp / 64);
+        k_sym_mirror<uint32_t><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
+        return;
+    }
+    // every rank ends with the whole D: pack the own tiles, all-gather, unpack with the mirror
+    auto t0x = std::chrono::steady_clock::now();
+    uint32_t* Pk = (uint32_t*)c.b_PRED.get((size_t)ntri * TT * 4);
+    int* slot = (int*)c.b_tslot.get((size_t)ntri * 4);
+    HIP_CHECK(hipMemcpyAsync(slot, slot_h.data(), (size_t)ntri * 4, hipMemcpyHostToDevice, st));
+    if (ntile) k_pack_tiles<T><<<ntile, 256, 0, st>>>(D, Vp, nb, tiles, (size_t)first[g], Pk);
+    std::vector<size_t> offs(G), lens(G);
+    for (int r = 0; r < G; ++r) {
+        offs[r] = (size_t)first[r] * TT * 4;
+        lens[r] = (size_t)(first[r + 1] - first[r]) * TT * 4;
+    }
+    HIP_CHECK(hipEventRecord(c.ev_b, st));
+    HIP_CHECK(hipStreamWaitEvent(cs, c.ev_b, 0));
+    c.comm->allgatherv(Pk, offs.data(), lens.data(), cs);
+    HIP_CHECK(hipEventRecord(c.ev_c, cs));
+    HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
+    k_unpack_tiles<T><<<ntri, 256, 0, st>>>(Pk, slot, nb, D, Vp);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(st));
+    ms_xchg += ms_since(t0x);
+}
+
+// General FW, several ranks: every rank ends with the whole D (row blocks all-gathered)
+template <class K>
+void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t st, double& ms_xchg) {
+    auto t0x = std::chrono::steady_clock::now();
+    std::vector<size_t> offs(pl.G), lens(pl.G);
+    for (int r = 0; r < pl.G; ++r) {
+        const size_t a = std::min<size_t>(Vp, (size_t)pl.blk_lo[r] * T), b = std::min<size_t>(Vp, (size_t)pl.blk_lo[r + 1] * T);
+        offs[r] = a * Vp * sizeof(K);
+        lens[r] = (b - a) * Vp * sizeof(K);
+    }
+    HIP_CHECK(hipEventRecord(c.ev_b, st));
+    HIP_CHECK(hipStreamWaitEvent(c.comm_stream, c.ev_b, 0));
+    c.comm->allgatherv(D, offs.data(), lens.data(), c.comm_stream);
+    HIP_CHECK(hipEventRecord(c.ev_c, c.comm_stream));
+    HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
+    HIP_CHECK(hipStreamSynchronize(st));
+    ms_xchg += ms_since(t0x);
+}
+
+// the symmetric FW over line buffers applies: undirected, u32 pair-packed 128-tiles
+template <class K, int T>
+bool sym_fw_for(const srg_ctx& c, const DevGraph& g) {
+    return sizeof(K) == 4 && T == 128 && c.fw_symmetric && !g.directed && c.fw_packed != 0;
 }
 
 // Dense path for key type K. Returns false (u32 only) when certification fails.
@@ -1157,10 +1257,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const size_t VV = Vp * Vp;
     const bool multi = c.comm && c.comm->nranks > 1;
     Timer tm(st);
-    if (multi && !c.gather_output && pl.contiguous) {  // this rank's rows: one block in `nodes` order
-        c.own_row0 = pl.first[pl.g];
-        c.own_row1 = (size_t)pl.first[pl.g] + pl.cnt[pl.g];
-    }
+    c.own_row0 = pl.p0;  // this rank's output rows (the host entry ships only these without the exchange)
+    c.own_row1 = pl.p1;
 
     K* W = (K*)c.b_W.get(VV * sizeof(K));
     uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
@@ -1197,19 +1295,20 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     HIP_CHECK(hipGetLastError());
     const double ms_build = tm.lap();
 
-    // ---- blocked Floyd-Warshall ----
+    // ---- blocked Floyd-Warshall; afterwards every rank holds the whole D ----
     uint64_t prof_relax = 0;
     int prof_n = 0;
-    const bool sym_fw = sizeof(K) == 4 && T == 128 && c.fw_symmetric && !g.directed && !multi && c.fw_packed != 0;
-    if (sym_fw) {
-        if constexpr (sizeof(K) == 4 && T == 128) {
-            fw_blocked_sym<T>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n);
-        }
-    } else if constexpr (sizeof(K) == 4) {
-        if (c.fw_packed) fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n);
-        else fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
+    double ms_dx = 0;  // multi-rank: D exchange at the end of FW (inside ms_fw, also in ms_exchange)
+    if (sym_fw_for<K, T>(c, g)) {
+        if constexpr (sizeof(K) == 4 && T == 128) fw_line_sym<T>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n, ms_dx);
     } else {
-        fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
+        if constexpr (sizeof(K) == 4) {
+            if (c.fw_packed) fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n);
+            else fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
+        } else {
+            fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
+        }
+        if (multi) gather_rows<K>(c, pl, D, Vp, T, st, ms_dx);
     }
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
@@ -1271,34 +1370,18 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         HIP_CHECK(hipStreamSynchronize(st));
         return v;
     };
-    // output rows of every rank: [first[r], first[r] + cnt[r]) in rank order (staged when the
-    // ranks' rows are not contiguous in `nodes` order)
+    // output rows of every rank: positions [n r / G, n (r+1) / G)
     const bool exchange = multi && c.gather_output;
-    if (exchange && !pl.contiguous) {
-        c.b_stage.get((size_t)n * n * 8);
-        uint32_t* allpos = (uint32_t*)c.b_allpos.get((size_t)n * 4);
-        HIP_CHECK(hipMemcpyAsync(allpos, pl.allpos.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    }
     auto exchange_rows = [&](void* out, size_t elem) {  // on cs, after st
         const size_t row = (size_t)n * elem;
         std::vector<size_t> offs(pl.G), lens(pl.G);
         for (int r = 0; r < pl.G; ++r) {
-            offs[r] = (size_t)pl.first[r] * row;
-            lens[r] = (size_t)pl.cnt[r] * row;
+            const size_t a = (uint64_t)n * r / pl.G, b = (uint64_t)n * (r + 1) / pl.G;
+            offs[r] = a * row;
+            lens[r] = (b - a) * row;
         }
         cs_after_st();
-        if (pl.contiguous) {
-            c.comm->allgatherv(out, offs.data(), lens.data(), cs);
-            return;
-        }
-        unsigned char* stage = (unsigned char*)c.b_stage.p;
-        const uint32_t* allpos = (const uint32_t*)c.b_allpos.p;
-        if (nloc)
-            k_rows_copy<<<std::min<uint32_t>(nloc, 4096), 256, 0, cs>>>((const unsigned char*)out, stage + offs[pl.g],
-                                                                      lpos, nloc, row, 0);
-        c.comm->allgatherv(stage, offs.data(), lens.data(), cs);
-        k_rows_copy<<<std::min<uint32_t>(n, 4096), 256, 0, cs>>>(stage, (unsigned char*)out, allpos, n, row, 1);
-        HIP_CHECK(hipGetLastError());
+        c.comm->allgatherv(out, offs.data(), lens.data(), cs);
     };
 
     // u32 certification: no saturated key in any used row (every rank must agree)
@@ -1335,10 +1418,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
              "from another used node)");
     }
     if (exchange) exchange_rows(out_lat, 8);  // overlaps the scan and the loss pass below
-    // host entry, one rank: the latency table is final -- it leaves during the scan / loss pass
-    const bool sink_rows = sink && !multi && pl.contiguous && nloc == n && sink->ok();
+    // host entry, own rows only (one rank, or several without the exchange): the latency rows are
+    // final -- they leave during the scan / loss pass
+    const bool sink_rows = sink && !exchange && nloc && sink->ok();
     if (sink_rows) {
-        sink->send_rows(st, out_lat, sink->lat, 0, n, 8);
+        sink->send_rows(st, out_lat, sink->lat, pl.p0, nloc, 8);
         sink->lat_sent = true;
     }
 
@@ -1356,23 +1440,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     float* Lfin = nullptr;
     double ms_scan = 0;
     HIP_CHECK(hipMemsetAsync(multi_cnt, 0, 8, st));
-    // essential bitmask of the own rows, then all-gathered (V^2/8 bytes)
+    // essential bitmask (V^2/8 bytes): every rank holds the whole D and W, so each builds all of it
     const uint32_t nw64 = (V + 63) / 64;
     unsigned long long* ess = (unsigned long long*)c.b_ess.get((size_t)V * nw64 * 8);
-    if (pl.u1 > pl.u0)
-        k_ess_mask<K><<<grid_for((size_t)(pl.u1 - pl.u0) * nw64 * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, pl.u0,
-                                                                                               pl.u1, nw64, ess);
-    if (multi) {
-        std::vector<size_t> offs(pl.G), lens(pl.G);
-        for (int r = 0; r < pl.G; ++r) {
-            const size_t a = std::min<size_t>(V, (size_t)pl.blk_lo[r] * T), b = std::min<size_t>(V, (size_t)pl.blk_lo[r + 1] * T);
-            offs[r] = a * nw64 * 8;
-            lens[r] = (b - a) * nw64 * 8;
-        }
-        cs_after_st();
-        c.comm->allgatherv(ess, offs.data(), lens.data(), cs);
-        st_after_cs();
-    }
+    k_ess_mask<K><<<grid_for((size_t)V * nw64 * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, 0u, V, nw64, ess);
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
@@ -1484,7 +1555,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                                                                    DST, npad, cscoff, cscent, P.selfloss, nodes, n,
                                                                    lpos, out_loss, &P.flags->changed, r0);
                     HIP_CHECK(hipGetLastError());
-                    sink->send_rows(st, out_loss, sink->loss, r0, r1 - r0, 4);
+                    sink->send_rows(st, out_loss, sink->loss, pl.p0 + r0, r1 - r0, 4);
                 }
             }
             k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
@@ -1511,7 +1582,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                                                                    DST, npad, cscoff, cscent, P.selfloss, nodes, n,
                                                                    lpos, out_loss, &P.flags->changed, r0);
                     HIP_CHECK(hipGetLastError());
-                    if (sink_rows) sink->send_rows(st, out_loss, sink->loss, r0, r1 - r0, 4);
+                    if (sink_rows) sink->send_rows(st, out_loss, sink->loss, pl.p0 + r0, r1 - r0, 4);
                 }
                 if (sink_rows) sink->loss_sent = true;
                 uint32_t sw = 0;
@@ -1596,11 +1667,15 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         stats->ms_scan += ms_scan;
         stats->ms_loss += ms_loss;
         stats->ms_extract += ms_extract;
-        stats->ms_exchange += ms_exchange;
+        stats->ms_exchange += ms_exchange + ms_dx;
         stats->path_kind = sizeof(K) == 4 ? SRG_PATH_DENSE_U32 : SRG_PATH_DENSE_U64;
         stats->loss_rounds = rounds;
         stats->multi_pred_pairs = nmulti;
-        stats->relaxations = (uint64_t)(pl.rb1 - pl.rb0) * T * Vp * Vp;
+        uint64_t own_tiles = 0;  // symmetric FW: this rank's stored tiles ((I + J) mod G == g)
+        for (int I = 0; I < pl.nb; ++I)
+            for (int J = I; J < pl.nb; ++J) own_tiles += (I + J) % pl.G == pl.g;
+        stats->relaxations = sym_fw_for<K, T>(c, g) ? own_tiles * (uint64_t)pl.nb * T * T * T
+                                                    : (uint64_t)(pl.rb1 - pl.rb0) * T * Vp * Vp;
         stats->essential_edges = n_ess;
         stats->scan_kind = scan_kind;
         stats->nranks = pl.G;
@@ -1661,10 +1736,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     // this rank's sources, in graph-locality (BFS) order, in batches of 64 lanes: sources of
     // one batch are close to each other, so their Bellman-Ford frontiers move together
     const uint32_t p0 = (uint32_t)((uint64_t)rk * n / G), p1 = (uint32_t)((uint64_t)(rk + 1) * n / G);
-    if (multi && !c.gather_output) {  // this rank's rows: positions [p0, p1) of `nodes`
-        c.own_row0 = p0;
-        c.own_row1 = p1;
-    }
+    c.own_row0 = p0;  // this rank's rows: positions [p0, p1) of `nodes`
+    c.own_row1 = p1;
     const uint32_t nloc = p1 - p0;
     const uint32_t nbatch = (nloc + 63) / 64;
     std::vector<uint32_t> h_off(V + 1), h_src(arcs);
@@ -2170,6 +2243,9 @@ int guard(char* errbuf, size_t errlen, const std::function<void()>& body) {
     } catch (const Failure& f) {
         set_err(errbuf, errlen, f.msg);
         return f.code;
+    } catch (const srg::CommError& e) {
+        set_err(errbuf, errlen, std::string("collective: ") + e.what());
+        return SRG_ERR_RCCL;
     } catch (const std::bad_alloc&) {
         set_err(errbuf, errlen, "out of host memory");
         return SRG_ERR_OOM;
@@ -2218,7 +2294,8 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
     reg.device = c->device;
     reg.wait = c->d2h_stream;
     const bool early = !direct && nn * 12 >= ((size_t)64 << 20);
-    if (early) {
+    const bool ext = (bool)c->ext_reg;
+    if (early && !ext) {
         reg.p[0] = out_lat;
         reg.b[0] = nn * 8;
         reg.p[1] = out_loss;
@@ -2310,8 +2387,18 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             gather(dg.loss, 4);
         }
         const uint32_t* dn = stage_in(c->b_nodes, nodes, n, st);
-        uint64_t* dol = (uint64_t*)c->b_olat.get(std::max<size_t>(nn, 1) * 8);
-        float* dos = (float*)c->b_oloss.get(std::max<size_t>(nn, 1) * 4);
+        // multi-rank without the output exchange: the device holds only this rank's rows [p0, p1)
+        // (the plan's split, make_plan / run_sparse); dol / dos then point p0 rows before that
+        // allocation, so the kernels' absolute row indices land in it (C4 at 8 ranks: 3.75 GB per
+        // GPU instead of 30 GB)
+        const bool own_rows_only = !direct && c->comm && c->comm->nranks > 1 && !c->gather_output;
+        const size_t q0 = own_rows_only ? (uint64_t)n * c->comm->rank / c->comm->nranks : 0;
+        const size_t q1 = own_rows_only ? (uint64_t)n * (c->comm->rank + 1) / c->comm->nranks : n;
+        const size_t dev_nn = (q1 - q0) * n;
+        uint64_t* dol = reinterpret_cast<uint64_t*>(reinterpret_cast<uintptr_t>(c->b_olat.get(std::max<size_t>(dev_nn, 1) * 8)) -
+                                                    q0 * n * 8);
+        float* dos = reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(c->b_oloss.get(std::max<size_t>(dev_nn, 1) * 4)) -
+                                              q0 * n * 4);
         HIP_CHECK(hipStreamSynchronize(st));
         const double ms_h2d = ms_since(t0);
         HostSink sink;
@@ -2324,12 +2411,22 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             sink.mode = c->d2h_mode;
             sink.sdma = &c->sdma;
             sink.device = c->device;
-            sink.ready = [&reg, &sink]() {
-                if (!reg.join()) return false;
-                sink.lat_view = reg.view[0];
-                sink.loss_view = reg.view[1];
-                return true;
-            };
+            if (ext) {
+                sink.ready = [c, &reg, &sink]() {
+                    void* v[2] = {nullptr, nullptr};
+                    if (!c->ext_reg(v, &reg.ms)) return false;
+                    sink.lat_view = v[0];
+                    sink.loss_view = v[1];
+                    return true;
+                };
+            } else {
+                sink.ready = [&reg, &sink]() {
+                    if (!reg.join()) return false;
+                    sink.lat_view = reg.view[0];
+                    sink.loss_view = reg.view[1];
+                    return true;
+                };
+            }
         }
         c->own_row0 = 0;
         c->own_row1 = ~(size_t)0;
@@ -2339,20 +2436,23 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             dg.late->join();
             HIP_CHECK(hipStreamSynchronize(c->loss_stream));
         }
-        // multi-rank without the output exchange: only this rank's rows leave the device
-        const size_t r0 = std::min<size_t>(c->own_row0, n), r1 = std::min<size_t>(c->own_row1, n);
-        const size_t rows_off = r1 > r0 ? r0 * n : 0, rows_nn = r1 > r0 ? (r1 - r0) * n : nn;
+        // multi-rank without the output exchange: only this rank's rows [own_row0, own_row1) leave
+        // the device (possibly none), and min_latency_ns is over those rows only
+        const bool rows_only = c->comm && c->comm->nranks > 1 && !c->gather_output && !direct;
+        const size_t r0 = rows_only ? std::min<size_t>(c->own_row0, n) : 0;
+        const size_t r1 = rows_only ? std::min<size_t>(c->own_row1, n) : n;
+        const size_t rows_off = r0 * n, rows_nn = r1 > r0 ? (r1 - r0) * n : 0;
         auto t1 = std::chrono::steady_clock::now();
         unsigned long long hmin = ~0ull;
-        if (nn && stats) {  // smallest latency over the table (feeds the runahead, manager.rs:238-243)
+        if (rows_nn && stats) {  // smallest latency over the table (feeds the runahead, manager.rs:238-243)
             unsigned long long* dmin = (unsigned long long*)c->b_multi.get(8);
             HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 8, st));
-            k_min_u64<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dol + rows_off, rows_nn, dmin);  // own rows
+            k_min_u64<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dol + rows_off, rows_nn, dmin);
             HIP_CHECK(hipMemcpyAsync(&hmin, dmin, 8, hipMemcpyDeviceToHost, st));
         }
-        if (nn && !sink.lat_sent)
+        if (rows_nn && !sink.lat_sent)
             HIP_CHECK(hipMemcpyAsync(out_lat + rows_off, dol + rows_off, rows_nn * 8, hipMemcpyDeviceToHost, st));
-        if (nn && !sink.loss_sent)
+        if (rows_nn && !sink.loss_sent)
             HIP_CHECK(hipMemcpyAsync(out_loss + rows_off, dos + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         sink.finish();
@@ -2360,7 +2460,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             stats->ms_h2d = ms_h2d;
             stats->ms_d2h = ms_since(t1);  // the D2H not hidden behind kernels
             stats->ms_total = ms_since(t0);
-            stats->ms_host_register = reg.join() ? reg.ms : -1.0;
+            stats->ms_host_register = ext ? (sink.registered ? reg.ms : -1.0) : reg.join() ? reg.ms : -1.0;
             stats->d2h_overlapped_bytes = sink.early_bytes;
             stats->min_latency_ns = hmin;
             if (direct) stats->path_kind = SRG_PATH_DIRECT;
@@ -2507,6 +2607,35 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
     }
 }
 
+int srg_get_option(srg_ctx* ctx, int option, double* value) {
+    if (!ctx || !value) return SRG_ERR_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    switch (option) {
+        case SRG_OPT_PROFILING: *value = ctx->profiling; break;
+        case SRG_OPT_SPARSE_THRESHOLD: *value = ctx->sparse_threshold; break;
+        case SRG_OPT_GATHER_OUTPUT: *value = ctx->gather_output; break;
+        case SRG_OPT_ALGORITHM: *value = ctx->algorithm; break;
+        case SRG_OPT_SPARSE_LOCALITY: *value = ctx->sparse_locality; break;
+        case SRG_OPT_FW_TILE: *value = ctx->fw_tile; break;
+        case SRG_OPT_FW_PACKED: *value = ctx->fw_packed; break;
+        case SRG_OPT_SPARSE_GROUP: *value = ctx->sparse_group; break;
+        case SRG_OPT_SPARSE_WGS_PER_CU: *value = ctx->sparse_wgs_per_cu; break;
+        case SRG_OPT_SPARSE_DELTA_DIV: *value = ctx->sparse_delta_div; break;
+        case SRG_OPT_SPARSE_DELTA_ALL: *value = ctx->sparse_delta_all; break;
+        case SRG_OPT_SPARSE_GLOBAL_BITMAPS: *value = ctx->sparse_global_bitmaps; break;
+        case SRG_OPT_FW_SYMMETRIC: *value = ctx->fw_symmetric; break;
+        case SRG_OPT_CHAIN_PRIO: *value = ctx->chain_prio; break;
+        case SRG_OPT_D2H_MODE: *value = ctx->d2h_mode; break;
+        case SRG_OPT_LOSS_CHUNKS: *value = ctx->loss_chunks; break;
+        case SRG_OPT_SCAN_GROUPS: *value = ctx->scan_groups; break;
+        case SRG_OPT_H2D_CODEC: *value = ctx->h2d_codec; break;
+        case SRG_OPT_EDGE_SHARD: *value = ctx->edge_shard; break;
+        case SRG_OPT_LATE_LOSS: *value = ctx->late_loss; break;
+        default: return SRG_ERR_ARG;
+    }
+    return SRG_OK;
+}
+
 void srg_destroy(srg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
@@ -2601,6 +2730,209 @@ int srg_comm_size(srg_ctx* ctx, int* nranks, int* rank) {
     *nranks = ctx->comm ? ctx->comm->nranks : 1;
     *rank = ctx->comm ? ctx->comm->rank : 0;
     return SRG_OK;
+}
+
+// ---- one call site, several GPUs of this process (srg_multi) ----------------------------------
+// Shadow builds its RoutingInfo once, in one process (sim_config.rs:137-141 -> manager.rs:301-324).
+// srg_multi drives N GPUs from that one call: one context per device attached to an in-process
+// group (collectives = pull kernels over xGMI), one worker thread per rank, and the caller's two
+// host arrays page-locked once (portable) while the ranks ship their edges and run FW.  Every rank
+// runs the SPMD build with the output exchange off and ships its own sources' rows over its own
+// PCIe link straight into the caller's arrays, so the call returns with the whole table there.
+struct srg_multi {
+    std::vector<srg_ctx*> ranks;
+    std::vector<int> devices;
+    srg::LocalGroup* group = nullptr;
+    std::mutex mu;
+    ~srg_multi() {
+        for (srg_ctx* c : ranks) srg_destroy(c);
+        if (group) srg::local_group_release(group);
+    }
+};
+
+int srg_multi_create(srg_multi** out, const int* devices, int num_devices, char* errbuf, size_t errlen) {
+    if (!out || !devices || num_devices < 1) {
+        set_err(errbuf, errlen, "bad argument");
+        return SRG_ERR_ARG;
+    }
+    *out = nullptr;
+    auto* m = new srg_multi();
+    m->devices.assign(devices, devices + num_devices);
+    m->group = srg::local_group_create(num_devices);
+    for (int r = 0; r < num_devices; ++r) {
+        srg_ctx* c = nullptr;
+        int rc = srg_create(&c, devices[r], errbuf, errlen);
+        if (rc == SRG_OK) {
+            m->ranks.push_back(c);
+            if (num_devices > 1) rc = srg_comm_init_local(c, reinterpret_cast<srg_local_group*>(m->group), r, errbuf, errlen);
+        }
+        if (rc != SRG_OK) {
+            delete m;
+            return rc;
+        }
+    }
+    *out = m;
+    return SRG_OK;
+}
+
+void srg_multi_destroy(srg_multi* m) { delete m; }
+
+int srg_multi_size(const srg_multi* m) { return m ? (int)m->ranks.size() : 0; }
+
+int srg_multi_set_option(srg_multi* m, int option, double value) {
+    if (!m) return SRG_ERR_ARG;
+    if (option == SRG_OPT_GATHER_OUTPUT || option == SRG_OPT_SIMULATE_RANK) return SRG_ERR_ARG;  // fixed by srg_multi
+    for (srg_ctx* c : m->ranks) {
+        const int rc = srg_set_option(c, option, value);
+        if (rc != SRG_OK) return rc;
+    }
+    return SRG_OK;
+}
+
+int srg_multi_compute_shortest_paths(srg_multi* m, const srg_edge_list* graph, const uint32_t* nodes,
+                                     uint32_t num_nodes, uint64_t* out_latency_ns, float* out_packet_loss,
+                                     srg_stats* stats, char* errbuf, size_t errlen) {
+    if (!m || !graph || (num_nodes && (!nodes || !out_latency_ns || !out_packet_loss))) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    const int G = (int)m->ranks.size();
+    if (G == 1) return srg_compute_shortest_paths(m->ranks[0], graph, nodes, num_nodes, out_latency_ns, out_packet_loss,
+                                                  stats, errbuf, errlen);
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t nn = (size_t)num_nodes * num_nodes;
+    // one registration of the caller's arrays for every rank, beside the ranks' H2D and FW
+    struct Reg {
+        std::mutex mu;
+        std::thread th;
+        bool done = false, ok = false;
+        double ms = 0;
+        void* p[2] = {nullptr, nullptr};
+        size_t b[2] = {0, 0};
+        bool wait() {
+            std::lock_guard<std::mutex> l(mu);
+            if (!done) {
+                if (th.joinable()) th.join();
+                done = true;
+            }
+            return ok;
+        }
+    } reg;
+    reg.p[0] = out_latency_ns;
+    reg.b[0] = nn * 8;
+    reg.p[1] = out_packet_loss;
+    reg.b[1] = nn * 4;
+    const bool big = nn * 12 >= ((size_t)64 << 20);
+    if (big) {
+        const int dev0 = m->devices[0];
+        reg.th = std::thread([&reg, dev0]() {
+            const auto ts = std::chrono::steady_clock::now();
+            if (hipSetDevice(dev0) != hipSuccess) return;
+            const unsigned fl = hipHostRegisterPortable | hipHostRegisterMapped;
+            if (hipHostRegister(reg.p[0], reg.b[0], fl) != hipSuccess) return;
+            if (hipHostRegister(reg.p[1], reg.b[1], fl) != hipSuccess) {
+                (void)hipHostUnregister(reg.p[0]);
+                return;
+            }
+            reg.ms = ms_since(ts);
+            reg.ok = true;
+        });
+    }
+    std::vector<int> rc(G, SRG_OK);
+    std::vector<std::string> msg(G);
+    std::vector<srg_stats> st(G);
+    std::vector<std::thread> th;
+    for (int r = 0; r < G; ++r) {
+        srg_ctx* c = m->ranks[r];
+        c->gather_output = false;
+        if (big)
+            c->ext_reg = [&reg, c](void** views, double* ms) {
+                if (!reg.wait()) return false;
+                for (int i = 0; i < 2; ++i)
+                    if (hipHostGetDevicePointer(&views[i], reg.p[i], 0) != hipSuccess) views[i] = nullptr;
+                *ms = reg.ms;
+                return true;
+            };
+        th.emplace_back([&, r, c]() {
+            char eb[1024];
+            rc[r] = srg_compute_shortest_paths(c, graph, nodes, num_nodes, out_latency_ns, out_packet_loss, &st[r], eb,
+                                               sizeof(eb));
+            msg[r] = eb;
+            if (rc[r] != SRG_OK) srg::local_group_abort(m->group);  // release peers waiting in a collective
+        });
+    }
+    for (auto& t : th) t.join();
+    for (srg_ctx* c : m->ranks) c->ext_reg = nullptr;
+    srg::local_group_reset(m->group);
+    if (big && reg.wait()) {  // every rank's copies into the arrays are complete (their sinks finished)
+        (void)hipHostUnregister(reg.p[0]);
+        (void)hipHostUnregister(reg.p[1]);
+    }
+    // the first rank that failed for its own reason (the others report the abort)
+    int first = -1;
+    for (int r = 0; r < G && first < 0; ++r)
+        if (rc[r] != SRG_OK && rc[r] != SRG_ERR_RCCL) first = r;
+    for (int r = 0; r < G && first < 0; ++r)
+        if (rc[r] != SRG_OK) first = r;
+    if (first >= 0) {
+        set_err(errbuf, errlen, msg[first]);
+        return rc[first];
+    }
+    if (stats) {
+        // wall times: the slowest rank; counts: summed; minimum latency: over every rank's rows
+        *stats = st[0];
+        stats->local_sources = 0;
+        stats->d2h_overlapped_bytes = 0;
+        stats->prof_launches = 0;
+        stats->prof_kernel_ms = 0;
+        stats->prof_relaxations = 0;
+        stats->relaxations = 0;
+        stats->multi_pred_pairs = 0;
+        for (const srg_stats& x : st) {
+            for (double srg_stats::*f : {&srg_stats::ms_h2d, &srg_stats::ms_build, &srg_stats::ms_fw, &srg_stats::ms_scan,
+                                          &srg_stats::ms_loss, &srg_stats::ms_extract, &srg_stats::ms_d2h,
+                                          &srg_stats::ms_exchange, &srg_stats::ms_host_register})
+                stats->*f = std::max(stats->*f, x.*f);
+            stats->loss_rounds = std::max(stats->loss_rounds, x.loss_rounds);
+            stats->local_sources += x.local_sources;
+            stats->d2h_overlapped_bytes += x.d2h_overlapped_bytes;
+            stats->prof_launches += x.prof_launches;
+            stats->prof_kernel_ms += x.prof_kernel_ms;
+            stats->prof_relaxations += x.prof_relaxations;
+            stats->relaxations += x.relaxations;
+            stats->multi_pred_pairs += x.multi_pred_pairs;
+            stats->min_latency_ns = std::min(stats->min_latency_ns, x.min_latency_ns);
+        }
+        stats->rank = 0;
+        stats->nranks = G;
+        stats->ms_total = ms_since(t0);
+    }
+    if (errbuf && errlen) errbuf[0] = 0;
+    return SRG_OK;
+}
+
+int srg_multi_get_direct_paths(srg_multi* m, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
+                               uint64_t* out_latency_ns, float* out_packet_loss, srg_stats* stats, char* errbuf,
+                               size_t errlen) {
+    if (!m) {
+        set_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    // rank 0 alone: its context must not wait for peers in a collective
+    srg_ctx* c = m->ranks[0];
+    srg::Comm* cm = nullptr;
+    {
+        std::lock_guard<std::mutex> l2(c->mu);
+        std::swap(cm, c->comm);
+    }
+    const int rc = srg_get_direct_paths(c, graph, nodes, num_nodes, out_latency_ns, out_packet_loss, stats, errbuf, errlen);
+    {
+        std::lock_guard<std::mutex> l2(c->mu);
+        std::swap(cm, c->comm);
+    }
+    return rc;
 }
 
 int srg_order_packet_events_device(srg_ctx* ctx, const srg_event_batch* b, const uint64_t* table, uint32_t table_n,

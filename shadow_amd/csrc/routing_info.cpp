@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -64,15 +65,13 @@ struct srg_routing_info {
     }
 };
 
-extern "C" {
+namespace {
 
-int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
-                           int use_shortest_paths, srg_routing_info** out, srg_stats* stats, char* errbuf,
-                           size_t errlen) {
-    if (!ctx || !graph || !out || (num_ids && !gml_ids)) {
-        put_err(errbuf, errlen, "null argument");
-        return SRG_ERR_ARG;
-    }
+// compute(nodes, n, out_lat, out_loss, stats, errbuf, errlen): one of the host entry points
+using Compute = std::function<int(const uint32_t*, uint32_t, uint64_t*, float*, srg_stats*, char*, size_t)>;
+
+int build_routing_info(const Compute& compute, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
+                       int use_shortest_paths, srg_routing_info** out, srg_stats* stats, char* errbuf, size_t errlen) {
     *out = nullptr;
     try {
         // node_id_to_index (mod.rs:126-128): GML id -> NodeIndex, later duplicate ids win (:161)
@@ -99,11 +98,7 @@ int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint3
         ri->loss.reset(new float[std::max<size_t>(nn, 1)]);
         srg_stats local{};
         srg_stats* st = stats ? stats : &local;
-        const int rc = use_shortest_paths
-                           ? srg_compute_shortest_paths(ctx, graph, nodes.data(), num_ids, ri->lat.get(),
-                                                        ri->loss.get(), st, errbuf, errlen)
-                           : srg_get_direct_paths(ctx, graph, nodes.data(), num_ids, ri->lat.get(),
-                                                  ri->loss.get(), st, errbuf, errlen);
+        const int rc = compute(nodes.data(), num_ids, ri->lat.get(), ri->loss.get(), st, errbuf, errlen);
         if (rc != SRG_OK) {
             delete ri;
             // .context("Failed to compute shortest paths between graph nodes") (sim_config.rs:446-447)
@@ -147,6 +142,50 @@ int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint3
         put_err(errbuf, errlen, "internal error");
         return SRG_ERR_INTERNAL;
     }
+}
+
+}  // namespace
+
+extern "C" {
+
+int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
+                           int use_shortest_paths, srg_routing_info** out, srg_stats* stats, char* errbuf,
+                           size_t errlen) {
+    if (!ctx || !graph || !out || (num_ids && !gml_ids)) {
+        put_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    *out = nullptr;
+    // RoutingInfo::path is total over the node set (mod.rs:444-446): a rank of a multi-rank
+    // context that fills only its own rows cannot build one
+    int nr = 1, rk = 0;
+    double gather = 1.0;
+    if (srg_comm_size(ctx, &nr, &rk) == SRG_OK && nr > 1 && srg_get_option(ctx, SRG_OPT_GATHER_OUTPUT, &gather) == SRG_OK &&
+        gather == 0.0) {
+        put_err(errbuf, errlen,
+                "srg_routing_info_build needs the whole table: this rank fills only its own rows "
+                "(SRG_OPT_GATHER_OUTPUT 0); use srg_routing_info_build_multi or SRG_OPT_GATHER_OUTPUT 1");
+        return SRG_ERR_ARG;
+    }
+    Compute f = [&](const uint32_t* nodes, uint32_t n, uint64_t* lat, float* loss, srg_stats* st, char* eb, size_t el) {
+        return use_shortest_paths ? srg_compute_shortest_paths(ctx, graph, nodes, n, lat, loss, st, eb, el)
+                                  : srg_get_direct_paths(ctx, graph, nodes, n, lat, loss, st, eb, el);
+    };
+    return build_routing_info(f, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
+}
+
+int srg_routing_info_build_multi(srg_multi* m, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
+                                 int use_shortest_paths, srg_routing_info** out, srg_stats* stats, char* errbuf,
+                                 size_t errlen) {
+    if (!m || !graph || !out || (num_ids && !gml_ids)) {
+        put_err(errbuf, errlen, "null argument");
+        return SRG_ERR_ARG;
+    }
+    Compute f = [&](const uint32_t* nodes, uint32_t n, uint64_t* lat, float* loss, srg_stats* st, char* eb, size_t el) {
+        return use_shortest_paths ? srg_multi_compute_shortest_paths(m, graph, nodes, n, lat, loss, st, eb, el)
+                                  : srg_multi_get_direct_paths(m, graph, nodes, n, lat, loss, st, eb, el);
+    };
+    return build_routing_info(f, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
 }
 
 void srg_routing_info_free(srg_routing_info* ri) { delete ri; }

@@ -227,6 +227,46 @@ class Router:
         return self._run(N.lib().srg_get_direct_paths, edges, nodes)
 
 
+class MultiRouter:
+    """srg_multi: ONE call site driving several GPUs of this process (Shadow's one-process model).
+
+    compute_shortest_paths has Router.compute_shortest_paths' arguments and result: the whole
+    n x n table lands in the caller's arrays, each GPU writing its own sources' rows."""
+
+    def __init__(self, devices):
+        devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        rc = N.lib().srg_multi_create(ctypes.byref(h), arr, len(devices), err, len(err))
+        if rc != N.SRG_OK:
+            _raise(rc, err.value.decode(errors="replace"))
+        self._h = h
+        self.devices = devices
+
+    def __len__(self):
+        return int(N.lib().srg_multi_size(self._h))
+
+    def set_option(self, option, value):
+        rc = N.lib().srg_multi_set_option(self._h, int(option), float(value))
+        if rc != N.SRG_OK:
+            _raise(rc, f"srg_multi_set_option({option}, {value}) failed")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().srg_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compute_shortest_paths(self, edges, nodes, out_lat=None, out_loss=None):
+        return Router._run(self, N.lib().srg_multi_compute_shortest_paths, edges, nodes, out_lat, out_loss)
+
+
 class LocalGroup:
     """srg_local_group: N ranks inside one process (threads), e.g. several ranks on one GPU."""
 
@@ -390,22 +430,30 @@ class RoutingInfo:
         return int(v.value)
 
     def tables(self):
-        """(latency_ns u64 [n, n], packet_loss f32 [n, n], gml_ids u32 [n]) -- zero-copy views."""
+        """(latency_ns u64 [n, n], packet_loss f32 [n, n], gml_ids u32 [n]) -- zero-copy views of the
+        native tables.  Each array keeps this RoutingInfo alive (its numpy base holds a reference),
+        so the native memory outlives every view even when the RoutingInfo itself is dropped."""
         lp, fp, ip, n = N._u64p(), N._f32p(), N._u32p(), ctypes.c_uint32()
         N.lib().srg_routing_info_tables(self._h, ctypes.byref(lp), ctypes.byref(fp), ctypes.byref(ip), ctypes.byref(n))
         n = n.value
         if n == 0:
             return (np.zeros((0, 0), np.uint64), np.zeros((0, 0), np.float32), np.zeros(0, np.uint32))
-        return (np.ctypeslib.as_array(lp, shape=(n, n)), np.ctypeslib.as_array(fp, shape=(n, n)),
-                np.ctypeslib.as_array(ip, shape=(n,)))
+
+        def view(ptr, ctype, shape):
+            buf = (ctype * int(np.prod(shape))).from_address(ctypes.addressof(ptr.contents))
+            buf._owner = self  # the ctypes array holds the owner; numpy's base chain holds the array
+            return np.ctypeslib.as_array(buf).reshape(shape)
+
+        return (view(lp, ctypes.c_uint64, (n, n)), view(fp, ctypes.c_float, (n, n)), view(ip, ctypes.c_uint32, (n,)))
 
     def __len__(self):
         return int(N.lib().srg_routing_info_num_nodes(self._h)) ** 2
 
 
 def generate_routing_info(graph, nodes, use_shortest_paths=True, router=None):
-    """sim_config.rs:425-462 through srg_routing_info_build: GML ids -> NodeIndex, shortest or
-    direct paths on the GPU, a dense RoutingInfo keyed by GML id (no n^2 HashMap)."""
+    """sim_config.rs:425-462 through srg_routing_info_build (srg_routing_info_build_multi for a
+    MultiRouter): GML ids -> NodeIndex, shortest or direct paths on the GPU(s), a dense RoutingInfo
+    keyed by GML id (no n^2 HashMap)."""
     router = router or Router.default()
     ids = np.ascontiguousarray(list(nodes), dtype=np.uint32)
     edges = graph.edges if isinstance(graph, NetworkGraph) else graph
@@ -416,9 +464,9 @@ def generate_routing_info(graph, nodes, use_shortest_paths=True, router=None):
     h = ctypes.c_void_p()
     st = N.Stats()
     err = ctypes.create_string_buffer(2048)
-    rc = N.lib().srg_routing_info_build(router._h, ctypes.byref(el), ids.ctypes.data, len(ids),
-                                        1 if use_shortest_paths else 0, ctypes.byref(h), ctypes.byref(st), err,
-                                        len(err))
+    build = N.lib().srg_routing_info_build_multi if isinstance(router, MultiRouter) else N.lib().srg_routing_info_build
+    rc = build(router._h, ctypes.byref(el), ids.ctypes.data, len(ids), 1 if use_shortest_paths else 0, ctypes.byref(h),
+               ctypes.byref(st), err, len(err))
     if rc != N.SRG_OK:
         _raise(rc, err.value.decode(errors="replace"))
     return RoutingInfo(h, st.as_dict())

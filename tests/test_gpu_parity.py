@@ -230,6 +230,16 @@ def test_latency_range_is_an_error(router):
     assert_parity(t, lat, loss)
 
 
+def test_u64_edge_past_key_range_is_an_error(router):
+    """Documented deviation (include/shadow_routing.h SRG_ERR_LATENCY_RANGE): u64 keys hold
+    distances below 2^62, so an edge of 2^63 ns counts as absent and the used pair it alone
+    connects fails with SRG_ERR_LATENCY_RANGE, where the reference's u64 Dijkstra returns 2^63."""
+    e = Edges(2, [0, 1, 0], [0, 1, 1], np.array([1000, 1000, 2 ** 63], dtype=np.uint64), [0.0, 0.0, 0.0], directed=False)
+    with pytest.raises(NetGraphError) as ei:
+        router.compute_shortest_paths(e, [0, 1])
+    assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
+
+
 def test_deterministic_bytes(router):
     g = synth.random_graph(150, 0.2, 9, lat_hi=4, parallel=0.2)
     a = router.compute_shortest_paths(g, list(range(150)))

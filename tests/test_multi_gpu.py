@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from shadow_amd import LocalGroup, NetGraphError, Router, RoutingPanic, synth
+from shadow_amd import LocalGroup, MultiRouter, NetGraphError, Router, RoutingPanic, generate_routing_info, synth
 from shadow_amd import _native as N
 from helpers import bits_equal
 
@@ -88,23 +88,41 @@ def test_ranks_match_single_gpu(c):
 
 @pytest.mark.parametrize("kind", ["scrambled", "all"])
 def test_ranks_without_exchange_fill_own_rows(kind):
-    """Output exchange off: each rank fills the rows of the sources it owns (with sorted nodes
-    those rows are one block, and the host entry copies only that block to the caller)."""
+    """Output exchange off: rank r routes the sources at positions [n r / G, n (r+1) / G) of the
+    node list, whatever their order, and fills exactly those output rows; its min_latency_ns is the
+    minimum over those rows only (RoutingInfo::get_smallest_latency_ns, mod.rs:474-476)."""
     e = synth.random_graph(400, 0.04, 11)
     nodes = node_list(kind, 400, 11)
     lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
     out, errs = run_ranks(3, e, nodes, gather=False)
     assert errs == [None] * 3
     covered = np.zeros(len(nodes), dtype=bool)
-    T = 128
-    nb = (400 + T - 1) // T
+    n = len(nodes)
     for r, t in enumerate(out):
-        lo, hi = r * nb // 3 * T, (r + 1) * nb // 3 * T
-        rows = [i for i, v in enumerate(nodes) if lo <= v < hi]
+        rows = list(range(n * r // 3, n * (r + 1) // 3))
+        assert t.stats["local_sources"] == len(rows)
         assert np.array_equal(t.latency_ns[rows], lat[rows])
         assert bits_equal(t.packet_loss[rows], loss[rows])
+        assert t.stats["min_latency_ns"] == int(lat[rows].min())
         covered[rows] = True
     assert covered.all()
+
+
+def test_ranks_without_exchange_more_ranks_than_nodes():
+    """n < G: some ranks own no source; they ship nothing and report no minimum."""
+    e = synth.random_graph(150, 0.06, 14)
+    nodes = [3, 77, 140]
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
+    out, errs = run_ranks(5, e, nodes, gather=False)
+    assert errs == [None] * 5, errs
+    for r, t in enumerate(out):
+        rows = list(range(3 * r // 5, 3 * (r + 1) // 5))
+        assert t.stats["local_sources"] == len(rows)
+        if rows:
+            assert np.array_equal(t.latency_ns[rows], lat[rows]) and bits_equal(t.packet_loss[rows], loss[rows])
+            assert t.stats["min_latency_ns"] == int(lat[rows].min())
+        else:
+            assert t.stats["min_latency_ns"] == 2 ** 64 - 1
 
 
 @pytest.mark.parametrize("G,shard", [(2, 1), (3, 1), (4, 0), (8, 1)])
@@ -203,3 +221,143 @@ def test_c3_full_size_ranks_match_single_gpu(c3_single, G):
         assert np.array_equal(t.latency_ns, ref.latency_ns), f"rank {r} latency"
         assert bits_equal(t.packet_loss, ref.packet_loss), f"rank {r} loss"
     assert sum(t.stats["local_sources"] for t in out) == 10000
+
+
+# ---- srg_multi: one call, several GPUs (here: several ranks sharing the test box's one GPU) ----
+@pytest.mark.parametrize("G,kw,kind", [
+    (2, dict(V=700, dens=0.03, seed=41), "all"),
+    (3, dict(V=520, dens=0.05, seed=42), "scrambled"),
+    (8, dict(V=1100, dens=0.02, seed=43), "subset"),
+    (4, dict(V=260, dens=0.2, seed=44, lat_lo=2**31, lat_hi=2**33), "all"),   # u64 keys
+    (3, dict(V=300, dens=0.05, seed=45, directed=True), "scrambled"),         # general FW
+    (2, dict(V=2000, dens=0.003, seed=46, algorithm="sparse"), "all"),        # sparse path
+], ids=["G2", "G3_scrambled", "G8_subset", "G4_u64", "G3_directed", "G2_sparse"])
+def test_multi_router_matches_oracle(G, kw, kind):
+    """srg_multi_compute_shortest_paths: the whole table in the caller's arrays (every rank its own
+    rows), equal to the oracle; stats aggregate the ranks (sources summed, min latency over all)."""
+    kw = dict(kw)
+    V, dens, seed = kw.pop("V"), kw.pop("dens"), kw.pop("seed")
+    algo = kw.pop("algorithm", None)
+    e = synth.random_graph(V, dens, seed, **kw)
+    nodes = node_list(kind, V, seed)
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
+    m = MultiRouter([0] * G)
+    assert len(m) == G
+    if algo == "sparse":
+        m.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_SPARSE)
+    t = m.compute_shortest_paths(e, nodes)
+    m.close()
+    assert t.stats["nranks"] == G and t.stats["local_sources"] == len(nodes)
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+    assert t.stats["min_latency_ns"] == int(lat.min())
+
+
+def test_multi_router_big_table_registered_once():
+    """A table past the early-D2H threshold (64 MB): the caller's arrays are page-locked once for
+    all ranks and every rank ships its rows into them while later kernels run."""
+    V = 2600
+    e = synth.atlas_like(V, seed=2600)
+    nodes = np.random.default_rng(5).permutation(V).tolist()
+    r1 = Router(0)
+    ref = r1.compute_shortest_paths(e, nodes)
+    r1.close()
+    m = MultiRouter([0, 0, 0])
+    t = m.compute_shortest_paths(e, nodes)
+    m.close()
+    assert np.array_equal(t.latency_ns, ref.latency_ns) and bits_equal(t.packet_loss, ref.packet_loss)
+    assert t.stats["d2h_overlapped_bytes"] == V * V * 12
+    assert t.stats["ms_host_register"] >= 0
+
+
+def test_multi_router_errors_agree():
+    """A reference error (unreachable used pair -> the assert_eq! panic) surfaces once, from the
+    one call, with the single-GPU code and message; the object stays usable afterwards."""
+    iso = synth.random_graph(300, 0.05, 12)
+    keep = ((iso.src != 299) & (iso.dst != 299)) | (iso.src == iso.dst)
+    from shadow_amd.graph import Edges
+    e = Edges(300, iso.src[keep], iso.dst[keep], iso.latency_ns[keep], iso.packet_loss[keep], False)
+    m = MultiRouter([0, 0, 0, 0])
+    with pytest.raises(RoutingPanic):
+        m.compute_shortest_paths(e, list(range(300)))
+    ok = synth.random_graph(200, 0.05, 13)
+    lat, loss = oracle.compute_shortest_paths(ok.as_tuple(), list(range(200)))
+    t = m.compute_shortest_paths(ok, list(range(200)))
+    assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+    m.close()
+
+
+def test_routing_info_multi_and_rank_guard():
+    """srg_routing_info_build_multi builds the dense RoutingInfo with every rank; the per-rank
+    srg_routing_info_build refuses a context that fills only its own rows."""
+    e = synth.random_graph(250, 0.05, 15)
+    ids = list(range(250))
+    m = MultiRouter([0, 0])
+    ri = generate_routing_info(e, ids, router=m)
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), ids)
+    lt, ls, gid = ri.tables()
+    assert np.array_equal(lt, lat) and bits_equal(ls, loss)
+    assert ri.get_smallest_latency_ns() == int(lat.min())
+    del ri  # the views keep the native tables alive
+    import gc
+    gc.collect()
+    assert np.array_equal(lt, lat)
+    m.close()
+    group = LocalGroup(2)
+    rt = Router(0)
+    rt.init_comm_local(group, 0)
+    rt.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
+    with pytest.raises(NetGraphError) as ei:
+        generate_routing_info(e, ids, router=rt)
+    assert ei.value.code == N.SRG_ERR_ARG
+    rt.close()
+    group.close()
+
+
+@pytest.mark.slow
+def test_c4_multi_router_8_ranks():
+    """Config C4 (barabasi_albert(50000, 4, seed=50000)) built by 8 ranks through srg_multi: each
+    rank holds only its 6 250 rows on the device (3.75 GB) and ships them into the one 30 GB host
+    table.  Every row's checksum equals the single-GPU device table's, and 64 seeded rows equal
+    the oracle (mod.rs:190-208: independent per-source runs)."""
+    import torch
+    from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+    V = 50000
+    e = synth.barabasi_albert(V, 4, seed=V)
+    dev = torch.device("cuda", 0)
+    dg = DeviceGraph(e)
+    nodes_t = torch.arange(V, dtype=torch.int32, device=dev)
+    ol = torch.empty((V, V), dtype=torch.int64, device=dev)
+    os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
+    r1 = Router(0)
+    st = compute_shortest_paths_device(r1, dg, nodes_t, ol, os_)
+    assert st["path_kind"] == N.SRG_PATH_SPARSE_U32
+    ref_lat = ol.sum(dim=1).cpu().numpy()
+    ref_loss = os_.view(torch.int32).to(torch.int64).sum(dim=1).cpu().numpy()
+    del ol, os_, dg
+    r1.close()
+    torch.cuda.empty_cache()
+    m = MultiRouter([0] * 8)
+    t = m.compute_shortest_paths(e, np.arange(V, dtype=np.uint32))
+    m.close()
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32 and t.stats["local_sources"] == V
+    got_lat = t.latency_ns.view(np.int64).sum(axis=1)
+    got_loss = t.packet_loss.view(np.int32).astype(np.int64).sum(axis=1)
+    assert np.array_equal(got_lat, ref_lat) and np.array_equal(got_loss, ref_loss)
+    rows = np.random.default_rng(50000).choice(V, size=64, replace=False)
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), list(range(V)), rows=rows.tolist(), mode=1, nthreads=16)
+    assert np.array_equal(t.latency_ns[rows], lat) and bits_equal(t.packet_loss[rows], loss)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("G", [2, 8])
+def test_c3_multi_router(c3_single, G):
+    """Config C3 through srg_multi with G ranks: the distributed symmetric FW (line-buffer
+    allgathers, packed-triangle exchange) and the position-split sources give the single-GPU
+    table bit for bit, in the caller's one array."""
+    e, ref = c3_single
+    m = MultiRouter([0] * G)
+    t = m.compute_shortest_paths(e, list(range(10000)))
+    m.close()
+    assert t.stats["nranks"] == G and t.stats["local_sources"] == 10000
+    assert np.array_equal(t.latency_ns, ref.latency_ns)
+    assert bits_equal(t.packet_loss, ref.packet_loss)
