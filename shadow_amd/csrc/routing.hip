@@ -1149,7 +1149,8 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     // line 0: every rank holds the same initial D
     k_pack_line<T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
     close_pivot(LB[0], 0, st);
-    if (nb > 1) fw_line_lb<T><<<dim3(nb, 4), 256, lds_line, st>>>(D, Vp, LB[0], 0, LB[0], 0, 1, lm, g, prio);
+    // (with nb == 1 this only copies the closed pivot tile back to D)
+    fw_line_lb<T><<<dim3(nb, 4), 256, lds_line, st>>>(D, Vp, LB[0], 0, LB[0], 0, 1, lm, g, prio);
     HIP_CHECK(hipGetLastError());
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
@@ -2084,7 +2085,8 @@ __global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const 
 // the device.  Host threads narrow chunk i+1 into a page-locked ring while chunk i is in flight.
 // Returns false (nothing usable staged) when an endpoint >= 65536 or a latency >= 2^32 is seen:
 // the caller then ships the plain arrays, whose checks report such edges as the reference does.
-bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss);
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
+              bool& all_narrow);
 
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
@@ -2095,7 +2097,11 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
 
 // Ships edges [a0, a1) into the full-length device arrays (the rank's slice when the edge list
 // is sharded, else all of it).
-bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss) {
+// all_narrow: every edge of the slice also stays narrowed on the device (b_n16s / b_n16d / b_n32l),
+// false when the host-slow switch shipped the rest of the slice plain.
+bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
+              bool& all_narrow) {
+    all_narrow = true;
     const size_t E = g->num_edges, A = a1 - a0;
     constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
     constexpr int NB = 3;                   // ring slots
@@ -2184,6 +2190,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             if (with_loss)
                 HIP_CHECK(hipMemcpyAsync((float*)dg.loss + r0, g->packet_loss + r0, rn * 4, hipMemcpyHostToDevice, st));
             if (dbg) std::fprintf(stderr, "codec: host slow after chunk %zu (%.2f ms), rest plain\n", ch, dt);
+            all_narrow = false;
             break;
         }
     }
@@ -2333,8 +2340,9 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // late loss: the losses follow the endpoints and latencies on their own stream, beside
         // the W build and FW (dense u32 path: WL is built from them on c->loss_stream)
         const bool want_late = c->late_loss && !direct && !shard;
+        bool all_narrow = false;
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) && g->num_vertices <= 65536 &&
-                           codec_in(*c, g, dg, st, a0, a1, !want_late);
+                           codec_in(*c, g, dg, st, a0, a1, !want_late, all_narrow);
         LateLoss late;
         late.ls = c->loss_stream;
         if (coded && want_late) start_late_loss(*c, g, dg, st, late);
@@ -2371,7 +2379,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             c->sim_edges = g->src;
             c->sim_E = E;
         }
-        if (shard) {  // the wide arrays, so each rank may have shipped its slice coded or plain
+        if (shard) {
             std::vector<size_t> offs(nr), lens(nr);
             auto gather = [&](const void* p, size_t elem) {
                 for (int q = 0; q < nr; ++q) {
@@ -2381,10 +2389,37 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 }
                 c->comm->allgatherv(const_cast<void*>(p), offs.data(), lens.data(), st);
             };
-            gather(dg.src, 4);
-            gather(dg.dst, 4);
-            gather(dg.lat, 8);
-            gather(dg.loss, 4);
+            // every rank shipped its slice narrowed (the usual case): exchange the narrow arrays
+            // (12 B per edge with the loss instead of 20) and widen the other ranks' slices here;
+            // else the wide arrays, since a rank may have shipped its slice plain
+            uint32_t* plain = (uint32_t*)c->b_red.get(16);
+            const uint32_t mine = coded && all_narrow ? 0u : 1u;
+            HIP_CHECK(hipMemcpyAsync(plain, &mine, 4, hipMemcpyHostToDevice, st));
+            c->comm->allreduce_max_u32(plain, 1, st);
+            uint32_t any_plain = 1;
+            HIP_CHECK(hipMemcpyAsync(&any_plain, plain, 4, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            if (!any_plain) {
+                uint16_t* s16 = (uint16_t*)c->b_n16s.p;
+                uint16_t* d16 = (uint16_t*)c->b_n16d.p;
+                uint32_t* l32 = (uint32_t*)c->b_n32l.p;
+                gather(s16, 2);
+                gather(d16, 2);
+                gather(l32, 4);
+                gather(dg.loss, 4);
+                // (a simulated rank received nothing: its other slices are the wide ones put once)
+                for (auto [e0, e1] : {std::pair<size_t, size_t>{0, a0}, std::pair<size_t, size_t>{a1, E}})
+                    if (e1 > e0 && !sim)
+                        k_widen_edges<<<grid_for(e1 - e0), kThreads, 0, st>>>(e1 - e0, s16 + e0, d16 + e0, l32 + e0,
+                                                                               (uint32_t*)dg.src + e0, (uint32_t*)dg.dst + e0,
+                                                                               (uint64_t*)dg.lat + e0);
+                HIP_CHECK(hipGetLastError());
+            } else {
+                gather(dg.src, 4);
+                gather(dg.dst, 4);
+                gather(dg.lat, 8);
+                gather(dg.loss, 4);
+            }
         }
         const uint32_t* dn = stage_in(c->b_nodes, nodes, n, st);
         // multi-rank without the output exchange: the device holds only this rank's rows [p0, p1)

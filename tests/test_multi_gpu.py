@@ -230,7 +230,7 @@ def test_c3_full_size_ranks_match_single_gpu(c3_single, G):
     (8, dict(V=1100, dens=0.02, seed=43), "subset"),
     (4, dict(V=260, dens=0.2, seed=44, lat_lo=2**31, lat_hi=2**33), "all"),   # u64 keys
     (3, dict(V=300, dens=0.05, seed=45, directed=True), "scrambled"),         # general FW
-    (2, dict(V=2000, dens=0.003, seed=46, algorithm="sparse"), "all"),        # sparse path
+    (2, dict(V=2000, dens=0.0, seed=46, algorithm="sparse"), "all"),          # sparse path (BA graph)
 ], ids=["G2", "G3_scrambled", "G8_subset", "G4_u64", "G3_directed", "G2_sparse"])
 def test_multi_router_matches_oracle(G, kw, kind):
     """srg_multi_compute_shortest_paths: the whole table in the caller's arrays (every rank its own
@@ -238,7 +238,7 @@ def test_multi_router_matches_oracle(G, kw, kind):
     kw = dict(kw)
     V, dens, seed = kw.pop("V"), kw.pop("dens"), kw.pop("seed")
     algo = kw.pop("algorithm", None)
-    e = synth.random_graph(V, dens, seed, **kw)
+    e = synth.barabasi_albert(V, 3, seed=seed) if algo == "sparse" else synth.random_graph(V, dens, seed, **kw)
     nodes = node_list(kind, V, seed)
     lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
     m = MultiRouter([0] * G)
