@@ -767,14 +767,18 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(uint32_t* __restrict__ D, s
 //   mode 1 (line K1 w.r.t. its own closed pivot, every tile j = blockIdx.x): C = lbK's tile,
 //          operands from lbK; the result also goes to D when this rank owns the tile (rank g),
 //          and the closed pivot tile j == K1 is copied back to D by its owner.
-template <int T>
-__global__ void __launch_bounds__(256, 2) fw_line_lb(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lbL,
-                                                     int L, uint32_t* __restrict__ lbK, int K1, int mode, LineMap lm,
-                                                     int g, int prio) {
-    constexpr int TM = T / 2;
+// QUAD = false: one whole tile per workgroup (grid = (tiles, 1)): the throughput form, for one rank,
+// whose chain hides behind the bulk anyway.
+template <int T, bool QUAD>
+__global__ void __launch_bounds__(256, QUAD ? 2 : 3) fw_line_lb(uint32_t* __restrict__ D, size_t ld,
+                                                                const uint32_t* __restrict__ lbL, int L,
+                                                                uint32_t* __restrict__ lbK, int K1, int mode, LineMap lm,
+                                                                int g, int prio) {
+    constexpr int TM = QUAD ? T / 2 : T;
+    constexpr int KCL = QUAD ? 32 : 16;
     constexpr size_t TT = (size_t)T * T;
     const int j = mode == 0 ? lm.j0(g, K1) + lm.G * (int)blockIdx.x : (int)blockIdx.x;
-    const int q = (int)blockIdx.y, qi = q >> 1, qj = q & 1;
+    const int q = QUAD ? (int)blockIdx.y : 0, qi = q >> 1, qj = q & 1;
     const int I = min(j, K1), J = max(j, K1);
     const bool own = lm.owner(j, K1) == g;
     uint32_t* Dt = D + (size_t)I * T * ld + (size_t)J * T;
@@ -804,8 +808,8 @@ __global__ void __launch_bounds__(256, 2) fw_line_lb(uint32_t* __restrict__ D, s
     const uint32_t* Bb = lb + lm.slot(J, P) * TT + (bcol ? (size_t)qj * TM : (size_t)qj * TM * T);
     Dt += (size_t)qi * TM * ld + qj * TM;
     Lt += (size_t)qi * TM * T + qj * TM;
-    if (mode == 0) fw_core_lb<TM, T, 32>(Dt, ld, Ab, acol, Bb, bcol, T, Lt, T);
-    else fw_core_lb<TM, T, 32>(Lt, T, Ab, acol, Bb, bcol, T, own ? Dt : nullptr, ld);
+    if (mode == 0) fw_core_lb<TM, T, KCL>(Dt, ld, Ab, acol, Bb, bcol, T, Lt, T);
+    else fw_core_lb<TM, T, KCL>(Lt, T, Ab, acol, Bb, bcol, T, own ? Dt : nullptr, ld);
 }
 
 // One squaring step of the pivot-tile closure, Pout = min(Pin, Pin (x) Pin): 16 x 16 outputs per

@@ -1105,9 +1105,23 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     constexpr size_t TT = (size_t)T * T;
     const bool multi = c.comm && c.comm->nranks > 1;
     const LineMap lm{nb, G};
-    const size_t lds_bulk = lb_lds_bytes<T, KCS>(), lds_line = lb_lds_bytes<T / 2, 32>();
+    const size_t lds_bulk = lb_lds_bytes<T, KCS>();
     set_lds(fw_bulk_lb<T, KCS>, lds_bulk);
-    set_lds(fw_line_lb<T>, lds_line);
+    // The chain's line launches.  One rank: the chain runs beside a bulk of ~nb^2/2 tiles, so the
+    // lines take whole tiles (the fewest CU slots taken from the bulk).  Several ranks: the bulk
+    // shrinks with G and the chain is the critical path: 64 x 64 quadrants, 4x the workgroups at a
+    // quarter of the latency.  The pivot closure is eight squaring launches of 64 workgroups
+    // either way (the one-workgroup closure, fw_close_at, took 159 us beside the bulk against
+    // 8 x 12.4 us: profiles/r03/).
+    const bool quad = multi;
+    const size_t lds_line = quad ? lb_lds_bytes<T / 2, 32>() : lb_lds_bytes<T, KCS>();
+    set_lds(fw_line_lb<T, true>, lb_lds_bytes<T / 2, 32>());
+    set_lds(fw_line_lb<T, false>, lb_lds_bytes<T, KCS>());
+    auto line = [&](uint32_t* lbL, int L, uint32_t* lbK, int K1, int mode, int tiles, hipStream_t s) {
+        if (!tiles) return;
+        if (quad) fw_line_lb<T, true><<<dim3(tiles, 4), 256, lds_line, s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+        else fw_line_lb<T, false><<<dim3(tiles, 1), 256, lds_line, s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+    };
     const bool prof = c.profiling && nb > 2;
     if (prof) {
         while (c.prof_events.size() < (size_t)2 * nb) {
@@ -1141,16 +1155,15 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     if (ntile) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
     hipStream_t aux = c.aux_stream, cs = c.comm_stream;
     const int prio = c.chain_prio;
-    auto close_pivot = [&](uint32_t* lbk, int k, hipStream_t s) {  // eight squarings, ending in the buffer
+    auto close_pivot = [&](uint32_t* lbk, int k, hipStream_t s) {
         uint32_t* P = lbk + (size_t)lm.slot(k, k) * TT;
-        for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < 8; ++q)  // eight squarings, ending in the buffer
             fw_square<T><<<dim3(T / 16, T / 16), 256, 0, s>>>(q % 2 ? ptmp : P, q % 2 ? P : ptmp, cflags + 8 * k, q, prio);
     };
     // line 0: every rank holds the same initial D
     k_pack_line<T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
     close_pivot(LB[0], 0, st);
-    // (with nb == 1 this only copies the closed pivot tile back to D)
-    fw_line_lb<T><<<dim3(nb, 4), 256, lds_line, st>>>(D, Vp, LB[0], 0, LB[0], 0, 1, lm, g, prio);
+    line(LB[0], 0, LB[0], 0, 1, nb, st);  // (with nb == 1 this only copies the closed pivot tile back to D)
     HIP_CHECK(hipGetLastError());
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
@@ -1159,8 +1172,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
             uint32_t* lbn = LB[k1 & 1];
             HIP_CHECK(hipEventRecord(c.ev_a, st));  // st: bulk of kb - 1 done
             HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
-            const int mine = lm.count(g, k1);
-            if (mine) fw_line_lb<T><<<dim3(mine, 4), 256, lds_line, aux>>>(D, Vp, lbk, kb, lbn, k1, 0, lm, g, prio);
+            line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
             if (multi) {
                 std::vector<size_t> offs(G), lens(G);
                 for (int r = 0; r < G; ++r) {
@@ -1174,7 +1186,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
                 HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
             }
             close_pivot(lbn, k1, aux);
-            fw_line_lb<T><<<dim3(nb, 4), 256, lds_line, aux>>>(D, Vp, lbn, k1, lbn, k1, 1, lm, g, prio);
+            line(lbn, k1, lbn, k1, 1, nb, aux);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipEventRecord(c.ev_d, aux));
         }
@@ -1203,6 +1215,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         return;
     }
     // every rank ends with the whole D: pack the own tiles, all-gather, unpack with the mirror
+    HIP_CHECK(hipStreamSynchronize(st));  // (FW done: the exchange is timed on its own)
     auto t0x = std::chrono::steady_clock::now();
     uint32_t* Pk = (uint32_t*)c.b_PRED.get((size_t)ntri * TT * 4);
     int* slot = (int*)c.b_tslot.get((size_t)ntri * 4);
@@ -1227,6 +1240,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
 // General FW, several ranks: every rank ends with the whole D (row blocks all-gathered)
 template <class K>
 void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t st, double& ms_xchg) {
+    HIP_CHECK(hipStreamSynchronize(st));  // (FW done: the exchange is timed on its own)
     auto t0x = std::chrono::steady_clock::now();
     std::vector<size_t> offs(pl.G), lens(pl.G);
     for (int r = 0; r < pl.G; ++r) {
