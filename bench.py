@@ -257,7 +257,7 @@ def apply_options(router, args):
                       ("sparse_delta_div", "SPARSE_DELTA_DIV"), ("fw_symmetric", "FW_SYMMETRIC"),
                       ("chain_prio", "CHAIN_PRIO"), ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
                       ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
-                      ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE")):
+                      ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT")):
         v = getattr(args, flag)
         if v is not None:
             router.set_option(getattr(N, "SRG_OPT_" + opt), v)
@@ -498,6 +498,8 @@ def main():
                          "0 = every rank ships all, -1 = auto (default: on from 4 ranks)")
     ap.add_argument("--scan-groups", type=int, default=None, help="host entry: scan launches interleaved with the loss (0 = auto)")
     ap.add_argument("--loss-chunks", type=int, default=None, help="dense: k_loss_rows launches (0 = auto)")
+    ap.add_argument("--fw-line-split", type=int, default=None,
+                    help="symmetric FW: sub-tiles per dimension of the chain's line launches (1/2/4; 0 = auto)")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs; 0 = add + min3")

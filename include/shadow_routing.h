@@ -167,6 +167,9 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_LATE_LOSS 30         /* host entry: 1 (default) = the edge losses cross PCIe after the endpoints
                                      * and latencies, on their own stream beside the W build and FW (which
                                      * need no loss); 0 = with them */
+#define SRG_OPT_FW_LINE_SPLIT 31     /* symmetric FW: sub-tiles per dimension of the critical chain's line
+                                     * launches, 1 (whole 128-tiles) / 2 / 4; 0 (default) = 1 on one rank,
+                                     * 2 on several */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

@@ -219,12 +219,6 @@ __global__ void __launch_bounds__(NTH) fw_phase1(K* __restrict__ D, size_t ld, i
     phase1_body<K, T, NTH>(D + (size_t)kb * T * ld + (size_t)kb * T, ld, prio);
 }
 
-// close the T x T tile at `base` (row stride ld): the pivot tile inside a line buffer
-template <class K, int T, int NTH = 512>
-__global__ void __launch_bounds__(NTH) fw_close_at(K* __restrict__ base, size_t ld, int prio) {
-    phase1_body<K, T, NTH>(base, ld, prio);
-}
-
 // Stage a KC x T chunk of A^T (A rows i, columns k0..k0+KC) and of B (rows k0.., cols j)
 // into LDS.  A rows may be gathered through `arow` (row index per tile row).
 template <class K, int T, int KC>
@@ -758,8 +752,10 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(uint32_t* __restrict__ D, s
                          lb + lm.slot(J, L) * TT, J >= L, T, nullptr, 0);
 }
 
-// Line launches of the FW critical chain, one 64 x 64 quadrant of a line tile per workgroup
-// (grid = (tiles, 4)) so that a line takes one quadrant's latency instead of one tile's.
+// Line launches of the FW critical chain, one (T/S) x (T/S) sub-tile of a line tile per
+// workgroup (grid = (tiles, S*S)): S = 1 whole tiles (the throughput form, for one rank, whose chain
+// hides behind the bulk), S = 2 quadrants, S = 4 32 x 32 sub-tiles (several ranks: the bulk shrinks
+// with G and the chain is the critical path, so a line should take one small sub-tile's latency).
 //   mode 0 (line K1 w.r.t. pivot L, this rank's tiles of line K1: j = j0 + G * blockIdx.x):
 //          C = D tile (min(j,K1), max(j,K1)), operands from line L's buffer lbL; the result
 //          also goes to lbK.  j == L is not updated (that tile, (L, K1), is final in line L):
@@ -767,23 +763,24 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(uint32_t* __restrict__ D, s
 //   mode 1 (line K1 w.r.t. its own closed pivot, every tile j = blockIdx.x): C = lbK's tile,
 //          operands from lbK; the result also goes to D when this rank owns the tile (rank g),
 //          and the closed pivot tile j == K1 is copied back to D by its owner.
-// QUAD = false: one whole tile per workgroup (grid = (tiles, 1)): the throughput form, for one rank,
-// whose chain hides behind the bulk anyway.
-template <int T, bool QUAD>
-__global__ void __launch_bounds__(256, QUAD ? 2 : 3) fw_line_lb(uint32_t* __restrict__ D, size_t ld,
-                                                                const uint32_t* __restrict__ lbL, int L,
-                                                                uint32_t* __restrict__ lbK, int K1, int mode, LineMap lm,
-                                                                int g, int prio) {
-    constexpr int TM = QUAD ? T / 2 : T;
-    constexpr int KCL = QUAD ? 32 : 16;
+template <int S>
+constexpr int line_kc() { return S == 1 ? 16 : S == 2 ? 32 : 64; }
+
+template <int T, int S>
+__global__ void __launch_bounds__(256, S == 1 ? 3 : 2) fw_line_lb(uint32_t* __restrict__ D, size_t ld,
+                                                                  const uint32_t* __restrict__ lbL, int L,
+                                                                  uint32_t* __restrict__ lbK, int K1, int mode,
+                                                                  LineMap lm, int g, int prio) {
+    constexpr int TM = T / S;
+    constexpr int KCL = line_kc<S>();
     constexpr size_t TT = (size_t)T * T;
     const int j = mode == 0 ? lm.j0(g, K1) + lm.G * (int)blockIdx.x : (int)blockIdx.x;
-    const int q = QUAD ? (int)blockIdx.y : 0, qi = q >> 1, qj = q & 1;
+    const int q = (int)blockIdx.y, qi = q / S, qj = q % S;
     const int I = min(j, K1), J = max(j, K1);
     const bool own = lm.owner(j, K1) == g;
     uint32_t* Dt = D + (size_t)I * T * ld + (size_t)J * T;
     uint32_t* Lt = lbK + lm.slot(j, K1) * TT;
-    auto copy_quadrant = [&](const uint32_t* src, size_t lds_, uint32_t* dst, size_t ldd) {
+    auto copy_sub = [&](const uint32_t* src, size_t lds_, uint32_t* dst, size_t ldd) {
         src += (size_t)qi * TM * lds_ + qj * TM;
         dst += (size_t)qi * TM * ldd + qj * TM;
         for (int e = threadIdx.x; e < TM * TM / 4; e += 256) {
@@ -792,11 +789,11 @@ __global__ void __launch_bounds__(256, QUAD ? 2 : 3) fw_line_lb(uint32_t* __rest
         }
     };
     if (mode == 1 && j == K1) {  // the closed pivot tile itself: back to D on its owner
-        if (own) copy_quadrant(Lt, T, Dt, ld);
+        if (own) copy_sub(Lt, T, Dt, ld);
         return;
     }
     if (mode == 0 && j == L) {  // the final tile (L, K1) from line L's buffer
-        copy_quadrant(lbL + lm.slot(K1, L) * TT, T, Lt, T);
+        copy_sub(lbL + lm.slot(K1, L) * TT, T, Lt, T);
         return;
     }
     if (prio) __builtin_amdgcn_s_setprio(3);  // the chain runs beside the bulk tiles (see fw_phase1)
@@ -812,37 +809,78 @@ __global__ void __launch_bounds__(256, QUAD ? 2 : 3) fw_line_lb(uint32_t* __rest
     else fw_core_lb<TM, T, KCL>(Lt, T, Ab, acol, Bb, bcol, T, own ? Dt : nullptr, ld);
 }
 
-// One squaring step of the pivot-tile closure, Pout = min(Pin, Pin (x) Pin): 16 x 16 outputs per
-// workgroup, grid (T/16, T/16).  Eight steps (ping-pong, the last into the line buffer) close the
-// tile -- paths of up to 2^8 >= T hops inside the block; keys are integers, so any order of the
-// relaxations gives the same closure.  flags[s] records whether step s changed anything; a step
-// after an unchanged one only copies (the tile is closed).  Replaces the one-workgroup closure on
-// the multi-rank critical chain: 64 workgroups per step instead of one CU for 128^3 relaxations.
+// Grid barrier among the launch's workgroups, which must all be resident together (a few small
+// workgroups; no other kernel waits for them, so every one is eventually admitted).  The
+// MI355X_MICROARCH.md visibility recipe: every wave drains its stores, workgroup barrier, one lane
+// releases at agent scope, adds to the arrival counter and polls it relaxed (bounded: on a timeout
+// it raises *timeout and the caller gives up; the host reports the failure), then acquires.
+__device__ __forceinline__ bool grid_sync(uint32_t* cnt, uint32_t target, uint32_t* timeout, uint32_t* s_ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t ok = 1;
+        for (uint32_t spins = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
+            if (spins > (1u << 21) || __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// Close the T x T pivot tile P (row stride T, inside a line buffer) in ONE launch: repeated
+// squaring P <- min(P, P (x) P) in place, 16 x 16 outputs per workgroup, grid (T/16, T/16), the
+// workgroups meeting at a grid barrier after every step and stopping after the first step that
+// changed nothing (atlas pivot tiles: two changing steps and that one).  In place
+// is exact: keys only decrease and every value read, old or new, is the length of a path inside
+// the tile, so a step in which no workgroup changed anything read one consistent state and
+// P = min(P, P (x) P) holds there: P is closed.  Eight steps (paths of 2^8 >= T hops) always
+// suffice.  sync = {arrival counter, changed flag of steps 0 .. 7, ...} (16 words, zeroed before
+// the launch).  Keys <= INF = 2^31 - 1: no sum wraps.
 template <int T>
-__global__ void __launch_bounds__(256) fw_square(const uint32_t* __restrict__ Pin, uint32_t* __restrict__ Pout,
-                                                 uint32_t* __restrict__ flags, int step, int prio) {
+__global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uint32_t* __restrict__ sync,
+                                                   uint32_t* __restrict__ timeout, int prio) {
     if (prio) __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t A[16][T + 1];
     __shared__ uint32_t B[T][17];
+    __shared__ uint32_t s_chg, s_ok, s_more;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int r = blockIdx.y * 16 + ty, c = blockIdx.x * 16 + tx;
-    const uint32_t old = Pin[(size_t)r * T + c];
-    if (step > 0 && __hip_atomic_load(&flags[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        Pout[(size_t)r * T + c] = old;  // converged: keep the ping-pong consistent
-        return;
-    }
-    for (int e = threadIdx.x; e < 16 * T; e += 256) {
-        const int y = e / T, k = e % T;
-        A[y][k] = Pin[(size_t)(blockIdx.y * 16 + y) * T + k];
-        const int kk = e / 16, x = e % 16;
-        B[kk][x] = Pin[(size_t)kk * T + blockIdx.x * 16 + x];
-    }
-    __syncthreads();
-    uint32_t v = old;
+    const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;
+    const uint32_t nwg = gridDim.x * gridDim.y;
+    for (int step = 0; step < 8; ++step) {
+        if (threadIdx.x == 0) s_chg = 0;
+        for (int e = threadIdx.x; e < 16 * T; e += 256) {
+            const int y = e / T, k = e % T;
+            A[y][k] = P[(size_t)(r0 + y) * T + k];
+            const int kk = e / 16, x = e % 16;
+            B[kk][x] = P[(size_t)kk * T + c0 + x];
+        }
+        __syncthreads();
+        const uint32_t old = A[ty][c0 + tx];
+        uint32_t v = old;
 #pragma unroll 8
-    for (int k = 0; k < T; k += 2) v = KeyOps<uint32_t>::min3(v, A[ty][k] + B[k][tx], A[ty][k + 1] + B[k + 1][tx]);
-    Pout[(size_t)r * T + c] = v;
-    if (__ballot(v != old) && (threadIdx.x & 63) == 0) atomicOr(&flags[step], 1u);
+        for (int k = 0; k < T; k += 2) v = KeyOps<uint32_t>::min3(v, A[ty][k] + B[k][tx], A[ty][k + 1] + B[k + 1][tx]);
+        if (v < old) {
+            P[(size_t)(r0 + ty) * T + c0 + tx] = v;
+            s_chg = 1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && s_chg) __hip_atomic_fetch_or(&sync[1 + step], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!grid_sync(&sync[0], nwg * (uint32_t)(step + 1), timeout, &s_ok)) return;
+        if (threadIdx.x == 0) s_more = __hip_atomic_load(&sync[1 + step], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (!s_more) return;
+    }
 }
 
 // lb[slot(j)] <- stored tile (min(j, L), max(j, L)) of D, j = blockIdx.x

@@ -574,7 +574,14 @@ struct srg_ctx {
         b_gblk, b_DST, b_scantmp, b_ess, b_rlen, b_roff;
     // multi-rank: local sources, their output rows, exchange staging
     DevBuf b_lnodes, b_lpos, b_red, b_outoff, b_outdst;
-    DevBuf b_ptmp, b_cflags, b_tiles, b_tslot;  // symmetric FW: closure ping-pong + flags, own tiles, packed slots
+    DevBuf b_cflags, b_tiles, b_tslot;  // symmetric FW: closure barrier words, own tiles, packed slots
+    uint32_t* fw_timeout = nullptr;     // symmetric FW: raised by a closure grid barrier that timed out
+    int fw_line_split = 0;              // symmetric FW: line sub-tiles per dimension (0 = auto) (SRG_OPT_FW_LINE_SPLIT)
+    // cross-stream hops of the FW schedule: hipStreamWriteValue32 / WaitValue32 on HSA signal
+    // memory (5 us per hop measured against 11 us for an event record + wait, tools/xq_probe.hip);
+    // events where the device lacks stream memory operations
+    uint32_t* sig[2] = {nullptr, nullptr};
+    uint32_t sig_val[2] = {0, 0};
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -582,11 +589,13 @@ struct srg_ctx {
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
-                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_ptmp, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst,
+                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst,
                           &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
+        for (uint32_t* p : sig)
+            if (p) (void)hipFree(p);
         for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
@@ -883,6 +892,18 @@ struct HostSink {
     }
 };
 
+// `to` waits until `from` has reached this point (signal `i` of the context, else event `ev`)
+void stream_hop(srg_ctx& c, int i, hipStream_t from, hipStream_t to, hipEvent_t ev) {
+    if (c.sig[i]) {
+        const uint32_t v = ++c.sig_val[i];
+        HIP_CHECK(hipStreamWriteValue32(from, c.sig[i], v, 0));
+        HIP_CHECK(hipStreamWaitValue32(to, c.sig[i], v, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    } else {
+        HIP_CHECK(hipEventRecord(ev, from));
+        HIP_CHECK(hipStreamWaitEvent(to, ev, 0));
+    }
+}
+
 // ---- distribution plan --------------------------------------------------
 // G ranks.  FW ownership: the general FW gives rank r the whole rows of the row blocks
 // [blk_lo[r], blk_lo[r+1]); the symmetric FW gives it the stored tiles (I, J) with
@@ -1109,18 +1130,22 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     set_lds(fw_bulk_lb<T, KCS>, lds_bulk);
     // The chain's line launches.  One rank: the chain runs beside a bulk of ~nb^2/2 tiles, so the
     // lines take whole tiles (the fewest CU slots taken from the bulk).  Several ranks: the bulk
-    // shrinks with G and the chain is the critical path: 64 x 64 quadrants, 4x the workgroups at a
-    // quarter of the latency.  The pivot closure is eight squaring launches of 64 workgroups
-    // either way (the one-workgroup closure, fw_close_at, took 159 us beside the bulk against
-    // 8 x 12.4 us: profiles/r03/).
-    const bool quad = multi;
-    const size_t lds_line = quad ? lb_lds_bytes<T / 2, 32>() : lb_lds_bytes<T, KCS>();
-    set_lds(fw_line_lb<T, true>, lb_lds_bytes<T / 2, 32>());
-    set_lds(fw_line_lb<T, false>, lb_lds_bytes<T, KCS>());
+    // shrinks with G and the chain is the critical path: sub-tiles, S^2 x the workgroups at a
+    // fraction of the latency (SRG_OPT_FW_LINE_SPLIT).  The pivot closure is one launch of 64
+    // workgroups either way (fw_close_sq; eight squaring launches took 45-117 us per pivot, the
+    // one-workgroup FW closure 159 us beside the bulk: profiles/r03b/).
+    const int split = c.fw_line_split ? c.fw_line_split : (multi ? 2 : 1);
+    set_lds(fw_line_lb<T, 1>, lb_lds_bytes<T, line_kc<1>()>());
+    set_lds(fw_line_lb<T, 2>, lb_lds_bytes<T / 2, line_kc<2>()>());
+    set_lds(fw_line_lb<T, 4>, lb_lds_bytes<T / 4, line_kc<4>()>());
     auto line = [&](uint32_t* lbL, int L, uint32_t* lbK, int K1, int mode, int tiles, hipStream_t s) {
         if (!tiles) return;
-        if (quad) fw_line_lb<T, true><<<dim3(tiles, 4), 256, lds_line, s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
-        else fw_line_lb<T, false><<<dim3(tiles, 1), 256, lds_line, s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+        if (split == 4)
+            fw_line_lb<T, 4><<<dim3(tiles, 16), 256, lb_lds_bytes<T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+        else if (split == 2)
+            fw_line_lb<T, 2><<<dim3(tiles, 4), 256, lb_lds_bytes<T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+        else
+            fw_line_lb<T, 1><<<dim3(tiles, 1), 256, lb_lds_bytes<T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
     };
     const bool prof = c.profiling && nb > 2;
     if (prof) {
@@ -1131,9 +1156,11 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         }
     }
     uint32_t* LB[2] = {(uint32_t*)c.b_L0.get(nb * TT * 4), (uint32_t*)c.b_L1.get(nb * TT * 4)};
-    uint32_t* ptmp = (uint32_t*)c.b_ptmp.get(TT * 4);            // closure ping-pong
-    uint32_t* cflags = (uint32_t*)c.b_cflags.get((size_t)nb * 8 * 4);
-    HIP_CHECK(hipMemsetAsync(cflags, 0, (size_t)nb * 8 * 4, st));
+    // closure barrier words: 16 per pivot (arrival counter, changed flag per step), then the
+    // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
+    uint32_t* cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
+    c.fw_timeout = cflags + (size_t)nb * 16;
+    HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
     // this rank's tiles (triangle indices, row-major), and for the final exchange every tile's
     // slot in the packed buffer (owner-major, each owner's tiles in triangle order)
     const int ntri = nb * (nb + 1) / 2;
@@ -1156,9 +1183,8 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     hipStream_t aux = c.aux_stream, cs = c.comm_stream;
     const int prio = c.chain_prio;
     auto close_pivot = [&](uint32_t* lbk, int k, hipStream_t s) {
-        uint32_t* P = lbk + (size_t)lm.slot(k, k) * TT;
-        for (int q = 0; q < 8; ++q)  // eight squarings, ending in the buffer
-            fw_square<T><<<dim3(T / 16, T / 16), 256, 0, s>>>(q % 2 ? ptmp : P, q % 2 ? P : ptmp, cflags + 8 * k, q, prio);
+        fw_close_sq<T><<<dim3(T / 16, T / 16), 256, 0, s>>>(lbk + (size_t)lm.slot(k, k) * TT, cflags + 16 * k,
+                                                             c.fw_timeout, prio);
     };
     // line 0: every rank holds the same initial D
     k_pack_line<T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
@@ -1170,25 +1196,19 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         uint32_t* lbk = LB[kb & 1];
         if (k1 < nb) {
             uint32_t* lbn = LB[k1 & 1];
-            HIP_CHECK(hipEventRecord(c.ev_a, st));  // st: bulk of kb - 1 done
-            HIP_CHECK(hipStreamWaitEvent(aux, c.ev_a, 0));
+            stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
-            if (multi) {
+            if (multi) {  // on the chain's own stream: no cross-queue hop around it
                 std::vector<size_t> offs(G), lens(G);
                 for (int r = 0; r < G; ++r) {
                     offs[r] = (size_t)lm.base(r, k1) * TT * 4;
                     lens[r] = (size_t)lm.count(r, k1) * TT * 4;
                 }
-                HIP_CHECK(hipEventRecord(c.ev_b, aux));
-                HIP_CHECK(hipStreamWaitEvent(cs, c.ev_b, 0));
-                c.comm->allgatherv(lbn, offs.data(), lens.data(), cs);
-                HIP_CHECK(hipEventRecord(c.ev_c, cs));
-                HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
+                c.comm->allgatherv(lbn, offs.data(), lens.data(), aux);
             }
             close_pivot(lbn, k1, aux);
             line(lbn, k1, lbn, k1, 1, nb, aux);
             HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipEventRecord(c.ev_d, aux));
         }
         // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
         const bool timed = prof && ntile > 0 && k1 < nb;
@@ -1206,7 +1226,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
             prof_relax += (uint64_t)m * T * T * T;
             ++prof_n;
         }
-        if (k1 < nb) HIP_CHECK(hipStreamWaitEvent(st, c.ev_d, 0));
+        if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
     }
     HIP_CHECK(hipGetLastError());
     if (!multi) {
@@ -1327,6 +1347,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     }
     HIP_CHECK(hipGetLastError());
     const double ms_fw = tm.lap();
+    if (sym_fw_for<K, T>(c, g)) {
+        uint32_t tmo = 0;
+        HIP_CHECK(hipMemcpy(&tmo, c.fw_timeout, 4, hipMemcpyDeviceToHost));
+        if (tmo) fail(SRG_ERR_HIP, "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
+    }
     if (wl_late) {
         // WL = min loss among the min-latency parallel edges (what k_w_split gives), from the
         // losses that crossed PCIe during FW.  Built here, after FW, rather than beside it: on a
@@ -2552,6 +2577,13 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c->loss_stream = c->d2h_stream;
         for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        int wv = 0;
+        if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv) {
+            for (uint32_t*& p : c->sig) HIP_CHECK(hipExtMallocWithFlags((void**)&p, 8, hipMallocSignalMemory));
+            HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[0], 0, 0));
+            HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[1], 0, 0));
+            HIP_CHECK(hipStreamSynchronize(c->stream));
+        }
     });
     if (rc != SRG_OK) {
         delete c;
@@ -2647,6 +2679,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->d2h_mode = (int)value;
             return SRG_OK;
+        case SRG_OPT_FW_LINE_SPLIT:
+            if (value != 0 && value != 1 && value != 2 && value != 4) return SRG_ERR_ARG;
+            ctx->fw_line_split = (int)value;
+            return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
             ctx->algorithm = (int)value;
@@ -2680,6 +2716,7 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_H2D_CODEC: *value = ctx->h2d_codec; break;
         case SRG_OPT_EDGE_SHARD: *value = ctx->edge_shard; break;
         case SRG_OPT_LATE_LOSS: *value = ctx->late_loss; break;
+        case SRG_OPT_FW_LINE_SPLIT: *value = ctx->fw_line_split; break;
         default: return SRG_ERR_ARG;
     }
     return SRG_OK;
