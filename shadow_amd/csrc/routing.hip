@@ -271,16 +271,17 @@ __global__ void k_init_d(const K* __restrict__ W, K* __restrict__ D, size_t ld) 
 // INF in a used (row, column) pair (u32 certification).  Only used columns can change an
 // output: a stored key <= INF plus an edge w > 0 never falsely equals a finite D[s][t], so an
 // unreachable UNUSED vertex leaves the u32 result exact.
+// Row kernels over (used row x used column) arrays: one workgroup per row (grid = rows), the
+// threads striding over the columns -- no 64-bit division per element (the grid-stride form with
+// i / ncols ran 10x below HBM rate: 0.6 ms per C3 pass).
 template <class K>
-__global__ void k_certify(const K* __restrict__ D, size_t ld, const uint32_t* __restrict__ rows, uint32_t nrows,
-                          const uint32_t* __restrict__ cols, uint32_t ncols, Flags* flags) {
-    const size_t total = (size_t)nrows * ncols;
+__global__ void __launch_bounds__(256) k_certify(const K* __restrict__ D, size_t ld, const uint32_t* __restrict__ rows,
+                                                 uint32_t nrows, const uint32_t* __restrict__ cols, uint32_t ncols,
+                                                 Flags* flags) {
+    const K* Dr = D + (size_t)rows[blockIdx.x] * ld;
     uint32_t hit = 0;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / ncols, j = i - r * ncols;
-        hit |= D[(size_t)rows[r] * ld + cols[j]] == KeyOps<K>::INF;
-    }
-    if (hit) atomicOr(&flags->inf_in_used_row, 1u);
+    for (uint32_t j = threadIdx.x; j < ncols; j += blockDim.x) hit |= Dr[cols[j]] == KeyOps<K>::INF;
+    if (__ballot(hit) && (threadIdx.x & 63) == 0) atomicOr(&flags->inf_in_used_row, 1u);
 }
 
 template <class K>
@@ -321,14 +322,11 @@ __global__ void k_loss_round(const uint32_t* __restrict__ PRED, const K* __restr
     if (changed) atomicOr(&flags->changed, 1u);
 }
 
-__global__ void k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uint32_t V, size_t ld,
-                              unsigned long long* out) {
-    const size_t total = (size_t)n * V;
+__global__ void __launch_bounds__(256) k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uint32_t V,
+                                                     size_t ld, unsigned long long* out) {
+    const uint32_t* row = PRED + (size_t)blockIdx.x * ld;
     unsigned long long c = 0;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / V, t = i - r * V;
-        c += PRED[r * ld + t] == PRED_MULTI;
-    }
+    for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) c += row[t] == PRED_MULTI;
     if (c) atomicAdd(out, c);
 }
 
@@ -336,17 +334,19 @@ __global__ void k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uin
 // rowpos[a]; columns are the full `cols` (= nodes) list.  L == nullptr: out_loss was already
 // written by k_loss_rows.
 template <class K>
-__global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, size_t ld,
-                          const uint32_t* __restrict__ snodes, uint32_t nloc, const uint32_t* __restrict__ cols,
-                          uint32_t ncols, const uint32_t* __restrict__ rowpos,
-                          const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
-                          uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags, int mode) {
-    // mode bit 0: latency (+ unreachable check), bit 1: loss from L
-    const size_t total = (size_t)nloc * ncols;
+__global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const float* __restrict__ L, size_t ld,
+                                                 const uint32_t* __restrict__ snodes, uint32_t nloc,
+                                                 const uint32_t* __restrict__ cols, uint32_t ncols,
+                                                 const uint32_t* __restrict__ rowpos,
+                                                 const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
+                                                 uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags,
+                                                 int mode) {
+    // mode bit 0: latency (+ unreachable check), bit 1: loss from L; one workgroup per local row a
+    const uint32_t a = blockIdx.x;
+    const uint32_t s = snodes[a], p = rowpos[a];
     uint32_t unreach = 0;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t a = i / ncols, b = i - a * ncols;
-        const uint32_t s = snodes[a], t = cols[b], p = rowpos[a];
+    for (uint32_t b = threadIdx.x; b < ncols; b += blockDim.x) {
+        const uint32_t t = cols[b];
         const size_t o = (size_t)p * ncols + b;
         if (p == b) {
             // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
@@ -358,10 +358,10 @@ __global__ void k_extract(const K* __restrict__ D, const float* __restrict__ L, 
                 unreach |= d == KeyOps<K>::INF;
                 out_lat[o] = (uint64_t)d;
             }
-            if (mode & 2) out_loss[o] = L[a * ld + t];
+            if (mode & 2) out_loss[o] = L[(size_t)a * ld + t];
         }
     }
-    if (unreach) atomicOr(&flags->unreachable_used_pair, 1u);
+    if (__ballot(unreach) && (threadIdx.x & 63) == 0) atomicOr(&flags->unreachable_used_pair, 1u);
 }
 
 // min over a u64 array (RoutingInfo::get_smallest_latency_ns, mod.rs:474-476: all n^2 entries,
@@ -1131,10 +1131,11 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     // The chain's line launches.  One rank: the chain runs beside a bulk of ~nb^2/2 tiles, so the
     // lines take whole tiles (the fewest CU slots taken from the bulk).  Several ranks: the bulk
     // shrinks with G and the chain is the critical path: sub-tiles, S^2 x the workgroups at a
-    // fraction of the latency (SRG_OPT_FW_LINE_SPLIT).  The pivot closure is one launch of 64
+    // fraction of the latency (SRG_OPT_FW_LINE_SPLIT; 4 measured best at N = 8: FW 7.2 vs 7.7 ms
+    // with quadrants, profiles/r03c/).  The pivot closure is one launch of 64
     // workgroups either way (fw_close_sq; eight squaring launches took 45-117 us per pivot, the
     // one-workgroup FW closure 159 us beside the bulk: profiles/r03b/).
-    const int split = c.fw_line_split ? c.fw_line_split : (multi ? 2 : 1);
+    const int split = c.fw_line_split ? c.fw_line_split : (multi ? 4 : 1);
     set_lds(fw_line_lb<T, 1>, lb_lds_bytes<T, line_kc<1>()>());
     set_lds(fw_line_lb<T, 2>, lb_lds_bytes<T / 2, line_kc<2>()>());
     set_lds(fw_line_lb<T, 4>, lb_lds_bytes<T / 4, line_kc<4>()>());
@@ -1426,7 +1427,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
 
     // u32 certification: no saturated key in any used row (every rank must agree)
     HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
-    if (nloc) k_certify<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, Vp, lnodes, nloc, nodes, n, P.flags);
+    if (nloc) k_certify<K><<<nloc, kThreads, 0, st>>>(D, Vp, lnodes, nloc, nodes, n, P.flags);
     const uint32_t inf_any = reduce_flag(&P.flags->inf_in_used_row);
     if (sizeof(K) == 4 && inf_any) {
         // a used pair at INF: unreachable -- unless some path could reach 2^31-1 ns, in which case
@@ -1444,7 +1445,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // latency outputs (+ diagonal self-loops) of the own rows, right after FW
     HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
     if (nloc)
-        k_extract<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, nullptr, Vp, lnodes, nloc, nodes, n, lpos,
+        k_extract<K><<<nloc, kThreads, 0, st>>>(D, nullptr, Vp, lnodes, nloc, nodes, n, lpos,
                                                                       P.selflat, P.selfloss, out_lat, out_loss,
                                                                       P.flags, 1);
     HIP_CHECK(hipGetLastError());
@@ -1584,7 +1585,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 };
                 const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                 if (c1 == c0) continue;
-                tight_v5<<<8u * nbTT5 * ((c1 - c0 + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                const uint32_t nblk = (nbTT5 + 3) / 4 * ((c1 - c0 + 7) / 8);
+                tight_v5<<<8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
                     DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0, v5_goff,
                     (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
                 HIP_CHECK(hipGetLastError());
@@ -1598,7 +1600,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                     sink->send_rows(st, out_loss, sink->loss, pl.p0 + r0, r1 - r0, 4);
                 }
             }
-            k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
+            k_count_multi<<<nloc, kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
             HIP_CHECK(hipGetLastError());
             ms_scan = tm.lap();
             if (interleave) {  // loss rows already folded and shipped, group by group
@@ -1660,7 +1662,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             set_lds(tight_scan<K, TS, KC>, lds3);
             tight_scan<K, TS, KC><<<dim3((unsigned)(Vp / TS), (nloc + TS - 1) / TS), 256, lds3, st>>>(D, W, Vp, lnodes,
                                                                                                     nloc, PRED);
-            k_count_multi<<<grid_for((size_t)nloc * V), kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
+            k_count_multi<<<nloc, kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
             float* L0 = (float*)c.b_L0.get(nmax * Vp * 4);
             float* L1 = (float*)c.b_L1.get(nmax * Vp * 4);
             k_fill<float><<<grid_for((size_t)nloc * Vp), kThreads, 0, st>>>(L0, (size_t)nloc * Vp, 1.0f);
@@ -1688,7 +1690,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const double ms_loss = tm.lap();
 
     if (nloc && !loss_written)
-        k_extract<K><<<grid_for((size_t)nloc * n), kThreads, 0, st>>>(D, Lfin, Vp, lnodes, nloc, nodes, n, lpos,
+        k_extract<K><<<nloc, kThreads, 0, st>>>(D, Lfin, Vp, lnodes, nloc, nodes, n, lpos,
                                                                       P.selflat, P.selfloss, out_lat, out_loss,
                                                                       P.flags, 2);
     HIP_CHECK(hipGetLastError());

@@ -183,9 +183,13 @@ struct alignas(64) V5Grp {
 // k_loss_rows resolves with the exact u64 keys (DST / ent_w of type K).  Targets unreachable
 // from the source are not used pairs (certified before the scan) and are no tight predecessor
 // of a reachable target, so their entries are never read through a single match.
-// grid: 8 * nbTT * ceil((nbS - c0) / 8) workgroups of 512 for the source blocks [c0, nbS)
-// (XCD-aware: the workgroups of one XCD share the 128-source block, whose staged rows then come
-// out of that XCD's L2)
+// grid: 8 * 32 * ceil(nblk / 8) workgroups of 512 for the source blocks [c0, nbS), nblk =
+// ceil(nbTT / 4) * ceil((nbS - c0) / 8) blocks of 4 target tiles x 8 source blocks, dealt to the
+// XCDs in turn.  XCD-aware: an XCD holds two such blocks at once (2 workgroups per CU), so every
+// target tile's pair records are read by 8 workgroups together and every source block's staged
+// rows by 4, and both come out of that XCD's L2 after the first read.  (With one source block per
+// XCD the rows were shared 64 ways, but every record stream came from the Infinity Cache, and the
+// scalar record loads are what each group waits for.)
 __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
@@ -193,8 +197,9 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
                                                     uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
-    const uint32_t c = c0 + xcd + 8 * (slot / nbTT), b = slot % nbTT;
-    if (c >= nbS) return;  // whole workgroup: no barrier is left waiting
+    const uint32_t blk = (slot >> 5) * 8 + xcd, nbb = (nbTT + 3) / 4;  // block of 4 tiles x 8 source blocks
+    const uint32_t b = (blk % nbb) * 4 + (slot & 3), c = c0 + (blk / nbb) * 8 + ((slot >> 2) & 7);
+    if (c >= nbS || b >= nbTT) return;  // whole workgroup: no barrier is left waiting
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t r0 = c * V5_SB + 2 * lane;  // this lane's two sources (columns of DST)
