@@ -264,7 +264,10 @@ def apply_options(router, args):
 
 
 def workload_key(args, V, seed, world):
+    # "lb": the dense FW runs the line-buffer bulk kernel (fw_bulk_lb, round 3): PMC traffic
+    # collected on an earlier kernel (fw_product_sym) is not attached to it
     return (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "")
+            + ("lb:" if args.graph != "ba" else "")
             + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
             f"w{args.sparse_wgs or 2}"

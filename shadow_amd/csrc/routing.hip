@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -577,11 +578,6 @@ struct srg_ctx {
     DevBuf b_cflags, b_tiles, b_tslot;  // symmetric FW: closure barrier words, own tiles, packed slots
     uint32_t* fw_timeout = nullptr;     // symmetric FW: raised by a closure grid barrier that timed out
     int fw_line_split = 0;              // symmetric FW: line sub-tiles per dimension (0 = auto) (SRG_OPT_FW_LINE_SPLIT)
-    // cross-stream hops of the FW schedule: hipStreamWriteValue32 / WaitValue32 on HSA signal
-    // memory (5 us per hop measured against 11 us for an event record + wait, tools/xq_probe.hip);
-    // events where the device lacks stream memory operations
-    uint32_t* sig[2] = {nullptr, nullptr};
-    uint32_t sig_val[2] = {0, 0};
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -594,8 +590,6 @@ struct srg_ctx {
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
-        for (uint32_t* p : sig)
-            if (p) (void)hipFree(p);
         for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
@@ -892,16 +886,26 @@ struct HostSink {
     }
 };
 
-// `to` waits until `from` has reached this point (signal `i` of the context, else event `ev`)
-void stream_hop(srg_ctx& c, int i, hipStream_t from, hipStream_t to, hipEvent_t ev) {
-    if (c.sig[i]) {
-        const uint32_t v = ++c.sig_val[i];
-        HIP_CHECK(hipStreamWriteValue32(from, c.sig[i], v, 0));
-        HIP_CHECK(hipStreamWaitValue32(to, c.sig[i], v, hipStreamWaitValueGte, 0xFFFFFFFFu));
-    } else {
-        HIP_CHECK(hipEventRecord(ev, from));
-        HIP_CHECK(hipStreamWaitEvent(to, ev, 0));
-    }
+// The caller's output arrays are page-locked for the SDMA copies; a fresh array (the Rust
+// binding's vec![0u64; n*n] is lazily zeroed memory) is faulted in by that registration, 4 KB at
+// a time.  Advising transparent huge pages first (the boxes run THP in "madvise" mode) lets the
+// not-yet-touched part of the range fault in 2 MB pages: ~600 faults for the 1.2 GB C3 table
+// instead of ~300 000.  Advisory only: pages already present stay as they are.
+void advise_huge(void* p, size_t bytes) {
+    const uintptr_t a = ((uintptr_t)p + ((size_t)2 << 20) - 1) & ~(uintptr_t)(((size_t)2 << 20) - 1);
+    const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)(((size_t)2 << 20) - 1);
+    if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
+}
+
+// `to` waits until `from` has reached this point.  Events, not stream memory operations:
+// hipStreamWaitValue32 was measured faster per hop (5 vs 11 us, tools/xq_probe.hip) but it is a
+// polling kernel the runtime knows nothing about -- with streams sharing a hardware queue
+// (GPU_MAX_HW_QUEUES = 4, several contexts per process) or a profiler that serialises dispatches
+// (rocprofv3 --pmc hung on it), a wait can sit in front of the write it waits for.
+void stream_hop(srg_ctx& c, hipStream_t from, hipStream_t to, hipEvent_t ev) {
+    (void)c;
+    HIP_CHECK(hipEventRecord(ev, from));
+    HIP_CHECK(hipStreamWaitEvent(to, ev, 0));
 }
 
 // ---- distribution plan --------------------------------------------------
@@ -1197,7 +1201,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         uint32_t* lbk = LB[kb & 1];
         if (k1 < nb) {
             uint32_t* lbn = LB[k1 & 1];
-            stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
+            stream_hop(c, st, aux, c.ev_a);  // st: bulk of kb - 1 done
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
             if (multi) {  // on the chain's own stream: no cross-queue hop around it
                 std::vector<size_t> offs(G), lens(G);
@@ -1227,7 +1231,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
             prof_relax += (uint64_t)m * T * T * T;
             ++prof_n;
         }
-        if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
+        if (k1 < nb) stream_hop(c, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
     }
     HIP_CHECK(hipGetLastError());
     if (!multi) {
@@ -2351,6 +2355,8 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         reg.th = std::thread([&reg]() {
             const auto t0 = std::chrono::steady_clock::now();
             if (hipSetDevice(reg.device) != hipSuccess) return;
+            advise_huge(reg.p[0], reg.b[0]);
+            advise_huge(reg.p[1], reg.b[1]);
             if (hipHostRegister(reg.p[0], reg.b[0], hipHostRegisterMapped) != hipSuccess) return;
             if (hipHostRegister(reg.p[1], reg.b[1], hipHostRegisterMapped) != hipSuccess) {
                 (void)hipHostUnregister(reg.p[0]);
@@ -2579,13 +2585,6 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c->loss_stream = c->d2h_stream;
         for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        int wv = 0;
-        if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv) {
-            for (uint32_t*& p : c->sig) HIP_CHECK(hipExtMallocWithFlags((void**)&p, 8, hipMallocSignalMemory));
-            HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[0], 0, 0));
-            HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[1], 0, 0));
-            HIP_CHECK(hipStreamSynchronize(c->stream));
-        }
     });
     if (rc != SRG_OK) {
         delete c;
@@ -2918,6 +2917,8 @@ int srg_multi_compute_shortest_paths(srg_multi* m, const srg_edge_list* graph, c
             const auto ts = std::chrono::steady_clock::now();
             if (hipSetDevice(dev0) != hipSuccess) return;
             const unsigned fl = hipHostRegisterPortable | hipHostRegisterMapped;
+            advise_huge(reg.p[0], reg.b[0]);
+            advise_huge(reg.p[1], reg.b[1]);
             if (hipHostRegister(reg.p[0], reg.b[0], fl) != hipSuccess) return;
             if (hipHostRegister(reg.p[1], reg.b[1], fl) != hipSuccess) {
                 (void)hipHostUnregister(reg.p[0]);

@@ -3,10 +3,10 @@ tools/pmc_fw.sh output directory -> profiles/fw_pmc_latest.json (read by bench.p
 
 usage: python tools/pmc_extract.py PMC_DIR SOURCE_TEXT [WORKLOAD_KEY] [KERNEL_SUBSTR]
 WORKLOAD_KEY is bench.py's key of the run the passes profiled (bench.py reports the traffic only
-for a run with the same key); KERNEL_SUBSTR defaults to fw_product_sym (the symmetric bulk tile).
+for a run with the same key); KERNEL_SUBSTR defaults to fw_bulk_lb (the symmetric bulk tile).
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB and on
 gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads, so hbm = 2*FETCH + WRITE.
-The bulk launches are the largest-grid fw_product dispatches (grid >= 90% of the maximum).
+The bulk launches are the largest-grid dispatches of that kernel (grid >= 90% of the maximum).
 """
 import collections
 import csv
@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     d, source = sys.argv[1], sys.argv[2]
     wkey = sys.argv[3] if len(sys.argv) > 3 else None
-    ksub = sys.argv[4] if len(sys.argv) > 4 else "fw_product_sym<"
+    ksub = sys.argv[4] if len(sys.argv) > 4 else "fw_bulk_lb<"
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     grids = collections.defaultdict(int)
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
