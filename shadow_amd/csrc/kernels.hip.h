@@ -810,16 +810,17 @@ __global__ void __launch_bounds__(256, S == 1 ? 3 : 2) fw_line_lb(uint32_t* __re
 }
 
 // Grid barrier among the launch's workgroups, which must all be resident together (a few small
-// workgroups; no other kernel waits for them, so every one is eventually admitted).  The
-// MI355X_MICROARCH.md visibility recipe: every wave drains its stores, workgroup barrier, one lane
-// releases at agent scope, adds to the arrival counter and polls it relaxed (bounded: on a timeout
-// it raises *timeout and the caller gives up; the host reports the failure), then acquires.
+// workgroups; no other kernel waits for them, so every one is eventually admitted).  Write-through
+// form of the MI355X_MICROARCH.md hand-off (its "sc1 stores, sc1 loads" row): every byte handed
+// across the barrier is stored and loaded with agent-scope (sc1) accesses, every wave drains its
+// stores, and after a workgroup barrier one lane adds to the arrival counter and polls it
+// (bounded: on a timeout it raises *timeout and the caller gives up; the host reports it).  No
+// release / acquire fence: the release's L2 write-back (buffer_wbl2) also flushes whatever the
+// FW bulk tiles beside this kernel have dirtied in the XCD's L2.
 __device__ __forceinline__ bool grid_sync(uint32_t* cnt, uint32_t target, uint32_t* timeout, uint32_t* s_ok) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t ok = 1;
         for (uint32_t spins = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
@@ -830,12 +831,14 @@ __device__ __forceinline__ bool grid_sync(uint32_t* cnt, uint32_t target, uint32
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         *s_ok = ok;
     }
     __syncthreads();
     return *s_ok != 0;
+}
+
+__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Close the T x T pivot tile P (row stride T, inside a line buffer) in ONE launch: repeated
@@ -846,7 +849,8 @@ __device__ __forceinline__ bool grid_sync(uint32_t* cnt, uint32_t target, uint32
 // the tile, so a step in which no workgroup changed anything read one consistent state and
 // P = min(P, P (x) P) holds there: P is closed.  Eight steps (paths of 2^8 >= T hops) always
 // suffice.  sync = {arrival counter, changed flag of steps 0 .. 7, ...} (16 words, zeroed before
-// the launch).  Keys <= INF = 2^31 - 1: no sum wraps.
+// the launch).  Keys <= INF = 2^31 - 1: no sum wraps.  P is read and written write-through
+// (grid_sync); the previous kernel's plain stores are visible at the launch boundary.
 template <int T>
 __global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uint32_t* __restrict__ sync,
                                                    uint32_t* __restrict__ timeout, int prio) {
@@ -857,13 +861,31 @@ __global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uin
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;
     const uint32_t nwg = gridDim.x * gridDim.y;
+    // write-through (sc1, aux = 16) 16-B loads of the 16 rows and 16 columns this workgroup needs
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)(T * T * 4), 0x00027000);
+    constexpr int NV = 16 * T / 4 / 256;  // 16-B vectors per thread per operand
+    static_assert(NV >= 1 && 16 * T / 4 % 256 == 0, "closure staging");
     for (int step = 0; step < 8; ++step) {
         if (threadIdx.x == 0) s_chg = 0;
-        for (int e = threadIdx.x; e < 16 * T; e += 256) {
-            const int y = e / T, k = e % T;
-            A[y][k] = P[(size_t)(r0 + y) * T + k];
-            const int kk = e / 16, x = e % 16;
-            B[kk][x] = P[(size_t)kk * T + c0 + x];
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        v4u va[NV], vb[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int v = threadIdx.x + 256 * q;
+            const int y = v / (T / 4), k4 = v % (T / 4);    // A: row r0 + y, columns 4 k4 ..
+            const int kk = v / 4, x4 = v % 4;               // B: row kk, columns c0 + 4 x4 ..
+            va[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r0 + y) * T + 4 * k4) * 4, 0, 16);
+            vb[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (kk * T + c0 + 4 * x4) * 4, 0, 16);
+        }
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int v = threadIdx.x + 256 * q;
+            const int y = v / (T / 4), k4 = v % (T / 4), kk = v / 4, x4 = v % 4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                A[y][4 * k4 + e] = va[q][e];
+                B[kk][4 * x4 + e] = vb[q][e];
+            }
         }
         __syncthreads();
         const uint32_t old = A[ty][c0 + tx];
@@ -871,7 +893,7 @@ __global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uin
 #pragma unroll 8
         for (int k = 0; k < T; k += 2) v = KeyOps<uint32_t>::min3(v, A[ty][k] + B[k][tx], A[ty][k + 1] + B[k + 1][tx]);
         if (v < old) {
-            P[(size_t)(r0 + ty) * T + c0 + tx] = v;
+            st_wt(&P[(size_t)(r0 + ty) * T + c0 + tx], v);
             s_chg = 1;
         }
         __syncthreads();
