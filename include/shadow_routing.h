@@ -169,7 +169,7 @@ void srg_destroy(srg_ctx* ctx);
                                      * need no loss); 0 = with them */
 #define SRG_OPT_FW_LINE_SPLIT 31     /* symmetric FW: sub-tiles per dimension of the critical chain's line
                                      * launches, 1 (whole 128-tiles) / 2 / 4; 0 (default) = 1 on one rank,
-                                     * 4 on several */
+                                     * 2 on two, 4 on more */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -577,6 +578,9 @@ struct srg_ctx {
     DevBuf b_lnodes, b_lpos, b_red, b_outoff, b_outdst;
     DevBuf b_cflags, b_tiles, b_tslot;  // symmetric FW: closure barrier words, own tiles, packed slots
     uint32_t* fw_timeout = nullptr;     // symmetric FW: raised by a closure grid barrier that timed out
+    uint32_t* sig[2] = {nullptr, nullptr};  // stream_hop signals (HSA signal memory), their last values
+    uint32_t sig_val[2] = {0, 0};
+    bool hop_values = false;            // this build's hops use the signals (stream_hop)
     int fw_line_split = 0;              // symmetric FW: line sub-tiles per dimension (0 = auto) (SRG_OPT_FW_LINE_SPLIT)
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
@@ -590,6 +594,8 @@ struct srg_ctx {
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
+        for (uint32_t* p : sig)
+            if (p) (void)hipFree(p);
         for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
@@ -897,13 +903,27 @@ void advise_huge(void* p, size_t bytes) {
     if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
 }
 
-// `to` waits until `from` has reached this point.  Events, not stream memory operations:
-// hipStreamWaitValue32 was measured faster per hop (5 vs 11 us, tools/xq_probe.hip) but it is a
-// polling kernel the runtime knows nothing about -- with streams sharing a hardware queue
-// (GPU_MAX_HW_QUEUES = 4, several contexts per process) or a profiler that serialises dispatches
-// (rocprofv3 --pmc hung on it), a wait can sit in front of the write it waits for.
-void stream_hop(srg_ctx& c, hipStream_t from, hipStream_t to, hipEvent_t ev) {
-    (void)c;
+// Contexts per device in this process (srg_create / srg_destroy): the FW's cross-stream hops
+// use stream memory operations only when a context is alone on its device (stream_hop).
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_ctx;
+
+// `to` waits until `from` has reached this point.  hipStreamWriteValue32 + hipStreamWaitValue32 on
+// HSA signal memory cost 5 us per hop against 11 us for hipEventRecord + hipStreamWaitEvent
+// (tools/xq_probe.hip; 1-3 ms of FW at N = 2..8).  The wait is a polling kernel the
+// runtime knows nothing about, so it is safe only while every wait is queued behind the write it
+// waits for: true for one context (its host thread enqueues each write before the wait, and
+// streams sharing a hardware queue keep that order), not for several contexts on one device
+// (in-process rank groups: two waits could each block the queue holding the other's write), nor
+// under a profiler that serialises dispatches (rocprofv3 --pmc hung on it): those use events
+// (and SRG_STREAM_HOPS=events forces them).
+void stream_hop(srg_ctx& c, int i, hipStream_t from, hipStream_t to, hipEvent_t ev) {
+    if (c.hop_values && c.sig[i]) {
+        const uint32_t v = ++c.sig_val[i];
+        HIP_CHECK(hipStreamWriteValue32(from, c.sig[i], v, 0));
+        HIP_CHECK(hipStreamWaitValue32(to, c.sig[i], v, hipStreamWaitValueGte, 0xFFFFFFFFu));
+        return;
+    }
     HIP_CHECK(hipEventRecord(ev, from));
     HIP_CHECK(hipStreamWaitEvent(to, ev, 0));
 }
@@ -1130,16 +1150,22 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     constexpr size_t TT = (size_t)T * T;
     const bool multi = c.comm && c.comm->nranks > 1;
     const LineMap lm{nb, G};
+    {
+        const char* hv = std::getenv("SRG_STREAM_HOPS");
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        c.hop_values = g_dev_ctx[c.device] == 1 && !(hv && std::strcmp(hv, "events") == 0);
+    }
     const size_t lds_bulk = lb_lds_bytes<T, KCS>();
     set_lds(fw_bulk_lb<T, KCS>, lds_bulk);
     // The chain's line launches.  One rank: the chain runs beside a bulk of ~nb^2/2 tiles, so the
     // lines take whole tiles (the fewest CU slots taken from the bulk).  Several ranks: the bulk
     // shrinks with G and the chain is the critical path: sub-tiles, S^2 x the workgroups at a
-    // fraction of the latency (SRG_OPT_FW_LINE_SPLIT; 4 measured best at N = 8: FW 7.2 vs 7.7 ms
-    // with quadrants, profiles/r03c/).  The pivot closure is one launch of 64
+    // fraction of the latency (SRG_OPT_FW_LINE_SPLIT; measured FW at sim 2:0 / 4:0 / 8:0 with whole
+    // tiles, quadrants, 32 x 32: 17.9 / 15.1 / 15.6, 14.9 / 12.2 / 12.1, 11.0 / 7.7 / 7.2 ms,
+    // profiles/r03c/, r03k/).  The pivot closure is one launch of 64
     // workgroups either way (fw_close_sq; eight squaring launches took 45-117 us per pivot, the
     // one-workgroup FW closure 159 us beside the bulk: profiles/r03b/).
-    const int split = c.fw_line_split ? c.fw_line_split : (multi ? 4 : 1);
+    const int split = c.fw_line_split ? c.fw_line_split : !multi ? 1 : G < 4 ? 2 : 4;
     set_lds(fw_line_lb<T, 1>, lb_lds_bytes<T, line_kc<1>()>());
     set_lds(fw_line_lb<T, 2>, lb_lds_bytes<T / 2, line_kc<2>()>());
     set_lds(fw_line_lb<T, 4>, lb_lds_bytes<T / 4, line_kc<4>()>());
@@ -1201,7 +1227,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         uint32_t* lbk = LB[kb & 1];
         if (k1 < nb) {
             uint32_t* lbn = LB[k1 & 1];
-            stream_hop(c, st, aux, c.ev_a);  // st: bulk of kb - 1 done
+            stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
             if (multi) {  // on the chain's own stream: no cross-queue hop around it
                 std::vector<size_t> offs(G), lens(G);
@@ -1231,7 +1257,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
             prof_relax += (uint64_t)m * T * T * T;
             ++prof_n;
         }
-        if (k1 < nb) stream_hop(c, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
+        if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
     }
     HIP_CHECK(hipGetLastError());
     if (!multi) {
@@ -2585,6 +2611,15 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c->loss_stream = c->d2h_stream;
         for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        int wv = 0;
+        if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv) {
+            for (uint32_t*& p : c->sig) HIP_CHECK(hipExtMallocWithFlags((void**)&p, 8, hipMallocSignalMemory));
+            HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[0], 0, 0));
+            HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[1], 0, 0));
+            HIP_CHECK(hipStreamSynchronize(c->stream));
+        }
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        ++g_dev_ctx[device];
     });
     if (rc != SRG_OK) {
         delete c;
@@ -2726,6 +2761,10 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
 void srg_destroy(srg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    {
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        --g_dev_ctx[ctx->device];
+    }
     delete ctx;
 }
 

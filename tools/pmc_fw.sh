@@ -4,6 +4,8 @@
 set -e
 out=$1; shift
 export TMPDIR=/tmp
+# rocprofv3 --pmc serialises dispatches: the FW cross-stream hops must be events (routing.hip stream_hop)
+export SRG_STREAM_HOPS=events
 mkdir -p "$out"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o run -- python3 -u bench.py --steps 1 --warmup 1 --no-cpu --no-profile "$@" > "$out/stats.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu --no-profile "$@" > "$out/fetch.log" 2>&1
