@@ -282,7 +282,20 @@ __global__ void __launch_bounds__(256) k_certify(const K* __restrict__ D, size_t
                                                  Flags* flags) {
     const K* Dr = D + (size_t)rows[blockIdx.x] * ld;
     uint32_t hit = 0;
-    for (uint32_t j = threadIdx.x; j < ncols; j += blockDim.x) hit |= Dr[cols[j]] == KeyOps<K>::INF;
+    constexpr uint32_t U = 8;  // independent loads in flight per thread (the gather is latency-bound)
+    for (uint32_t j0 = threadIdx.x; j0 < ncols; j0 += blockDim.x * U) {
+        uint32_t cc[U];
+        K d[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t j = j0 + u * blockDim.x;
+            cc[u] = cols[j < ncols ? j : 0];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) d[u] = Dr[cc[u]];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) hit |= (j0 + u * blockDim.x < ncols) & (d[u] == KeyOps<K>::INF);
+    }
     if (__ballot(hit) && (threadIdx.x & 63) == 0) atomicOr(&flags->inf_in_used_row, 1u);
 }
 
@@ -343,24 +356,45 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
                                                  const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
                                                  uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags,
                                                  int mode) {
-    // mode bit 0: latency (+ unreachable check), bit 1: loss from L; one workgroup per local row a
+    // mode bit 0: latency (+ unreachable check), bit 1: loss from L; one workgroup per local row a,
+    // U columns per thread in flight (the gathers are latency-bound)
     const uint32_t a = blockIdx.x;
     const uint32_t s = snodes[a], p = rowpos[a];
+    const K* Ds = D + (size_t)s * ld;
+    const float* La = L ? L + (size_t)a * ld : nullptr;
+    uint64_t* ol = out_lat + (size_t)p * ncols;
+    float* os = out_loss + (size_t)p * ncols;
     uint32_t unreach = 0;
-    for (uint32_t b = threadIdx.x; b < ncols; b += blockDim.x) {
-        const uint32_t t = cols[b];
-        const size_t o = (size_t)p * ncols + b;
-        if (p == b) {
-            // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
-            if (mode & 1) out_lat[o] = self_lat[s];
-            if (mode & 2) out_loss[o] = self_loss[s];
-        } else {
-            if (mode & 1) {
-                const K d = D[(size_t)s * ld + t];
-                unreach |= d == KeyOps<K>::INF;
-                out_lat[o] = (uint64_t)d;
+    constexpr uint32_t U = 4;
+    for (uint32_t b0 = threadIdx.x; b0 < ncols; b0 += blockDim.x * U) {
+        uint32_t tt[U];
+        K d[U];
+        float l[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t b = b0 + u * blockDim.x;
+            tt[u] = cols[b < ncols ? b : 0];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (mode & 1) d[u] = Ds[tt[u]];
+            if (mode & 2) l[u] = La[tt[u]];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t b = b0 + u * blockDim.x;
+            if (b >= ncols) break;
+            if (p == b) {
+                // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
+                if (mode & 1) ol[b] = self_lat[s];
+                if (mode & 2) os[b] = self_loss[s];
+            } else {
+                if (mode & 1) {
+                    unreach |= d[u] == KeyOps<K>::INF;
+                    ol[b] = (uint64_t)d[u];
+                }
+                if (mode & 2) os[b] = l[u];
             }
-            if (mode & 2) out_loss[o] = L[(size_t)a * ld + t];
         }
     }
     if (__ballot(unreach) && (threadIdx.x & 63) == 0) atomicOr(&flags->unreachable_used_pair, 1u);

@@ -150,6 +150,29 @@ def test_fw_symmetric_matches_general(V):
         assert_parity(out[1], lat, loss)
 
 
+def test_fw_stream_hops_events_match_values(monkeypatch):
+    """The FW's two cross-stream hops per pivot as stream-value waits (a context alone on its
+    device) and as events (SRG_STREAM_HOPS=events: several contexts per device, profilers) give
+    the same table bit for bit, and the oracle's rows (routing.hip stream_hop)."""
+    V = 1500
+    g = synth.atlas_like(V, seed=91)
+    nodes = list(range(V))
+    out = []
+    for hops in (None, "events"):
+        if hops:
+            monkeypatch.setenv("SRG_STREAM_HOPS", hops)
+        else:
+            monkeypatch.delenv("SRG_STREAM_HOPS", raising=False)
+        r = Router(0)
+        out.append(r.compute_shortest_paths(g, nodes))
+        r.close()
+    assert np.array_equal(out[0].latency_ns, out[1].latency_ns)
+    assert bits_equal(out[0].packet_loss, out[1].packet_loss)
+    rows = [0, 777, V - 1]
+    lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes, rows=rows, mode=2)
+    assert np.array_equal(out[0].latency_ns[rows], lat) and bits_equal(out[0].packet_loss[rows], loss)
+
+
 def test_scan_ragged_sources():
     """Several 128-source blocks, target tiles and u-chunks, with n and V off every block size and
     a used-node subset in random order (lanes past n, targets past V, sentinel pairs)."""
