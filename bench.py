@@ -369,6 +369,7 @@ def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, rooflin
         "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
         "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
         "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
+        "latency_unit_ns": s["latency_unit_ns"],
         "roofline": roofline, "cpu_baseline": cpu, **extra,
     }
     print(json.dumps(line), flush=True)
@@ -469,7 +470,8 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--lat-scale", type=int, default=1,
                     help="multiply every edge latency by this factor (e.g. 1000 puts C3's used paths past "
-                         "2^31 ns, so the u64-key FW runs: the u64 path benchmark)")
+                         "2^31 ns; the latency unit then keeps u32 keys in units of the latencies' gcd, and "
+                         "SRG_LATENCY_UNIT=1 in the environment forces nanosecond keys: the u64 path benchmark)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")

@@ -38,13 +38,14 @@ extern "C" {
 #define SRG_ERR_MULTI_EDGE 3    /* "More than one edge connecting node {a} to {b}"      mod.rs:269-274 */
 #define SRG_ERR_UNREACHABLE 4   /* assert_eq!(paths.len(), nodes.len().pow(2)) panics   mod.rs:219 */
 #define SRG_ERR_LATENCY_RANGE 5 /* latency.convert(Nano).unwrap() overflow (mod.rs:336), or a used
-                                   pair with no path below 2^62 ns on a graph whose worst-case path
-                                   sum reaches 2^62.  The u64 keys hold distances below 2^62 only (an
-                                   edge of >= 2^62 ns counts as absent), so such a pair may be
-                                   unreachable OR have a shortest path in [2^62, 2^64) that the
-                                   reference would return (e.g. one 2^63 ns edge) -- a documented
-                                   deviation; a graph whose used pairs all have paths below 2^62 ns
-                                   succeeds whatever its edge latencies */
+                                   pair with no path below 2^62 units on a graph whose worst-case
+                                   path sum reaches 2^62 units (unit = srg_stats.latency_unit_ns, the
+                                   gcd of the non-self-loop latencies).  The u64 keys hold distances
+                                   below 2^62 units only (an edge of >= 2^62 units counts as absent),
+                                   so such a pair may be unreachable OR have a shortest path in
+                                   [2^62, 2^64) ns that the reference would return (e.g. one edge of
+                                   2^63 + 1 ns) -- a documented deviation; a graph whose used pairs
+                                   all have paths below 2^62 units succeeds whatever its latencies */
 #define SRG_ERR_HIP 6           /* HIP runtime failure (no device, launch failure) */
 #define SRG_ERR_OOM 7           /* device allocation failed */
 #define SRG_ERR_PARSE 8         /* GML / attribute error from NetworkGraph::parse (mod.rs:134-181) */
@@ -100,6 +101,9 @@ typedef struct srg_stats {
     uint64_t min_latency_ns;    /* host entry: min latency over all n^2 outputs, diagonal included
                                    (RoutingInfo::get_smallest_latency_ns, mod.rs:474-476);
                                    UINT64_MAX when n = 0                                       */
+    uint64_t latency_unit_ns;   /* shortest paths: the gcd of the non-self-loop edge latencies; the
+                                   kernels count latency in these units (exact: every path sum is a
+                                   multiple), outputs are back in ns.  1 = nanosecond keys        */
 } srg_stats;
 
 #define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */

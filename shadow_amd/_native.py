@@ -132,6 +132,7 @@ class Stats(ctypes.Structure):
         ("ms_host_register", ctypes.c_double),
         ("d2h_overlapped_bytes", ctypes.c_uint64),
         ("min_latency_ns", ctypes.c_uint64),
+        ("latency_unit_ns", ctypes.c_uint64),
     ]
 
     def as_dict(self):

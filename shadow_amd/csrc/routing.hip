@@ -89,6 +89,7 @@ struct DevBuf {
 
 struct EdgeStats {
     unsigned long long max_lat;   // max latency over non-self-loop edges
+    unsigned long long unit;      // gcd of the non-self-loop latencies (0: none, or all zero)
     uint32_t bad_endpoint;        // an endpoint >= V
     uint32_t lat_overflow;        // a non-self-loop latency == UINT64_MAX (ns conversion overflow)
 };
@@ -123,11 +124,29 @@ __global__ void k_check_nodes(const uint32_t* __restrict__ nodes, uint32_t n, ui
     }
 }
 
+// binary gcd (gcd(0, b) = b)
+__device__ __forceinline__ unsigned long long gcd64(unsigned long long a, unsigned long long b) {
+    if (a == 0) return b;
+    if (b == 0) return a;
+    const int sh = __builtin_ctzll(a | b);
+    a >>= __builtin_ctzll(a);
+    do {
+        b >>= __builtin_ctzll(b);
+        if (a > b) {
+            const unsigned long long t = a;
+            a = b;
+            b = t;
+        }
+        b -= a;
+    } while (b);
+    return a << sh;
+}
+
 __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                             const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t V,
                             uint32_t* __restrict__ selfcnt, uint64_t* __restrict__ self_lat,
                             float* __restrict__ self_loss, EdgeStats* st) {
-    unsigned long long mx = 0;
+    unsigned long long mx = 0, un = 0;
     uint32_t bad = 0, ovf = 0;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
@@ -143,14 +162,27 @@ __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const 
         } else {
             mx = l > mx ? l : mx;
             ovf |= (l == UINT64_MAX);
+            if (un != 1) un = gcd64(un, l);  // the latency unit (compute_device: keys = latency / unit)
         }
     }
     // wave reduction then one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
         unsigned long long o = __shfl_down(mx, off, 64);
         mx = o > mx ? o : mx;
+        un = gcd64(un, __shfl_down(un, off, 64));
     }
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_lat, mx);
+    if ((threadIdx.x & 63) == 0 && un) {
+        // gcd has no atomic: compare-and-swap until the stored unit divides this wave's
+        unsigned long long cur = st->unit;
+        for (;;) {
+            const unsigned long long nu = gcd64(cur, un);
+            if (nu == cur) break;
+            const unsigned long long prev = atomicCAS(&st->unit, cur, nu);
+            if (prev == cur) break;
+            cur = prev;
+        }
+    }
     if (bad) atomicOr(&st->bad_endpoint, 1u);
     if (ovf) atomicOr(&st->lat_overflow, 1u);
 }
@@ -170,19 +202,22 @@ __global__ void k_fill(K* __restrict__ p, size_t count, K v) {
         p[i] = v;
 }
 
+// latency -> key: latency / unit, where the unit (the gcd of all non-self-loop latencies) divides
+// every path sum, so keys compare and add exactly as the latencies do; outputs are key * unit
 template <class K>
-__device__ __forceinline__ K to_key(uint64_t l) {
+__device__ __forceinline__ K to_key(uint64_t l, uint64_t unit) {
+    if (unit != 1) l /= unit;
     if constexpr (sizeof(K) == 4) return l >= KeyOps<K>::INF ? KeyOps<K>::INF : (uint32_t)l;
     else return (K)l;
 }
 
 template <class K>
 __global__ void k_w_lat(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                        const uint64_t* __restrict__ lat, int directed, K* __restrict__ W, size_t ld) {
+                        const uint64_t* __restrict__ lat, uint64_t unit, int directed, K* __restrict__ W, size_t ld) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
         if (s == t) continue;  // self-loops never shorten a path; kept for the diagonal only
-        const K l = to_key<K>(lat[e]);
+        const K l = to_key<K>(lat[e], unit);
         atomicMin(&W[(size_t)s * ld + t], l);
         if (!directed) atomicMin(&W[(size_t)t * ld + s], l);
     }
@@ -190,12 +225,12 @@ __global__ void k_w_lat(uint64_t E, const uint32_t* __restrict__ src, const uint
 
 template <class K>
 __global__ void k_w_loss(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                         const uint64_t* __restrict__ lat, const float* __restrict__ loss, int directed,
+                         const uint64_t* __restrict__ lat, uint64_t unit, const float* __restrict__ loss, int directed,
                          const K* __restrict__ W, uint32_t* __restrict__ WL, size_t ld) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
         if (s == t) continue;
-        const K l = to_key<K>(lat[e]);
+        const K l = to_key<K>(lat[e], unit);
         // -0.0 compares equal to 0.0 (partial_cmp) and folds identically: normalise it
         const uint32_t bits = __float_as_uint(loss[e] + 0.0f);
         if (W[(size_t)s * ld + t] == l) atomicMin(&WL[(size_t)s * ld + t], bits);
@@ -207,13 +242,14 @@ __global__ void k_w_loss(uint64_t E, const uint32_t* __restrict__ src, const uin
 //   KW[s][t] = min over parallel edges of (latency << 32 | loss bits)    (mod.rs:305-313)
 // (loss in [0,1] is non-negative, so its f32 bit order is its numeric order).
 __global__ void k_w_key(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                        const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                        const uint64_t* __restrict__ lat, uint64_t unit, const float* __restrict__ loss,
                         unsigned long long* __restrict__ KW, size_t ld) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
         if (s == t) continue;  // self-loops never shorten a path; kept for the diagonal only
         // null loss: latency only (WL is then built by k_w_loss once the losses have arrived)
-        const unsigned long long k = ((unsigned long long)lat[e] << 32) | (loss ? __float_as_uint(loss[e] + 0.0f) : 0u);
+        const uint64_t l = unit != 1 ? lat[e] / unit : lat[e];  // < 2^32-1: the u32 path's precondition
+        const unsigned long long k = ((unsigned long long)l << 32) | (loss ? __float_as_uint(loss[e] + 0.0f) : 0u);
         atomicMin(&KW[(size_t)s * ld + t], k);
     }
 }
@@ -355,7 +391,7 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
                                                  const uint32_t* __restrict__ rowpos,
                                                  const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
                                                  uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags,
-                                                 int mode) {
+                                                 int mode, uint64_t unit) {
     // mode bit 0: latency (+ unreachable check), bit 1: loss from L; one workgroup per local row a,
     // U columns per thread in flight (the gathers are latency-bound)
     const uint32_t a = blockIdx.x;
@@ -391,7 +427,7 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
             } else {
                 if (mode & 1) {
                     unreach |= d[u] == KeyOps<K>::INF;
-                    ol[b] = (uint64_t)d[u];
+                    ol[b] = (uint64_t)d[u] * unit;
                 }
                 if (mode & 2) os[b] = l[u];
             }
@@ -725,8 +761,10 @@ struct Prelude {
     float* selfloss;
     Flags* flags;
     std::vector<uint32_t> nodes_h;  // host copy of `nodes` (partitioning, error text)
-    bool range_risk = false;         // max_lat * (V-1) >= 2^62: an INF used pair on the u64 keys may be a
-                                     // path >= 2^62 ns (SRG_ERR_LATENCY_RANGE), not an unreachable one
+    bool range_risk = false;         // max_key * (V-1) >= 2^62: an INF used pair on the u64 keys may be a
+                                     // path >= 2^62 units (SRG_ERR_LATENCY_RANGE), not an unreachable one
+    uint64_t unit = 1;               // latency unit in ns: keys = latency / unit (compute_device)
+    unsigned long long max_key = 0;  // max_lat / unit
 };
 
 Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, hipStream_t st,
@@ -1370,7 +1408,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
         HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, st));
         wl_late = g.late && !g.late->applied;
-        if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, wl_late ? nullptr : g.loss, KW, Vp);
+        if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, P.unit, wl_late ? nullptr : g.loss, KW, Vp);
         const unsigned nb64 = (unsigned)(Vp / 64);
         k_w_split<false><<<dim3(nb64, nb64), 256, 0, st>>>(KW, Vp, g.directed, (uint32_t*)W, WL, (uint32_t*)D);
     } else {
@@ -1378,8 +1416,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         k_fill<K><<<grid_for(VV), kThreads, 0, st>>>(W, VV, KeyOps<K>::INF);
         HIP_CHECK(hipMemsetAsync(WL, 0xFF, VV * 4, st));
         if (g.E) {
-            k_w_lat<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.directed, W, Vp);
-            k_w_loss<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, g.loss, g.directed, W, WL,
+            k_w_lat<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, P.unit, g.directed, W, Vp);
+            k_w_loss<K><<<grid_for(g.E), kThreads, 0, st>>>(g.E, g.src, g.dst, g.lat, P.unit, g.loss, g.directed, W, WL,
                                                              Vp);
         }
         k_init_d<K><<<grid_for(VV), kThreads, 0, st>>>(W, D, Vp);
@@ -1431,7 +1469,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         if constexpr (sizeof(K) == 4) {
             unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
             HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, ax));
-            if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, ax>>>(g.E, g.src, g.dst, g.lat, g.loss, KW, Vp);
+            if (g.E) k_w_key<<<grid_for(g.E), kThreads, 0, ax>>>(g.E, g.src, g.dst, g.lat, P.unit, g.loss, KW, Vp);
             const unsigned nb64 = (unsigned)(Vp / 64);
             k_w_split<true><<<dim3(nb64, nb64), 256, 0, ax>>>(KW, Vp, g.directed, nullptr, WL, nullptr);
             HIP_CHECK(hipGetLastError());
@@ -1496,7 +1534,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     if (sizeof(K) == 4 && inf_any) {
         // a used pair at INF: unreachable -- unless some path could reach 2^31-1 ns, in which case
         // the u64 keys decide (the u32 FW work is redone)
-        const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (V > 1 ? V - 1 : 1);
+        const unsigned __int128 bound = (unsigned __int128)P.max_key * (V > 1 ? V - 1 : 1);
         if (bound >= KeyOps<uint32_t>::INF) {
             if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));  // the u64 rerun rewrites WL
             return false;
@@ -1511,11 +1549,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     if (nloc)
         k_extract<K><<<nloc, kThreads, 0, st>>>(D, nullptr, Vp, lnodes, nloc, nodes, n, lpos,
                                                                       P.selflat, P.selfloss, out_lat, out_loss,
-                                                                      P.flags, 1);
+                                                                      P.flags, 1, P.unit);
     HIP_CHECK(hipGetLastError());
     if (reduce_flag(&P.flags->unreachable_used_pair)) {
         if (sizeof(K) == 8 && P.range_risk)
-            fail(SRG_ERR_LATENCY_RANGE, "a used pair has no path below 2^62 ns (max edge latency " +
+            fail(SRG_ERR_LATENCY_RANGE, "a used pair has no path below 2^62 latency units (max edge latency " +
                                             std::to_string(P.es.max_lat) +
                                             " ns): unreachable, or a latency sum the reference's u64 would wrap");
         fail(SRG_ERR_UNREACHABLE,
@@ -1756,7 +1794,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     if (nloc && !loss_written)
         k_extract<K><<<nloc, kThreads, 0, st>>>(D, Lfin, Vp, lnodes, nloc, nodes, n, lpos,
                                                                       P.selflat, P.selfloss, out_lat, out_loss,
-                                                                      P.flags, 2);
+                                                                      P.flags, 2, P.unit);
     HIP_CHECK(hipGetLastError());
     const double ms_extract = tm.lap();
 
@@ -1823,8 +1861,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     float* in_b = (float*)c.b_entb.get(std::max<size_t>(arcs, 1) * 4);
     HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
     if (g.E)
-        k_csr_fill<<<grid_for(g.E), kThreads, 0, st>>>(g.E, esrc, edst, g.lat, g.loss, g.directed, off, cur, in_src,
-                                                       in_w, in_b);
+        k_csr_fill<<<grid_for(g.E), kThreads, 0, st>>>(g.E, esrc, edst, g.lat, P.unit, g.loss, g.directed, off, cur,
+                                                       in_src, in_w, in_b);
     // out-arcs for the work marks: the in-CSR itself when undirected
     const uint32_t* out_off = off;
     const uint32_t* out_dst = in_src;
@@ -1929,10 +1967,10 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         }
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
-                     selflat, selfloss, out_lat, out_loss, fl, 0xFFFFFFFFu, 0u, gb};
+                     selflat, selfloss, out_lat, out_loss, fl, P.unit, 0xFFFFFFFFu, 0u, gb};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
-            a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.es.max_lat / (unsigned long long)c.sparse_delta_div);
+            a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
         a.all_lanes = c.sparse_delta_all ? 1u : 0u;
         if (c.profiling) {
             while (c.prof_events.size() < 2) {
@@ -2020,14 +2058,21 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     // u64 keys hold path sums below INF = 2^62 (a sum of two keys never wraps); a graph whose
     // worst-case path could reach 2^62 still runs, and only a used pair left at INF is an error:
     // SRG_ERR_LATENCY_RANGE then, since it may be a path the reference would wrap (mod.rs:327)
-    const unsigned __int128 bound = (unsigned __int128)P.es.max_lat * (g.V > 1 ? g.V - 1 : 1);
+    // latency unit: every non-self-loop latency is a multiple of their gcd, hence so is every path
+    // sum; keys count units (a ms-granular graph fits u32 keys up to 2^31-1 ms of path), outputs
+    // are key * unit -- exact.  SRG_LATENCY_UNIT=1 keeps nanosecond keys (tests, A/B).
+    const char* lu = std::getenv("SRG_LATENCY_UNIT");
+    P.unit = (P.es.unit > 1 && !(lu && std::strcmp(lu, "1") == 0)) ? P.es.unit : 1;
+    P.max_key = P.es.max_lat / P.unit;
+    if (stats) stats->latency_unit_ns = P.unit;
+    const unsigned __int128 bound = (unsigned __int128)P.max_key * (g.V > 1 ? g.V - 1 : 1);
     P.range_risk = bound >= ((unsigned __int128)1 << 62);
     const int G = c.comm ? c.comm->nranks : 1, rk = c.comm ? c.comm->rank : 0;
-    if (choose_sparse(c, g) && P.es.max_lat < 0xFFFFFFFFull) {
+    if (choose_sparse(c, g) && P.max_key < 0xFFFFFFFFull) {
         loss_arrive(g, P.selfloss, st);
         if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
     }
-    if (P.es.max_lat < 0xFFFFFFFFull) {
+    if (P.max_key < 0xFFFFFFFFull) {
         // FW tile: 128 (more work per launch) on one GPU; the multi-rank schedule is bound by
         // the per-pivot chain (close pivot -> panels), whose latency scales with T^3
         const int tile = c.fw_tile ? c.fw_tile : 128;
@@ -3009,7 +3054,7 @@ int srg_multi_compute_shortest_paths(srg_multi* m, const srg_edge_list* graph, c
         srg_ctx* c = m->ranks[r];
         c->gather_output = false;
         if (big)
-            c->ext_reg = [&reg, c](void** views, double* ms) {
+            c->ext_reg = [&reg](void** views, double* ms) {
                 if (!reg.wait()) return false;
                 for (int i = 0; i < 2; ++i)
                     if (hipHostGetDevicePointer(&views[i], reg.p[i], 0) != hipSuccess) views[i] = nullptr;

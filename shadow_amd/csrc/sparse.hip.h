@@ -80,13 +80,13 @@ __global__ void k_csr_fill_out(uint64_t E, const uint32_t* __restrict__ src, con
 }
 
 __global__ void k_csr_fill(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                           const uint64_t* __restrict__ lat, const float* __restrict__ loss, int directed,
+                           const uint64_t* __restrict__ lat, uint64_t unit, const float* __restrict__ loss, int directed,
                            const uint32_t* __restrict__ off, uint32_t* __restrict__ cur, uint32_t* __restrict__ in_src,
                            uint32_t* __restrict__ in_w, float* __restrict__ in_b) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
         if (s == t) continue;
-        const uint32_t w = lat_key32(lat[e]);
+        const uint32_t w = lat_key32(unit != 1 ? lat[e] / unit : lat[e]);  // latency units (compute_device)
         const float b = __fsub_rn(1.0f, loss[e] + 0.0f);
         uint32_t k = off[t] + atomicAdd(&cur[t], 1u);
         in_src[k] = s;
@@ -123,7 +123,8 @@ struct SparseArgs {
     float* out_loss;
     uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2..3] total evaluations,
                                  // [5] some relaxation saturated the u32 latency key (a path >= 2^32-1 ns)
-    uint32_t delta;              // bucket width in ns (0xFFFFFFFF = one bucket: plain Bellman-Ford)
+    uint64_t unit;               // latency unit in ns (outputs = key * unit)
+    uint32_t delta;              // bucket width in latency units (0xFFFFFFFF = one bucket: plain Bellman-Ford)
     uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
 };
@@ -470,7 +471,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                 } else {
                     const uint32_t lat = (uint32_t)(l >> 32);
                     bad |= lat == 0xFFFFFFFFu;
-                    ol = lat;
+                    ol = (uint64_t)lat * a.unit;
                     os = __uint_as_float((uint32_t)l);
                 }
                 a.out_lat[(size_t)row * a.ncols + j] = ol;

@@ -230,20 +230,29 @@ def test_unused_isolated_vertex_keeps_u32(router):
         router.compute_shortest_paths(iso2, list(range(101)))
 
 
-def test_latency_range_is_an_error(router):
-    """Documented divergence: when a used pair has no path below 2^62 ns on a
-    graph whose worst-case path sum reaches 2^62, the library returns SRG_ERR_LATENCY_RANGE, where
-    the release build of the reference would wrap u64
+def test_latency_range_is_an_error(router, monkeypatch):
+    """Documented divergence: when a used pair has no path below 2^62 latency
+    units on a graph whose worst-case path sum reaches 2^62 units, the library returns
+    SRG_ERR_LATENCY_RANGE, where the release build of the reference would wrap u64
     silently (mod.rs:327 `+` on u64, overflow checks off in src/Cargo.toml:56-61).  The Rust
-    binding panics on it, like the `.unwrap()` of an overflowing unit conversion (mod.rs:336)."""
+    binding panics on it, like the `.unwrap()` of an overflowing unit conversion (mod.rs:336).
+    With nanosecond keys (SRG_LATENCY_UNIT=1) a 2^61-ns pair of links is such a graph; with the
+    latency unit (their gcd, 2^61) the same graph is 2 units of path and matches the reference."""
     big = 2 ** 61
     e = Edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [1, 1, 1, big, big], [0.0] * 5, False)
+    t = router.compute_shortest_paths(e, [0, 1, 2])
+    assert t[(0, 2)].latency_ns == 2 ** 62 and t.stats["latency_unit_ns"] == big
+    assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), [0, 1, 2])
+    assert_parity(t, lat, loss)
+    monkeypatch.setenv("SRG_LATENCY_UNIT", "1")
     with pytest.raises(NetGraphError) as ei:
         router.compute_shortest_paths(e, [0, 1, 2])
     assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
     ok = Edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [1, 1, 1, 2 ** 40, 2 ** 40], [0.0] * 5, False)
     t = router.compute_shortest_paths(ok, [0, 1, 2])
     assert t[(0, 2)].latency_ns == 2 ** 41 and t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+    assert t.stats["latency_unit_ns"] == 1
     # worst case max_lat * (V-1) >= 2^62, but no used shortest path comes near it (a "disabled"
     # 2^61-ns link beside a 2-hop route): the reference's Dijkstra succeeds, and so does this
     dis = Edges(3, [0, 1, 2, 0, 1, 0], [0, 1, 2, 1, 2, 2], [1, 1, 1, 1, 1, big], [0.0] * 6, False)
@@ -253,11 +262,21 @@ def test_latency_range_is_an_error(router):
     assert_parity(t, lat, loss)
 
 
-def test_u64_edge_past_key_range_is_an_error(router):
+def test_u64_edge_past_key_range_is_an_error(router, monkeypatch):
     """Documented deviation (include/shadow_routing.h SRG_ERR_LATENCY_RANGE): u64 keys hold
-    distances below 2^62, so an edge of 2^63 ns counts as absent and the used pair it alone
-    connects fails with SRG_ERR_LATENCY_RANGE, where the reference's u64 Dijkstra returns 2^63."""
+    distances below 2^62 units, so with nanosecond keys an edge of 2^63 ns + 1 counts as absent and
+    the used pair it alone connects fails with SRG_ERR_LATENCY_RANGE, where the reference's u64
+    Dijkstra returns it.  An edge of exactly 2^63 ns is one latency unit of 2^63 ns (the gcd of
+    the non-self-loop latencies) and comes out as the reference's 2^63."""
     e = Edges(2, [0, 1, 0], [0, 1, 1], np.array([1000, 1000, 2 ** 63], dtype=np.uint64), [0.0, 0.0, 0.0], directed=False)
+    t = router.compute_shortest_paths(e, [0, 1])
+    assert t[(0, 1)].latency_ns == 2 ** 63 and t.stats["latency_unit_ns"] == 2 ** 63
+    odd = Edges(2, [0, 1, 0, 0], [0, 1, 1, 1], np.array([1000, 1000, 2 ** 63 + 1, 2 ** 63 + 2], dtype=np.uint64),
+                [0.0] * 4, directed=False)
+    with pytest.raises(NetGraphError) as ei:
+        router.compute_shortest_paths(odd, [0, 1])
+    assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
+    monkeypatch.setenv("SRG_LATENCY_UNIT", "1")
     with pytest.raises(NetGraphError) as ei:
         router.compute_shortest_paths(e, [0, 1])
     assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
@@ -379,10 +398,12 @@ def test_host_entry_early_rows_match_device(router, mode, groups):
 
 
 @pytest.mark.parametrize("shift,offset", [(32, 0), (32, 1), (40, 7), (0, 2 ** 33)])
-def test_u64_low_word_scan(router, shift, offset):
+def test_u64_low_word_scan(router, shift, offset, monkeypatch):
     """u64 keys: the pair-lane scan on the keys' low 32 bits equals the oracle.  Latencies that are multiples of 2^32 make every candidate
     match in the low words (false matches everywhere: the loss pass's exact multi-predecessor
-    check must resolve them); with offsets the low words are informative again."""
+    check must resolve them); with offsets the low words are informative again.  Nanosecond
+    keys (SRG_LATENCY_UNIT=1): with the latency unit, the offset-free cases would be u32 keys."""
+    monkeypatch.setenv("SRG_LATENCY_UNIT", "1")
     g = synth.random_graph(300, 0.08, 5 + shift, lat_lo=1, lat_hi=6, parallel=0.1)
     lat = g.latency_ns.astype(np.uint64) * np.uint64(2 ** shift) + np.uint64(offset)
     e = Edges(g.num_vertices, g.src, g.dst, lat, g.packet_loss, directed=False)
@@ -397,6 +418,41 @@ def test_u64_low_word_scan(router, shift, offset):
     t = router.compute_shortest_paths(e, nodes)
     assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
     assert_parity(t, ref_lat, ref_loss)
+
+
+@pytest.mark.parametrize("algo", ["dense", "sparse"])
+def test_latency_unit_keys(router, algo, monkeypatch):
+    """Latency unit (routing.hip compute_device): keys count units of the gcd of the non-self-loop
+    latencies.  Millisecond-granular latencies whose paths pass 2^31 ns keep u32 keys (dense FW
+    or the sparse Bellman-Ford) and give the bytes of nanosecond keys (u64 FW), and the oracle's."""
+    if algo == "dense":
+        g = synth.atlas_like(700, seed=61)
+    else:
+        g = synth.random_graph(2100, 0.004, 62, lat_lo=1, lat_hi=200, parallel=0.1)
+    lat = g.latency_ns.astype(np.uint64)
+    if algo == "dense":  # multiples of 3 ms
+        lat = np.maximum(lat // np.uint64(1000), np.uint64(1)) * np.uint64(3_000_000)
+    else:  # multiples of 30 ms
+        lat = lat * np.uint64(30_000_000)
+    e = Edges(g.num_vertices, g.src, g.dst, lat, g.packet_loss, directed=False)
+    nodes = list(range(0, g.num_vertices, 2)) if algo == "sparse" else list(range(g.num_vertices))
+    if algo == "sparse":
+        router.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_SPARSE)
+    try:
+        t = router.compute_shortest_paths(e, nodes)
+        monkeypatch.setenv("SRG_LATENCY_UNIT", "1")
+        t1 = router.compute_shortest_paths(e, nodes)
+    finally:
+        router.set_option(N.SRG_OPT_ALGORITHM, N.SRG_ALGO_AUTO)
+    assert int(t.latency_ns.max()) >= 2 ** 31  # past the nanosecond u32 keys
+    unit = t.stats["latency_unit_ns"]
+    assert unit % 3_000_000 == 0 and t1.stats["latency_unit_ns"] == 1
+    want = N.SRG_PATH_SPARSE_U32 if algo == "sparse" else N.SRG_PATH_DENSE_U32
+    assert t.stats["path_kind"] == want and t1.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+    assert np.array_equal(t.latency_ns, t1.latency_ns) and bits_equal(t.packet_loss, t1.packet_loss)
+    rows = [0, 1, len(nodes) - 1]
+    rl, rs = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
+    assert np.array_equal(t.latency_ns[rows], rl) and bits_equal(t.packet_loss[rows], rs)
 
 
 def test_h2d_codec_matches_plain(router):

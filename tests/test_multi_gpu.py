@@ -53,6 +53,7 @@ CASES = [
     dict(G=8, V=900, dens=0.01, seed=4, nodes="all"),
     dict(G=4, V=260, dens=0.2, seed=5, nodes="all", lat_lo=2**31, lat_hi=2**33),  # u64 keys
     dict(G=2, V=130, dens=0.3, seed=6, nodes="scrambled", threshold=0.0),        # dense scan
+    dict(G=4, V=260, dens=0.2, seed=7, nodes="all", lat_lo=2**31, lat_hi=2**33, ms=True),  # latency unit
 ]
 
 
@@ -69,6 +70,8 @@ def node_list(kind, V, seed):
 def test_ranks_match_single_gpu(c):
     kw = {k: c[k] for k in ("lat_lo", "lat_hi") if k in c}
     e = synth.random_graph(c["V"], c["dens"], c["seed"], **kw)
+    if c.get("ms"):  # millisecond multiples: u32 keys in units of the latencies' gcd on every rank
+        e.latency_ns = e.latency_ns // np.uint64(10**6) * np.uint64(10**6)
     nodes = node_list(c["nodes"], c["V"], c["seed"])
     ref_router = Router(0)
     if c.get("threshold") is not None:
@@ -81,6 +84,8 @@ def test_ranks_match_single_gpu(c):
     assert errs == [None] * c["G"], errs
     for r, t in enumerate(out):
         assert t.stats["nranks"] == c["G"] and t.stats["rank"] == r
+        assert t.stats["path_kind"] == ref.stats["path_kind"]
+        assert t.stats["latency_unit_ns"] == ref.stats["latency_unit_ns"]
         assert np.array_equal(t.latency_ns, lat), f"rank {r} latency"
         assert bits_equal(t.packet_loss, loss), f"rank {r} loss"
     assert sum(t.stats["local_sources"] for t in out) == len(nodes)
