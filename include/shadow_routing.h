@@ -172,8 +172,9 @@ void srg_destroy(srg_ctx* ctx);
                                      * and latencies, on their own stream beside the W build and FW (which
                                      * need no loss); 0 = with them */
 #define SRG_OPT_FW_LINE_SPLIT 31     /* symmetric FW: sub-tiles per dimension of the critical chain's line
-                                     * launches, 1 (whole 128-tiles) / 2 / 4; 0 (default) = 1 on one rank,
-                                     * 2 on two, 4 on more */
+                                     * launches, 1 (whole 128-tiles) / 2 / 4; 0 (default) = by the bulk a
+                                     * pivot leaves this rank: >= 2048 tiles 1, >= 1024 tiles 2, else 4
+                                     * (C3: 1 on one rank, 2 on two, 4 on more; C1/C2: 4) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

@@ -1229,15 +1229,17 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     }
     const size_t lds_bulk = lb_lds_bytes<T, KCS>();
     set_lds(fw_bulk_lb<T, KCS>, lds_bulk);
-    // The chain's line launches.  One rank: the chain runs beside a bulk of ~nb^2/2 tiles, so the
-    // lines take whole tiles (the fewest CU slots taken from the bulk).  Several ranks: the bulk
-    // shrinks with G and the chain is the critical path: sub-tiles, S^2 x the workgroups at a
-    // fraction of the latency (SRG_OPT_FW_LINE_SPLIT; measured FW at sim 2:0 / 4:0 / 8:0 with whole
-    // tiles, quadrants, 32 x 32: 17.9 / 15.1 / 15.6, 14.9 / 12.2 / 12.1, 11.0 / 7.7 / 7.2 ms,
-    // profiles/r03c/, r03k/).  The pivot closure is one launch of 64
-    // workgroups either way (fw_close_sq; eight squaring launches took 45-117 us per pivot, the
-    // one-workgroup FW closure 159 us beside the bulk: profiles/r03b/).
-    const int split = c.fw_line_split ? c.fw_line_split : !multi ? 1 : G < 4 ? 2 : 4;
+    // The chain's line launches.  A large bulk (C3 on one rank: ~nb^2/2 = 3 160 tiles, four rounds
+    // of the chip's 768 slots) hides the chain, so the lines take whole tiles (the fewest CU slots
+    // taken from the bulk).  A bulk below ~2 rounds (several ranks, or a small graph) leaves the
+    // chain as the critical path: sub-tiles, S^2 x the workgroups at a fraction of the latency
+    // (SRG_OPT_FW_LINE_SPLIT; FW at sim 2:0 / 4:0 / 8:0 with whole tiles, quadrants, 32 x 32:
+    // 17.9 / 15.1 / 15.6, 14.9 / 12.2 / 12.1, 11.0 / 7.7 / 7.2 ms, profiles/r03c/, r03k/; one rank,
+    // C2 (nb = 32) 3.6 / 2.8 / 2.6 ms, C1 (nb = 8) 0.79 / 0.48 / 0.47 ms, profiles/r03x/).  The
+    // pivot closure is one launch of 64 workgroups either way (fw_close_sq; eight squaring launches
+    // took 45-117 us per pivot, the one-workgroup FW closure 159 us beside the bulk: r03b/).
+    const int bulk_tiles = nb * (nb + 1) / 2 / G;
+    const int split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
     set_lds(fw_line_lb<T, 1>, lb_lds_bytes<T, line_kc<1>()>());
     set_lds(fw_line_lb<T, 2>, lb_lds_bytes<T / 2, line_kc<2>()>());
     set_lds(fw_line_lb<T, 4>, lb_lds_bytes<T / 4, line_kc<4>()>());
