@@ -299,7 +299,9 @@ def roofline_for(agg, kind, args, edges, V, wkey, sym):
     relax = agg["prof_relaxations"] / agg["prof_launches"]
     achieved = relax * OPS_PER_RELAX.get(kind, 2.0) / (avg_ms * 1e-3) / 1e12
     traffic, tsrc = load_traffic("fw_product", wkey)
-    if sym:
+    if sym and kind == 1:
+        kname = "fw_bulk_lb<u64,64,16> (FW phase 3 over the stored tiles I <= J, operands from the pivot's line buffer, u64 keys)"
+    elif sym:
         kname = "fw_bulk_lb<128,16> (FW phase 3 over the stored tiles I <= J, operands from the pivot's line buffer, pair-packed)"
     elif kind == 0:
         kname = ("fw_product<u32,128,16,2> (FW phase 3, pair-packed, non-lookahead tiles)" if args.fw_packed else
@@ -643,7 +645,7 @@ def main():
         dev_ms = (time.perf_counter() - t1) * 1e3 / 2
         del ol, os_
     wkey = workload_key(args, V, seed, world)
-    sym = (kind == 0 and args.fw_packed and args.fw_symmetric != 0 and not edges.directed)
+    sym = ((kind == 0 and args.fw_packed) or kind == 1) and args.fw_symmetric != 0 and not edges.directed
     roofline = roofline_for(agg, kind, args, edges, V, wkey, sym)
 
     if args.simulate_rank:

@@ -712,6 +712,139 @@ __device__ __forceinline__ void fw_core_lb(uint32_t* __restrict__ C, size_t ldc,
 template <int T, int KC>
 constexpr size_t lb_lds_bytes() { return (size_t)2 * KC * (T + 2) * sizeof(u64p); }
 
+// ---- u64 keys (K = uint64_t, 64-tiles): the same products with one key per element ----------
+// A staged operand chunk is X[k][x] (KC k-rows of TM keys, row stride TM + 2: 16-B aligned rows);
+// the row form reads 16 B = two k of one x, the column form 16 B = two x of one k.
+template <int TM, int KC>
+struct SymOp64 {
+    static constexpr int NV = TM * KC / 2 / 256;  // 16-B vectors per thread per operand
+    static_assert(TM * KC / 2 % 256 == 0, "sym64 staging");
+    Vec16<uint64_t> r[NV];
+};
+
+template <int TM, int KC>
+__device__ __forceinline__ void sym_load64(SymOp64<TM, KC>& o, const uint64_t* __restrict__ base, size_t ld,
+                                           bool colform, int k0) {
+#pragma unroll
+    for (int q = 0; q < SymOp64<TM, KC>::NV; ++q) {
+        const int v = (int)threadIdx.x + 256 * q;
+        if (!colform) {
+            const int x = v / (KC / 2), kq = v % (KC / 2);
+            o.r[q] = ld16(base + (size_t)x * ld + k0 + 2 * kq);
+        } else {
+            const int kk = v / (TM / 2), xq = v % (TM / 2);
+            o.r[q] = ld16(base + (size_t)(k0 + kk) * ld + 2 * xq);
+        }
+    }
+}
+
+template <int TM, int KC>
+__device__ __forceinline__ void sym_store64(const SymOp64<TM, KC>& o, uint64_t* __restrict__ X, bool colform) {
+    constexpr int LDX = TM + 2;
+#pragma unroll
+    for (int q = 0; q < SymOp64<TM, KC>::NV; ++q) {
+        const int v = (int)threadIdx.x + 256 * q;
+        if (!colform) {
+            const int x = v / (KC / 2), kq = v % (KC / 2);
+            X[(2 * kq) * LDX + x] = o.r[q].v[0];
+            X[(2 * kq + 1) * LDX + x] = o.r[q].v[1];
+        } else {
+            const int kk = v / (TM / 2), xq = v % (TM / 2);
+            stv<uint64_t, 2>(X + kk * LDX + 2 * xq, o.r[q]);
+        }
+    }
+}
+
+// fw_core_lb for u64 keys (INF = 2^62: no sum wraps).  Thread (ty, tx) holds rows ty*M + i (its A
+// reads are wave broadcasts: one 16-B read per two rows) and columns tx + 16 j (its B reads are 16
+// lanes x 8 B contiguous: conflict-free).  Per k: M x M relaxations of a 64-bit add, a 64-bit
+// compare and two selects (the u64 price of SURVEY §8d: 5 int32 ops).
+template <int TM, int TK, int KC>
+__device__ __forceinline__ void fw_core_lb64(uint64_t* __restrict__ C, size_t ldc, const uint64_t* __restrict__ Ab,
+                                             bool acol, const uint64_t* __restrict__ Bb, bool bcol, size_t ldab,
+                                             uint64_t* __restrict__ C2, size_t ldc2) {
+    using S = SymOp64<TM, KC>;
+    constexpr int M = TM / 16;
+    constexpr int LDX = TM + 2;
+    constexpr int BUF = 2 * KC * LDX;  // A and B chunks
+    constexpr int NCH = TK / KC;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    uint64_t* lds = reinterpret_cast<uint64_t*>(smem_raw);
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    S sa, sb;
+    sym_load64<TM, KC>(sa, Ab, ldab, acol, 0);
+    sym_load64<TM, KC>(sb, Bb, ldab, bcol, 0);
+    uint64_t c[M][M];
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j < M; ++j) c[i][j] = C[(size_t)(ty * M + i) * ldc + tx + 16 * j];
+    sym_store64<TM, KC>(sa, lds, acol);
+    sym_store64<TM, KC>(sb, lds + KC * LDX, bcol);
+    __syncthreads();
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const uint64_t* Ap = lds + (ch & 1) * BUF;
+        const uint64_t* Bp = Ap + KC * LDX;
+        if (ch + 1 < NCH) {  // issue early
+            sym_load64<TM, KC>(sa, Ab, ldab, acol, (ch + 1) * KC);
+            sym_load64<TM, KC>(sb, Bb, ldab, bcol, (ch + 1) * KC);
+        }
+#pragma unroll 2
+        for (int k = 0; k < KC; ++k) {  // (a full unroll hoists every k's LDS reads: spills)
+            uint64_t a[M], b[M];
+            if constexpr (M >= 2) {
+#pragma unroll
+                for (int g = 0; g < M / 2; ++g) {
+                    const VecN<uint64_t, 2> va = ldv<uint64_t, 2>(Ap + k * LDX + ty * M + 2 * g);
+                    a[2 * g] = va.v[0];
+                    a[2 * g + 1] = va.v[1];
+                }
+            } else {
+                a[0] = Ap[k * LDX + ty];
+            }
+#pragma unroll
+            for (int j = 0; j < M; ++j) b[j] = Bp[k * LDX + tx + 16 * j];
+#pragma unroll
+            for (int i = 0; i < M; ++i)
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    const uint64_t s = a[i] + b[j];
+                    c[i][j] = s < c[i][j] ? s : c[i][j];
+                }
+        }
+        if (ch + 1 < NCH) {  // write late into the other buffer
+            uint64_t* An = lds + ((ch + 1) & 1) * BUF;
+            sym_store64<TM, KC>(sa, An, acol);
+            sym_store64<TM, KC>(sb, An + KC * LDX, bcol);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            C[(size_t)(ty * M + i) * ldc + tx + 16 * j] = c[i][j];
+            if (C2) C2[(size_t)(ty * M + i) * ldc2 + tx + 16 * j] = c[i][j];
+        }
+}
+
+template <int T, int KC>
+constexpr size_t lb_lds_bytes64() { return (size_t)2 * 2 * KC * (T + 2) * sizeof(uint64_t); }
+
+// LDS of a line-buffer product of TM-tiles: pair-packed u32 or u64 keys
+template <class K, int TM, int KC>
+constexpr size_t lb_lds() { return sizeof(K) == 4 ? lb_lds_bytes<TM, KC>() : lb_lds_bytes64<TM, KC>(); }
+
+// one product of the line-buffer schedule, for either key type
+template <class K, int TM, int TK, int KC>
+__device__ __forceinline__ void fw_core(K* __restrict__ C, size_t ldc, const K* __restrict__ Ab, bool acol,
+                                        const K* __restrict__ Bb, bool bcol, size_t ldab, K* __restrict__ C2,
+                                        size_t ldc2) {
+    if constexpr (sizeof(K) == 4) fw_core_lb<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, C2, ldc2);
+    else fw_core_lb64<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, C2, ldc2);
+}
+
 // ---- distribution of the stored tiles over G ranks (routing.hip fw_line_sym) ----------------
 // Tile (I, J), I <= J, belongs to rank (I + J) mod G: every rank holds ~1/G of every row and of
 // every LINE (line L's tile j is (min(j,L), max(j,L)), owner (j + L) mod G), so both the bulk of a
@@ -741,14 +874,14 @@ struct LineMap {
 // Bulk of pivot L: this rank's stored tiles (triangle indices tiles[0 .. gridDim.x)) except
 // those in lines x0, x1 (the pivot's own line, final, and the next pivot's line, updated by the
 // chain).  C in D (row stride ld), operands from line L's buffer.
-template <int T, int KC>
-__global__ void __launch_bounds__(256, 3) fw_bulk_lb(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lb,
-                                                     int L, int x0, int x1, LineMap lm, const int* __restrict__ tiles) {
+template <class K, int T, int KC>
+__global__ void __launch_bounds__(256, 3) fw_bulk_lb(K* __restrict__ D, size_t ld, const K* __restrict__ lb, int L,
+                                                     int x0, int x1, LineMap lm, const int* __restrict__ tiles) {
     int I, J;
     tri_tile(lm.nb, tiles[blockIdx.x], I, J);
     if (I == x0 || I == x1 || J == x0 || J == x1) return;  // whole workgroup
     constexpr size_t TT = (size_t)T * T;
-    fw_core_lb<T, T, KC>(D + (size_t)I * T * ld + (size_t)J * T, ld, lb + lm.slot(I, L) * TT, I > L,
+    fw_core<K, T, T, KC>(D + (size_t)I * T * ld + (size_t)J * T, ld, lb + lm.slot(I, L) * TT, I > L,
                          lb + lm.slot(J, L) * TT, J >= L, T, nullptr, 0);
 }
 
@@ -766,10 +899,9 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(uint32_t* __restrict__ D, s
 template <int S>
 constexpr int line_kc() { return S == 1 ? 16 : S == 2 ? 32 : 64; }
 
-template <int T, int S>
-__global__ void __launch_bounds__(256, S == 1 ? 3 : 2) fw_line_lb(uint32_t* __restrict__ D, size_t ld,
-                                                                  const uint32_t* __restrict__ lbL, int L,
-                                                                  uint32_t* __restrict__ lbK, int K1, int mode,
+template <class K, int T, int S>
+__global__ void __launch_bounds__(256, S == 1 ? 3 : 2) fw_line_lb(K* __restrict__ D, size_t ld, const K* __restrict__ lbL,
+                                                                  int L, K* __restrict__ lbK, int K1, int mode,
                                                                   LineMap lm, int g, int prio) {
     constexpr int TM = T / S;
     constexpr int KCL = line_kc<S>();
@@ -778,14 +910,15 @@ __global__ void __launch_bounds__(256, S == 1 ? 3 : 2) fw_line_lb(uint32_t* __re
     const int q = (int)blockIdx.y, qi = q / S, qj = q % S;
     const int I = min(j, K1), J = max(j, K1);
     const bool own = lm.owner(j, K1) == g;
-    uint32_t* Dt = D + (size_t)I * T * ld + (size_t)J * T;
-    uint32_t* Lt = lbK + lm.slot(j, K1) * TT;
-    auto copy_sub = [&](const uint32_t* src, size_t lds_, uint32_t* dst, size_t ldd) {
+    K* Dt = D + (size_t)I * T * ld + (size_t)J * T;
+    K* Lt = lbK + lm.slot(j, K1) * TT;
+    auto copy_sub = [&](const K* src, size_t lds_, K* dst, size_t ldd) {
+        constexpr int VE = 16 / (int)sizeof(K);
         src += (size_t)qi * TM * lds_ + qj * TM;
         dst += (size_t)qi * TM * ldd + qj * TM;
-        for (int e = threadIdx.x; e < TM * TM / 4; e += 256) {
-            const int r = e / (TM / 4), c4 = e % (TM / 4);
-            st16(dst + (size_t)r * ldd + c4 * 4, ld16(src + (size_t)r * lds_ + c4 * 4));
+        for (int e = threadIdx.x; e < TM * TM / VE; e += 256) {
+            const int r = e / (TM / VE), cv = e % (TM / VE);
+            st16(dst + (size_t)r * ldd + cv * VE, ld16(src + (size_t)r * lds_ + cv * VE));
         }
     };
     if (mode == 1 && j == K1) {  // the closed pivot tile itself: back to D on its owner
@@ -797,16 +930,16 @@ __global__ void __launch_bounds__(256, S == 1 ? 3 : 2) fw_line_lb(uint32_t* __re
         return;
     }
     if (prio) __builtin_amdgcn_s_setprio(3);  // the chain runs beside the bulk tiles (see fw_phase1)
-    const uint32_t* lb = mode == 0 ? lbL : lbK;
+    const K* lb = mode == 0 ? lbL : lbK;
     const int P = mode == 0 ? L : K1;
     const bool acol = I > P, bcol = J >= P;
     // A rows qi: row form advances rows, col form advances columns (and B likewise for columns qj)
-    const uint32_t* Ab = lb + lm.slot(I, P) * TT + (acol ? (size_t)qi * TM : (size_t)qi * TM * T);
-    const uint32_t* Bb = lb + lm.slot(J, P) * TT + (bcol ? (size_t)qj * TM : (size_t)qj * TM * T);
+    const K* Ab = lb + lm.slot(I, P) * TT + (acol ? (size_t)qi * TM : (size_t)qi * TM * T);
+    const K* Bb = lb + lm.slot(J, P) * TT + (bcol ? (size_t)qj * TM : (size_t)qj * TM * T);
     Dt += (size_t)qi * TM * ld + qj * TM;
     Lt += (size_t)qi * TM * T + qj * TM;
-    if (mode == 0) fw_core_lb<TM, T, KCL>(Dt, ld, Ab, acol, Bb, bcol, T, Lt, T);
-    else fw_core_lb<TM, T, KCL>(Lt, T, Ab, acol, Bb, bcol, T, own ? Dt : nullptr, ld);
+    if (mode == 0) fw_core<K, TM, T, KCL>(Dt, ld, Ab, acol, Bb, bcol, T, Lt, T);
+    else fw_core<K, TM, T, KCL>(Lt, T, Ab, acol, Bb, bcol, T, own ? Dt : nullptr, ld);
 }
 
 // Grid barrier among the launch's workgroups, which must all be resident together (a few small
@@ -837,8 +970,9 @@ __device__ __forceinline__ bool grid_sync(uint32_t* cnt, uint32_t target, uint32
     return *s_ok != 0;
 }
 
-__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+template <class K>
+__device__ __forceinline__ void st_wt(K* p, K v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // a vector store, sc1
 }
 
 // Close the T x T pivot tile P (row stride T, inside a line buffer) in ONE launch: repeated
@@ -850,21 +984,24 @@ __device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
 // P = min(P, P (x) P) holds there: P is closed.  Eight steps (paths of 2^8 >= T hops) always
 // suffice.  sync = {arrival counter, changed flag of steps 0 .. 7, ...} (16 words, zeroed before
 // the launch).  Keys <= INF = 2^31 - 1: no sum wraps.  P is read and written write-through
-// (grid_sync); the previous kernel's plain stores are visible at the launch boundary.
-template <int T>
-__global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uint32_t* __restrict__ sync,
+// (grid_sync); the previous kernel's plain stores are visible at the launch boundary.  K = u64:
+// keys <= INF = 2^62, the same.
+template <class K, int T>
+__global__ void __launch_bounds__(256) fw_close_sq(K* __restrict__ P, uint32_t* __restrict__ sync,
                                                    uint32_t* __restrict__ timeout, int prio) {
     if (prio) __builtin_amdgcn_s_setprio(3);
-    __shared__ uint32_t A[16][T + 1];
-    __shared__ uint32_t B[T][17];
+    __shared__ K A[16][T + 1];
+    __shared__ K B[T][17];
     __shared__ uint32_t s_chg, s_ok, s_more;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;
     const uint32_t nwg = gridDim.x * gridDim.y;
     // write-through (sc1, aux = 16) 16-B loads of the 16 rows and 16 columns this workgroup needs
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)(T * T * 4), 0x00027000);
-    constexpr int NV = 16 * T / 4 / 256;  // 16-B vectors per thread per operand
-    static_assert(NV >= 1 && 16 * T / 4 % 256 == 0, "closure staging");
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)(T * T * sizeof(K)), 0x00027000);
+    constexpr int VE = 16 / (int)sizeof(K);  // keys per 16-B vector
+    constexpr int NV = 16 * T / VE / 256;    // 16-B vectors per thread per operand
+    static_assert(NV >= 1 && 16 * T / VE % 256 == 0, "closure staging");
     for (int step = 0; step < 8; ++step) {
         if (threadIdx.x == 0) s_chg = 0;
         typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -872,26 +1009,29 @@ __global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uin
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int v = threadIdx.x + 256 * q;
-            const int y = v / (T / 4), k4 = v % (T / 4);    // A: row r0 + y, columns 4 k4 ..
-            const int kk = v / 4, x4 = v % 4;               // B: row kk, columns c0 + 4 x4 ..
-            va[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r0 + y) * T + 4 * k4) * 4, 0, 16);
-            vb[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (kk * T + c0 + 4 * x4) * 4, 0, 16);
+            const int y = v / (T / VE), ka = v % (T / VE);    // A: row r0 + y, columns VE ka ..
+            const int kk = v / (16 / VE), xb = v % (16 / VE);  // B: row kk, columns c0 + VE xb ..
+            va[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((r0 + y) * T + VE * ka) * sizeof(K)), 0, 16);
+            vb[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((kk * T + c0 + VE * xb) * sizeof(K)), 0, 16);
         }
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             const int v = threadIdx.x + 256 * q;
-            const int y = v / (T / 4), k4 = v % (T / 4), kk = v / 4, x4 = v % 4;
+            const int y = v / (T / VE), ka = v % (T / VE), kk = v / (16 / VE), xb = v % (16 / VE);
+            K ea[VE], eb[VE];
+            __builtin_memcpy(ea, &va[q], 16);
+            __builtin_memcpy(eb, &vb[q], 16);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                A[y][4 * k4 + e] = va[q][e];
-                B[kk][4 * x4 + e] = vb[q][e];
+            for (int e = 0; e < VE; ++e) {
+                A[y][VE * ka + e] = ea[e];
+                B[kk][VE * xb + e] = eb[e];
             }
         }
         __syncthreads();
-        const uint32_t old = A[ty][c0 + tx];
-        uint32_t v = old;
+        const K old = A[ty][c0 + tx];
+        K v = old;
 #pragma unroll 8
-        for (int k = 0; k < T; k += 2) v = KeyOps<uint32_t>::min3(v, A[ty][k] + B[k][tx], A[ty][k + 1] + B[k + 1][tx]);
+        for (int k = 0; k < T; k += 2) v = KeyOps<K>::min3(v, A[ty][k] + B[k][tx], A[ty][k + 1] + B[k + 1][tx]);
         if (v < old) {
             st_wt(&P[(size_t)(r0 + ty) * T + c0 + tx], v);
             s_chg = 1;
@@ -906,15 +1046,16 @@ __global__ void __launch_bounds__(256) fw_close_sq(uint32_t* __restrict__ P, uin
 }
 
 // lb[slot(j)] <- stored tile (min(j, L), max(j, L)) of D, j = blockIdx.x
-template <int T>
-__global__ void __launch_bounds__(256) k_pack_line(const uint32_t* __restrict__ D, size_t ld, uint32_t* __restrict__ lb,
-                                                   int L, LineMap lm) {
+template <class K, int T>
+__global__ void __launch_bounds__(256) k_pack_line(const K* __restrict__ D, size_t ld, K* __restrict__ lb, int L,
+                                                   LineMap lm) {
+    constexpr int VE = 16 / (int)sizeof(K);
     const int j = (int)blockIdx.x, I = min(j, L), J = max(j, L);
-    const uint32_t* src = D + (size_t)I * T * ld + (size_t)J * T;
-    uint32_t* dst = lb + (size_t)lm.slot(j, L) * T * T;
-    for (int e = threadIdx.x; e < T * T / 4; e += 256) {
-        const int r = e / (T / 4), c4 = e % (T / 4);
-        st16(dst + (size_t)r * T + c4 * 4, ld16(src + (size_t)r * ld + c4 * 4));
+    const K* src = D + (size_t)I * T * ld + (size_t)J * T;
+    K* dst = lb + (size_t)lm.slot(j, L) * T * T;
+    for (int e = threadIdx.x; e < T * T / VE; e += 256) {
+        const int r = e / (T / VE), cv = e % (T / VE);
+        st16(dst + (size_t)r * T + cv * VE, ld16(src + (size_t)r * ld + cv * VE));
     }
 }
 
@@ -922,31 +1063,32 @@ __global__ void __launch_bounds__(256) k_pack_line(const uint32_t* __restrict__ 
 // P[first + i] (T x T each; its segment of the allgather), and after the allgather every rank
 // unpacks every tile t from P[slot[t]] into its row-major D, with the mirror (J, I) = (I, J)^T
 // through 64 x 64 LDS transposes.
-template <int T>
-__global__ void __launch_bounds__(256) k_pack_tiles(const uint32_t* __restrict__ D, size_t ld, int nb,
-                                                    const int* __restrict__ tiles, size_t first, uint32_t* __restrict__ P) {
+template <class K, int T>
+__global__ void __launch_bounds__(256) k_pack_tiles(const K* __restrict__ D, size_t ld, int nb,
+                                                    const int* __restrict__ tiles, size_t first, K* __restrict__ P) {
+    constexpr int VE = 16 / (int)sizeof(K);
     int I, J;
     tri_tile(nb, tiles[blockIdx.x], I, J);
-    const uint32_t* src = D + (size_t)I * T * ld + (size_t)J * T;
-    uint32_t* dst = P + (first + blockIdx.x) * (size_t)T * T;
-    for (int e = threadIdx.x; e < T * T / 4; e += 256) {
-        const int r = e / (T / 4), c4 = e % (T / 4);
-        st16(dst + (size_t)r * T + c4 * 4, ld16(src + (size_t)r * ld + c4 * 4));
+    const K* src = D + (size_t)I * T * ld + (size_t)J * T;
+    K* dst = P + (first + blockIdx.x) * (size_t)T * T;
+    for (int e = threadIdx.x; e < T * T / VE; e += 256) {
+        const int r = e / (T / VE), cv = e % (T / VE);
+        st16(dst + (size_t)r * T + cv * VE, ld16(src + (size_t)r * ld + cv * VE));
     }
 }
 
-template <int T>
-__global__ void __launch_bounds__(256) k_unpack_tiles(const uint32_t* __restrict__ P, const int* __restrict__ slot, int nb,
-                                                      uint32_t* __restrict__ D, size_t ld) {
+template <class K, int T>
+__global__ void __launch_bounds__(256) k_unpack_tiles(const K* __restrict__ P, const int* __restrict__ slot, int nb,
+                                                      K* __restrict__ D, size_t ld) {
     int I, J;
     tri_tile(nb, (int)blockIdx.x, I, J);
-    const uint32_t* src = P + (size_t)slot[blockIdx.x] * T * T;
-    __shared__ uint32_t tile[64][65];
+    const K* src = P + (size_t)slot[blockIdx.x] * T * T;
+    __shared__ K tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int sb = 0; sb < (T / 64) * (T / 64); ++sb) {
         const int bi = sb / (T / 64), bj = sb % (T / 64);
         for (int r = ty; r < 64; r += 4) {
-            const uint32_t v = src[(size_t)(bi * 64 + r) * T + bj * 64 + tx];
+            const K v = src[(size_t)(bi * 64 + r) * T + bj * 64 + tx];
             tile[r][tx] = v;
             D[((size_t)I * T + bi * 64 + r) * ld + (size_t)J * T + bj * 64 + tx] = v;
         }

@@ -1214,8 +1214,8 @@ __global__ void k_low_words(const uint64_t* __restrict__ x, size_t n, uint32_t* 
 // At the end the lower triangle is mirrored (one rank) or the ranks' tiles are all-gathered and
 // unpacked with the mirror, so that every rank holds the whole D.  shadow_amd/dist.py line_fw
 // restates this schedule in numpy (tests/test_dist_cpu.py runs it on gloo ranks).
-template <int T>
-void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
+template <class K, int T>
+void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
                  int& prof_n, double& ms_xchg) {
     constexpr int KCS = 16;
     const int nb = pl.nb, G = pl.G, g = pl.g;
@@ -1227,8 +1227,8 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         std::lock_guard<std::mutex> lk(g_dev_mu);
         c.hop_values = g_dev_ctx[c.device] == 1 && !(hv && std::strcmp(hv, "events") == 0);
     }
-    const size_t lds_bulk = lb_lds_bytes<T, KCS>();
-    set_lds(fw_bulk_lb<T, KCS>, lds_bulk);
+    const size_t lds_bulk = lb_lds<K, T, KCS>();
+    set_lds(fw_bulk_lb<K, T, KCS>, lds_bulk);
     // The chain's line launches.  A large bulk (C3 on one rank: ~nb^2/2 = 3 160 tiles, four rounds
     // of the chip's 768 slots) hides the chain, so the lines take whole tiles (the fewest CU slots
     // taken from the bulk).  A bulk below ~2 rounds (several ranks, or a small graph) leaves the
@@ -1240,17 +1240,17 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     // took 45-117 us per pivot, the one-workgroup FW closure 159 us beside the bulk: r03b/).
     const int bulk_tiles = nb * (nb + 1) / 2 / G;
     const int split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
-    set_lds(fw_line_lb<T, 1>, lb_lds_bytes<T, line_kc<1>()>());
-    set_lds(fw_line_lb<T, 2>, lb_lds_bytes<T / 2, line_kc<2>()>());
-    set_lds(fw_line_lb<T, 4>, lb_lds_bytes<T / 4, line_kc<4>()>());
-    auto line = [&](uint32_t* lbL, int L, uint32_t* lbK, int K1, int mode, int tiles, hipStream_t s) {
+    set_lds(fw_line_lb<K, T, 1>, lb_lds<K, T, line_kc<1>()>());
+    set_lds(fw_line_lb<K, T, 2>, lb_lds<K, T / 2, line_kc<2>()>());
+    set_lds(fw_line_lb<K, T, 4>, lb_lds<K, T / 4, line_kc<4>()>());
+    auto line = [&](K* lbL, int L, K* lbK, int K1, int mode, int tiles, hipStream_t s) {
         if (!tiles) return;
         if (split == 4)
-            fw_line_lb<T, 4><<<dim3(tiles, 16), 256, lb_lds_bytes<T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+            fw_line_lb<K, T, 4><<<dim3(tiles, 16), 256, lb_lds<K, T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
         else if (split == 2)
-            fw_line_lb<T, 2><<<dim3(tiles, 4), 256, lb_lds_bytes<T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+            fw_line_lb<K, T, 2><<<dim3(tiles, 4), 256, lb_lds<K, T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
         else
-            fw_line_lb<T, 1><<<dim3(tiles, 1), 256, lb_lds_bytes<T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+            fw_line_lb<K, T, 1><<<dim3(tiles, 1), 256, lb_lds<K, T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
     };
     const bool prof = c.profiling && nb > 2;
     if (prof) {
@@ -1260,7 +1260,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
             c.prof_events.push_back(e);
         }
     }
-    uint32_t* LB[2] = {(uint32_t*)c.b_L0.get(nb * TT * 4), (uint32_t*)c.b_L1.get(nb * TT * 4)};
+    K* LB[2] = {(K*)c.b_L0.get(nb * TT * sizeof(K)), (K*)c.b_L1.get(nb * TT * sizeof(K))};
     // closure barrier words: 16 per pivot (arrival counter, changed flag per step), then the
     // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
     uint32_t* cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
@@ -1287,27 +1287,27 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     if (ntile) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
     hipStream_t aux = c.aux_stream, cs = c.comm_stream;
     const int prio = c.chain_prio;
-    auto close_pivot = [&](uint32_t* lbk, int k, hipStream_t s) {
-        fw_close_sq<T><<<dim3(T / 16, T / 16), 256, 0, s>>>(lbk + (size_t)lm.slot(k, k) * TT, cflags + 16 * k,
+    auto close_pivot = [&](K* lbk, int k, hipStream_t s) {
+        fw_close_sq<K, T><<<dim3(T / 16, T / 16), 256, 0, s>>>(lbk + (size_t)lm.slot(k, k) * TT, cflags + 16 * k,
                                                              c.fw_timeout, prio);
     };
     // line 0: every rank holds the same initial D
-    k_pack_line<T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
+    k_pack_line<K, T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
     close_pivot(LB[0], 0, st);
     line(LB[0], 0, LB[0], 0, 1, nb, st);  // (with nb == 1 this only copies the closed pivot tile back to D)
     HIP_CHECK(hipGetLastError());
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1;
-        uint32_t* lbk = LB[kb & 1];
+        K* lbk = LB[kb & 1];
         if (k1 < nb) {
-            uint32_t* lbn = LB[k1 & 1];
+            K* lbn = LB[k1 & 1];
             stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
             if (multi) {  // on the chain's own stream: no cross-queue hop around it
                 std::vector<size_t> offs(G), lens(G);
                 for (int r = 0; r < G; ++r) {
-                    offs[r] = (size_t)lm.base(r, k1) * TT * 4;
-                    lens[r] = (size_t)lm.count(r, k1) * TT * 4;
+                    offs[r] = (size_t)lm.base(r, k1) * TT * sizeof(K);
+                    lens[r] = (size_t)lm.count(r, k1) * TT * sizeof(K);
                 }
                 c.comm->allgatherv(lbn, offs.data(), lens.data(), aux);
             }
@@ -1318,7 +1318,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
         // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
         const bool timed = prof && ntile > 0 && k1 < nb;
         if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        if (ntile > 0) fw_bulk_lb<T, KCS><<<ntile, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, tiles);
+        if (ntile > 0) fw_bulk_lb<K, T, KCS><<<ntile, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, tiles);
         HIP_CHECK(hipGetLastError());
         if (timed) {
             int64_t m = 0;  // relaxations of this launch: own tiles off lines kb and k1
@@ -1336,27 +1336,27 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, uint32_t* D, size_t Vp, hipStream_t
     HIP_CHECK(hipGetLastError());
     if (!multi) {
         const unsigned nb64 = (unsigned)(Vp / 64);
-        k_sym_mirror<uint32_t><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
+        k_sym_mirror<K><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
         return;
     }
     // every rank ends with the whole D: pack the own tiles, all-gather, unpack with the mirror
     HIP_CHECK(hipStreamSynchronize(st));  // (FW done: the exchange is timed on its own)
     auto t0x = std::chrono::steady_clock::now();
-    uint32_t* Pk = (uint32_t*)c.b_PRED.get((size_t)ntri * TT * 4);
+    K* Pk = (K*)c.b_PRED.get((size_t)ntri * TT * sizeof(K));
     int* slot = (int*)c.b_tslot.get((size_t)ntri * 4);
     HIP_CHECK(hipMemcpyAsync(slot, slot_h.data(), (size_t)ntri * 4, hipMemcpyHostToDevice, st));
-    if (ntile) k_pack_tiles<T><<<ntile, 256, 0, st>>>(D, Vp, nb, tiles, (size_t)first[g], Pk);
+    if (ntile) k_pack_tiles<K, T><<<ntile, 256, 0, st>>>(D, Vp, nb, tiles, (size_t)first[g], Pk);
     std::vector<size_t> offs(G), lens(G);
     for (int r = 0; r < G; ++r) {
-        offs[r] = (size_t)first[r] * TT * 4;
-        lens[r] = (size_t)(first[r + 1] - first[r]) * TT * 4;
+        offs[r] = (size_t)first[r] * TT * sizeof(K);
+        lens[r] = (size_t)(first[r + 1] - first[r]) * TT * sizeof(K);
     }
     HIP_CHECK(hipEventRecord(c.ev_b, st));
     HIP_CHECK(hipStreamWaitEvent(cs, c.ev_b, 0));
     c.comm->allgatherv(Pk, offs.data(), lens.data(), cs);
     HIP_CHECK(hipEventRecord(c.ev_c, cs));
     HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
-    k_unpack_tiles<T><<<ntri, 256, 0, st>>>(Pk, slot, nb, D, Vp);
+    k_unpack_tiles<K, T><<<ntri, 256, 0, st>>>(Pk, slot, nb, D, Vp);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(st));
     ms_xchg += ms_since(t0x);
@@ -1382,10 +1382,11 @@ void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t
     ms_xchg += ms_since(t0x);
 }
 
-// the symmetric FW over line buffers applies: undirected, u32 pair-packed 128-tiles
+// the symmetric FW over line buffers applies: undirected, u32 pair-packed 128-tiles or u64 64-tiles
 template <class K, int T>
 bool sym_fw_for(const srg_ctx& c, const DevGraph& g) {
-    return sizeof(K) == 4 && T == 128 && c.fw_symmetric && !g.directed && c.fw_packed != 0;
+    return ((sizeof(K) == 4 && T == 128 && c.fw_packed != 0) || (sizeof(K) == 8 && T == 64)) && c.fw_symmetric &&
+           !g.directed;
 }
 
 // Dense path for key type K. Returns false (u32 only) when certification fails.
@@ -1440,7 +1441,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     int prof_n = 0;
     double ms_dx = 0;  // multi-rank: D exchange at the end of FW (inside ms_fw, also in ms_exchange)
     if (sym_fw_for<K, T>(c, g)) {
-        if constexpr (sizeof(K) == 4 && T == 128) fw_line_sym<T>(c, pl, (uint32_t*)D, Vp, st, prof_relax, prof_n, ms_dx);
+        if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64))
+            fw_line_sym<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx);
     } else {
         if constexpr (sizeof(K) == 4) {
             if (c.fw_packed) fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n);

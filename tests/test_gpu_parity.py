@@ -150,6 +150,32 @@ def test_fw_symmetric_matches_general(V):
         assert_parity(out[1], lat, loss)
 
 
+@pytest.mark.parametrize("V,split", [(60, 0), (200, 0), (700, 1), (700, 2), (700, 4), (1500, 0)])
+def test_fw_symmetric_u64_matches_general(V, split, monkeypatch):
+    """u64 keys (nanosecond keys, SRG_LATENCY_UNIT=1, on latencies x 1000 so that used paths pass
+    2^31 ns): the symmetric line-buffer FW on 64-tiles (fw_core_lb64, fw_close_sq<u64>) equals the
+    general u64 FW bit for bit at one to 24 tiles and every line split; oracle rows pin it."""
+    monkeypatch.setenv("SRG_LATENCY_UNIT", "1")
+    g = synth.atlas_like(V, seed=V + 11)
+    e = Edges(V, g.src, g.dst, g.latency_ns * np.uint64(1000), g.packet_loss, directed=False)
+    nodes = np.random.default_rng(V).permutation(V).tolist()
+    out = []
+    for sym in (0, 1):
+        r = Router(0)
+        r.set_option(N.SRG_OPT_FW_SYMMETRIC, sym)
+        if split:
+            r.set_option(N.SRG_OPT_FW_LINE_SPLIT, split)
+        t = r.compute_shortest_paths(e, nodes)
+        assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U64 and t.stats["latency_unit_ns"] == 1
+        out.append(t)
+        r.close()
+    assert np.array_equal(out[0].latency_ns, out[1].latency_ns)
+    assert bits_equal(out[0].packet_loss, out[1].packet_loss)
+    rows = [0, V // 2, V - 1]
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
+    assert np.array_equal(out[1].latency_ns[rows], lat) and bits_equal(out[1].packet_loss[rows], loss)
+
+
 def test_fw_stream_hops_events_match_values(monkeypatch):
     """The FW's two cross-stream hops per pivot as stream-value waits (a context alone on its
     device) and as events (SRG_STREAM_HOPS=events: several contexts per device, profilers) give
