@@ -648,6 +648,7 @@ struct srg_ctx {
     DevBuf b_lnodes, b_lpos, b_red, b_outoff, b_outdst;
     DevBuf b_cflags, b_tiles, b_tslot;  // symmetric FW: closure barrier words, own tiles, packed slots
     uint32_t* fw_timeout = nullptr;     // symmetric FW: raised by a closure grid barrier that timed out
+    unsigned char* hbox = nullptr;      // page-locked mailbox for small device -> host readbacks (rb_async)
     uint32_t* sig[2] = {nullptr, nullptr};  // stream_hop signals (HSA signal memory), their last values
     uint32_t sig_val[2] = {0, 0};
     bool hop_values = false;            // this build's hops use the signals (stream_hop)
@@ -671,6 +672,7 @@ struct srg_ctx {
         for (hipEvent_t e : ev_lring)
             if (e) (void)hipEventDestroy(e);
         if (h_lring) (void)hipHostFree(h_lring);
+        if (hbox) (void)hipHostFree(hbox);
         for (hipStream_t s : {aux_stream, comm_stream, d2h_stream, stream})
             if (s) (void)hipStreamDestroy(s);
         delete pool;
@@ -753,6 +755,24 @@ void set_lds(F func, size_t bytes) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
 }
 
+// Small device -> host readbacks (flags, counters) through the context's page-locked mailbox:
+// one asynchronous DMA each, read after the stream's next synchronisation.  Into pageable host
+// memory the runtime stages such a copy synchronously (~20 us per call on top of the sync;
+// C1 paid a dozen of them per build).  64-byte slots, kMailSlots of them.
+constexpr int kMailSlots = 64;
+template <class T>
+void rb_async(srg_ctx& c, int slot, const T* dev, hipStream_t st) {
+    static_assert(sizeof(T) <= 64, "mailbox slot");
+    HIP_CHECK(hipMemcpyAsync(c.hbox + 64 * slot, dev, sizeof(T), hipMemcpyDeviceToHost, st));
+}
+template <class T>
+T rb_get(const srg_ctx& c, int slot) {
+    T v;
+    std::memcpy(&v, c.hbox + 64 * slot, sizeof(T));
+    return v;
+}
+enum MailSlot { MS_EDGESTATS, MS_FLAGS, MS_TIMEOUT, MS_REDUCE, MS_TAIL0, MS_TAIL1, MS_NMULTI, MS_CHANGED, MS_MIN };
+
 // Common validation: nodes in range & unique, edge endpoints, self-loop counts, latency range.
 struct Prelude {
     EdgeStats es;
@@ -788,10 +808,12 @@ Prelude prelude(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     HIP_CHECK(hipGetLastError());
     Flags fl;
     P.nodes_h.resize(n);
-    HIP_CHECK(hipMemcpyAsync(&P.es, es, sizeof(EdgeStats), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&fl, P.flags, sizeof(Flags), hipMemcpyDeviceToHost, st));
+    rb_async(c, MS_EDGESTATS, es, st);
+    rb_async(c, MS_FLAGS, P.flags, st);
     if (n) HIP_CHECK(hipMemcpyAsync(P.nodes_h.data(), nodes, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    P.es = rb_get<EdgeStats>(c, MS_EDGESTATS);
+    fl = rb_get<Flags>(c, MS_FLAGS);
     if (P.es.bad_endpoint) fail(SRG_ERR_ARG, "edge endpoint out of range (>= num_vertices)");
     if (fl.bad_node & 1) fail(SRG_ERR_ARG, "node index out of range (>= num_vertices)");
     if (fl.bad_node & 2) fail(SRG_ERR_ARG, "duplicate node index in `nodes`");
@@ -1453,12 +1475,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         if (multi) gather_rows<K>(c, pl, D, Vp, T, st, ms_dx);
     }
     HIP_CHECK(hipGetLastError());
+    if (sym_fw_for<K, T>(c, g)) rb_async(c, MS_TIMEOUT, c.fw_timeout, st);  // read after FW, on its stream
     const double ms_fw = tm.lap();
-    if (sym_fw_for<K, T>(c, g)) {
-        uint32_t tmo = 0;
-        HIP_CHECK(hipMemcpy(&tmo, c.fw_timeout, 4, hipMemcpyDeviceToHost));
-        if (tmo) fail(SRG_ERR_HIP, "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
-    }
+    if (sym_fw_for<K, T>(c, g) && rb_get<uint32_t>(c, MS_TIMEOUT))
+        fail(SRG_ERR_HIP, "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
     if (wl_late) {
         // WL = min loss among the min-latency parallel edges (what k_w_split gives), from the
         // losses that crossed PCIe during FW.  Built here, after FW, rather than beside it: on a
@@ -1512,10 +1532,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             c.comm->allreduce_max_u32(red, 1, cs);
             st_after_cs();
         }
-        uint32_t v = 0;
-        HIP_CHECK(hipMemcpyAsync(&v, red, 4, hipMemcpyDeviceToHost, st));
+        rb_async(c, MS_REDUCE, red, st);
         HIP_CHECK(hipStreamSynchronize(st));
-        return v;
+        return rb_get<uint32_t>(c, MS_REDUCE);
     };
     // output rows of every rank: positions [n r / G, n (r+1) / G)
     const bool exchange = multi && c.gather_output;
@@ -1620,12 +1639,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         void* tmp = c.b_scantmp.get(tbytes);
         HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, ta, indeg, cscoff, (int)(NT + 1), st));
         HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tc, v5_glen, v5_goff, (int)(NG5 + 1), st));
-        uint32_t tail[2];
-        HIP_CHECK(hipMemcpyAsync(&tail[0], cscoff + NT, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(&tail[1], v5_goff + NG5, 4, hipMemcpyDeviceToHost, st));
+        rb_async(c, MS_TAIL0, cscoff + NT, st);
+        rb_async(c, MS_TAIL1, v5_goff + NG5, st);
         HIP_CHECK(hipStreamSynchronize(st));
-        E_ess = tail[0];
-        E_layout = 2ull * tail[1];
+        E_ess = rb_get<uint32_t>(c, MS_TAIL0);
+        E_layout = 2ull * rb_get<uint32_t>(c, MS_TAIL1);
     }
     n_ess = E_ess;
     if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));  // WL (late loss) before the entry fill
@@ -1792,8 +1810,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             Lfin = Lin;
         }
     }
-    HIP_CHECK(hipMemcpyAsync(&nmulti, multi_cnt, 8, hipMemcpyDeviceToHost, st));
+    rb_async(c, MS_NMULTI, multi_cnt, st);
     const double ms_loss = tm.lap();
+    nmulti = rb_get<unsigned long long>(c, MS_NMULTI);
 
     if (nloc && !loss_written)
         k_extract<K><<<nloc, kThreads, 0, st>>>(D, Lfin, Vp, lnodes, nloc, nodes, n, lpos,
@@ -2639,13 +2658,14 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             unsigned long long* dmin = (unsigned long long*)c->b_multi.get(8);
             HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 8, st));
             k_min_u64<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dol + rows_off, rows_nn, dmin);
-            HIP_CHECK(hipMemcpyAsync(&hmin, dmin, 8, hipMemcpyDeviceToHost, st));
+            rb_async(*c, MS_MIN, dmin, st);
         }
         if (rows_nn && !sink.lat_sent)
             HIP_CHECK(hipMemcpyAsync(out_lat + rows_off, dol + rows_off, rows_nn * 8, hipMemcpyDeviceToHost, st));
         if (rows_nn && !sink.loss_sent)
             HIP_CHECK(hipMemcpyAsync(out_loss + rows_off, dos + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
+        if (rows_nn && stats) hmin = rb_get<unsigned long long>(*c, MS_MIN);
         sink.finish();
         if (stats) {
             stats->ms_h2d = ms_h2d;
@@ -2687,6 +2707,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+        HIP_CHECK(hipHostMalloc((void**)&c->hbox, 64 * kMailSlots, hipHostMallocDefault));
         c->sdma.init(device);  // SDMA engine for the host entry's early D2H (else hipMemcpyAsync)
         // the late-loss H2D and WL build share the D2H stream (idle until FW ends): a fifth
         // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
