@@ -150,8 +150,9 @@ void srg_destroy(srg_ctx* ctx);
                                         below the bucket bound, 0 (default) = when any is */
 #define SRG_OPT_SPARSE_GLOBAL_BITMAPS 14 /* sparse: 1 = keep the per-batch vertex bitmaps in global memory
                                         (automatic when 5V/8 bytes do not fit the LDS budget) */
-#define SRG_OPT_FW_SYMMETRIC 17     /* dense u32: 1 (default) = for an undirected graph on one rank, update only
-                                       the FW tiles I <= J (D stays symmetric) and mirror at the end */
+#define SRG_OPT_FW_SYMMETRIC 17     /* dense: 1 (default) = for an undirected graph, update only the FW tiles
+                                       I <= J (D stays symmetric; u32 keys on 128-tiles, u64 keys on 64-tiles,
+                                       one rank or many) and mirror at the end; 0 = the general FW */
 #define SRG_OPT_CHAIN_PRIO 18       /* dense: 1 (default) = the FW lookahead chain kernels raise their wave priority */
 #define SRG_OPT_D2H_MODE 20         /* host entry: how finished rows are shipped into the page-locked caller
                                      * arrays while kernels run: 1 (default) = an SDMA engine, 0 =
