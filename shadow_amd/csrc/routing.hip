@@ -2176,7 +2176,7 @@ void events_sort(srg_ctx& c, const EvIn& in, const uint64_t* deliver, const EvKe
     for (uint32_t p = 0; p < bits; p += 8) {
         k_rs_hist<WIDE><<<ntiles, RS_THREADS, 0, st>>>(k0, h0, n, p, ntiles, hist);
         HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, offs, nh, st));
-        k_rs_scatter<WIDE><<<ntiles, RS_THREADS, 0, st>>>(k0, h0, i0, k1, h1, i1, n, p, ntiles, offs);
+        k_rs_scatter<WIDE><<<ntiles, RS_THREADS, 0, st>>>(k0, h0, i0, k1, h1, i1, n, p, ntiles, hist, offs);
         std::swap(k0, k1);
         std::swap(h0, h1);
         std::swap(i0, i1);
