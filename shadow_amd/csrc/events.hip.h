@@ -248,17 +248,23 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const unsigned long l
     for (int q = 0; q < RS_THREADS / 64; ++q) wcnt[q][tid] = 0;
     __syncthreads();
     const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    // every round's keys in flight at once (the rounds below only rank them)
+    unsigned long long rlo[RS_ROUNDS], rhi[RS_ROUNDS];
+    uint32_t rid[RS_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        const uint32_t li = (uint32_t)r * RS_THREADS + tid;
+        rlo[r] = li < tn ? klo[base + li] : 0ull;
+        rhi[r] = WIDE && li < tn ? khi[base + li] : 0ull;
+        rid[r] = li < tn ? idx[base + li] : 0u;
+    }
+#pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
         const uint32_t li = (uint32_t)r * RS_THREADS + tid;
         const bool valid = li < tn;
-        unsigned long long lo = 0, hi = 0;
-        uint32_t id = 0, d = 0;
-        if (valid) {
-            lo = klo[base + li];
-            if (WIDE) hi = khi[base + li];
-            id = idx[base + li];
-            d = rs_digit(lo, hi, p);
-        }
+        const unsigned long long lo = rlo[r], hi = rhi[r];
+        const uint32_t id = rid[r];
+        const uint32_t d = valid ? rs_digit(lo, hi, p) : 0u;
         unsigned long long m = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
