@@ -1729,10 +1729,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             ms_scan = tm.lap();
             if (interleave) {  // loss rows already folded and shipped, group by group
                 sink->loss_sent = true;
-                uint32_t sw = 0;
-                HIP_CHECK(hipMemcpyAsync(&sw, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                rb_async(c, MS_CHANGED, &P.flags->changed, st);
                 HIP_CHECK(hipStreamSynchronize(st));
-                rounds = (int)sw;
+                rounds = (int)rb_get<uint32_t>(c, MS_CHANGED);
                 loss_written = true;
             } else if (lds_rows <= 150 * 1024) {
                 // per-row Gauss-Seidel in LDS, writes out_loss directly
@@ -1751,10 +1750,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                     if (sink_rows) sink->send_rows(st, out_loss, sink->loss, pl.p0 + r0, r1 - r0, 4);
                 }
                 if (sink_rows) sink->loss_sent = true;
-                uint32_t sw = 0;
-                HIP_CHECK(hipMemcpyAsync(&sw, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                rb_async(c, MS_CHANGED, &P.flags->changed, st);
                 HIP_CHECK(hipStreamSynchronize(st));
-                rounds = (int)sw;
+                rounds = (int)rb_get<uint32_t>(c, MS_CHANGED);
                 loss_written = true;
             } else {
                 float* L0 = (float*)c.b_L0.get(nmax * Vp * 4);
@@ -1769,9 +1767,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                         &P.flags->changed);
                     HIP_CHECK(hipGetLastError());
                     ++rounds;
-                    uint32_t ch = 0;
-                    HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                    rb_async(c, MS_CHANGED, &P.flags->changed, st);
                     HIP_CHECK(hipStreamSynchronize(st));
+                    const uint32_t ch = rb_get<uint32_t>(c, MS_CHANGED);
                     std::swap(Lin, Lout);
                     if (!ch) break;
                     if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
@@ -1800,9 +1798,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                     PRED, D, W, WL, lnodes, nloc, V, Vp, Lin, Lout, P.flags);
                 HIP_CHECK(hipGetLastError());
                 ++rounds;
-                uint32_t ch = 0;
-                HIP_CHECK(hipMemcpyAsync(&ch, &P.flags->changed, 4, hipMemcpyDeviceToHost, st));
+                rb_async(c, MS_CHANGED, &P.flags->changed, st);
                 HIP_CHECK(hipStreamSynchronize(st));
+                const uint32_t ch = rb_get<uint32_t>(c, MS_CHANGED);
                 std::swap(Lin, Lout);
                 if (!ch) break;
                 if (rounds > (int)V + 2) fail(SRG_ERR_INTERNAL, "loss rounds did not converge");
