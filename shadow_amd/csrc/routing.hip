@@ -2473,14 +2473,21 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
     reg.wait = c->d2h_stream;
     const bool early = !direct && nn * 12 >= ((size_t)64 << 20);
     const bool ext = (bool)c->ext_reg;
+    // a rank of a group that fills only its own rows [n r / N, n (r+1) / N) of a table the ranks
+    // share (SRG_OPT_GATHER_OUTPUT 0, one process per GPU) page-locks only those rows: N processes
+    // pinning the whole shared table each cost N times the pinning, and a shared-memory table is
+    // typically 4-KB pages (~50 ms per 1.2 GB)
+    const bool rows_part = !direct && c->comm && c->comm->nranks > 1 && !c->gather_output;
+    const size_t reg_r0 = rows_part ? (size_t)num_nodes * c->comm->rank / c->comm->nranks : 0;
+    const size_t reg_r1 = rows_part ? (size_t)num_nodes * (c->comm->rank + 1) / c->comm->nranks : num_nodes;
     if (early && !ext) {
-        reg.p[0] = out_lat;
-        reg.b[0] = nn * 8;
-        reg.p[1] = out_loss;
-        reg.b[1] = nn * 4;
+        reg.p[0] = out_lat + reg_r0 * num_nodes;
+        reg.b[0] = (reg_r1 - reg_r0) * num_nodes * 8;
+        reg.p[1] = out_loss + reg_r0 * num_nodes;
+        reg.b[1] = (reg_r1 - reg_r0) * num_nodes * 4;
         reg.th = std::thread([&reg]() {
             const auto t0 = std::chrono::steady_clock::now();
-            if (hipSetDevice(reg.device) != hipSuccess) return;
+            if (!reg.b[0] || hipSetDevice(reg.device) != hipSuccess) return;
             advise_huge(reg.p[0], reg.b[0]);
             advise_huge(reg.p[1], reg.b[1]);
             if (hipHostRegister(reg.p[0], reg.b[0], hipHostRegisterMapped) != hipSuccess) return;
@@ -2628,10 +2635,11 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                     return true;
                 };
             } else {
-                sink.ready = [&reg, &sink]() {
+                sink.ready = [&reg, &sink, reg_r0, num_nodes]() {
                     if (!reg.join()) return false;
-                    sink.lat_view = reg.view[0];
-                    sink.loss_view = reg.view[1];
+                    // views of rows [reg_r0, ...): based so that row r lands at view + r * n
+                    sink.lat_view = (unsigned char*)reg.view[0] - reg_r0 * num_nodes * 8;
+                    sink.loss_view = (unsigned char*)reg.view[1] - reg_r0 * num_nodes * 4;
                     return true;
                 };
             }

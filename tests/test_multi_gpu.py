@@ -113,6 +113,30 @@ def test_ranks_without_exchange_fill_own_rows(kind):
     assert covered.all()
 
 
+def test_ranks_without_exchange_own_rows_page_locked():
+    """Output exchange off with a table past the early-D2H threshold (n^2 x 12 B >= 64 MB): each
+    rank page-locks only its own rows [n r / G, n (r+1) / G) of the caller's table and ships them
+    while later kernels run (SDMA into the mapped rows); the rows equal the single-GPU table's."""
+    V = 2400
+    e = synth.atlas_like(V, seed=2400)
+    nodes = node_list("scrambled", V, 12)
+    ref_router = Router(0)
+    ref = ref_router.compute_shortest_paths(e, nodes)
+    ref_router.close()
+    G = 3
+    out, errs = run_ranks(G, e, nodes, gather=False)
+    assert errs == [None] * G, errs
+    n = len(nodes)
+    for r, t in enumerate(out):
+        rows = list(range(n * r // G, n * (r + 1) // G))
+        assert np.array_equal(t.latency_ns[rows], ref.latency_ns[rows]), f"rank {r}"
+        assert bits_equal(t.packet_loss[rows], ref.packet_loss[rows]), f"rank {r}"
+        assert t.stats["d2h_overlapped_bytes"] == len(rows) * n * 12, f"rank {r}"
+    rows = [0, n // 2, n - 1]
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
+    assert np.array_equal(ref.latency_ns[rows], lat) and bits_equal(ref.packet_loss[rows], loss)
+
+
 def test_ranks_without_exchange_more_ranks_than_nodes():
     """n < G: some ranks own no source; they ship nothing and report no minimum."""
     e = synth.random_graph(150, 0.06, 14)
