@@ -368,6 +368,9 @@ def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, rooflin
         "apsp_wall_ms": round(ms_per_step, 3),
         "ms_h2d": round(agg.get("ms_h2d", 0) / n, 3), "ms_d2h": round(agg.get("ms_d2h", 0) / n, 3),
         "d2h_overlapped_GB": round(agg.get("d2h_overlapped_bytes", 0) / n / 1e9, 3),
+        # page-locking of the caller's output rows on a helper thread (hidden unless it outlasts
+        # H2D + FW; -1 = not used)
+        "ms_host_register": round(agg.get("ms_host_register", 0) / n, 3),
         "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
         "loss_rounds": s["loss_rounds"], "multi_pred_pairs": s["multi_pred_pairs"],
         "essential_edges": s["essential_edges"], "scan_kind": s["scan_kind"],
