@@ -637,6 +637,8 @@ struct srg_ctx {
     size_t h_ring_bytes = 0;
     hipEvent_t ev_ring[3] = {nullptr, nullptr, nullptr};
     DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
+    DevBuf b_exc;                    // sequential-pair codec: a chunk's exceptions (index, src, dst)
+    std::vector<std::vector<uint32_t>> codec_ex;  // its per-worker exception lists
     size_t own_row0 = 0, own_row1 = ~(size_t)0;  // the output rows this rank routed (multi-rank: [p0, p1))
     int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
     hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
@@ -701,7 +703,7 @@ struct srg_ctx {
         for (hipEvent_t e : ev_ring)
             if (e) (void)hipEventDestroy(e);
         if (h_ring) (void)hipHostFree(h_ring);
-        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_DST2})
+        for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_DST2, &b_exc})
             b->release();
     }
 };
@@ -2283,6 +2285,27 @@ __global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const 
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
               bool& all_narrow);
 
+// Sequential-pair codec, device side: edge i of a chunk is (src, dst) = (es[j], ed[j] + i - ei[j])
+// for the last exception j with ei[j] <= i (ei[0] = 0: a chunk starts with one), latency = l32[i].
+// Consecutive lanes search the same few exceptions (wave-broadcast loads).
+__global__ void k_decode_seq(size_t ne, const uint32_t* __restrict__ l32, const uint32_t* __restrict__ exc, uint32_t nexc,
+                             uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint64_t* __restrict__ lat) {
+    const uint32_t* ei = exc;
+    const uint32_t* es = exc + nexc;
+    const uint32_t* ed = exc + 2 * (size_t)nexc;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < ne; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = nexc - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (ei[mid] <= (uint32_t)i) lo = mid;
+            else hi = mid - 1;
+        }
+        src[i] = es[lo];
+        dst[i] = ed[lo] + ((uint32_t)i - ei[lo]);
+        lat[i] = l32[i];
+    }
+}
+
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
     T* d = (T*)b.get(std::max<size_t>(count, 1) * sizeof(T));
@@ -2292,6 +2315,12 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
 
 // Ships edges [a0, a1) into the full-length device arrays (the rank's slice when the edge list
 // is sharded, else all of it).
+// Sequential-pair mode (whole lists only; SRG_CODEC_SEQ=0 turns it off): an edge list in
+// row order -- a GML complete graph lists (i, i), (i, i+1), ... (i, V-1), then row i+1 -- needs
+// no endpoints over PCIe: an edge (s, d) following (s, d - 1) is implied, and only the others
+// (row starts, ~V of them) cross as exceptions, so a chunk is its u32 latencies (4 B per edge
+// instead of 8) plus ~12 B per row.  A chunk with more than 1/8 exceptions is re-narrowed to
+// u16 endpoints and the rest of the list stays in that mode.
 // all_narrow: every edge of the slice also stays narrowed on the device (b_n16s / b_n16d / b_n32l),
 // false when the host-slow switch shipped the rest of the slice plain.
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
@@ -2328,6 +2357,12 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     const bool dbg = std::getenv("SRG_DEBUG_CODEC") != nullptr;
     double t_conv = 0, t_wait = 0;
     const size_t nch = (A + CE - 1) / CE;
+    const char* sq = std::getenv("SRG_CODEC_SEQ");
+    bool seq = A == E && sq && std::strcmp(sq, "1") == 0;  // (opt-in until measured on the GPU)
+    uint32_t* dexc = seq ? (uint32_t*)c.b_exc.get(CE * 4) : nullptr;
+    const int nwk = c.pool->size();
+    if ((int)c.codec_ex.size() < nwk) c.codec_ex.resize(nwk);
+    size_t seq_chunks = 0;
     for (size_t ch = 0; ch < nch; ++ch) {
         const int b = (int)(ch % NB);
         auto tw = std::chrono::steady_clock::now();
@@ -2340,6 +2375,8 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
         float* hb = (float*)(hl + CE);
         auto tc = std::chrono::steady_clock::now();
         t_wait += std::chrono::duration<double, std::milli>(tc - tw).count();
+        std::atomic<bool> dense{false};
+        const bool seq_ch = seq;
         c.pool->run([&](int w, int nw) {
             const size_t a = ne * w / nw, z = ne * (w + 1) / nw;
             const uint32_t* src = g->src + e0;
@@ -2347,18 +2384,65 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             const uint64_t* lat = g->latency_ns + e0;
             uint32_t orx = 0;
             uint64_t orl = 0;
-            for (size_t i = a; i < z; ++i) {
-                const uint32_t x = src[i], y = dst[i];
-                const uint64_t l = lat[i];
-                orx |= x | y;
-                orl |= l;
-                hs[i] = (uint16_t)x;
-                hd[i] = (uint16_t)y;
-                hl[i] = (uint32_t)l;
+            if (seq_ch) {
+                std::vector<uint32_t>& ex = c.codec_ex[w];
+                ex.clear();
+                const size_t cap = 3 * ((z - a) / 8 + 1);
+                // the previous edge of the slice (none at a chunk's start: an exception)
+                uint32_t ps = a ? src[a - 1] : 0u, pd = a ? dst[a - 1] : 0u;
+                bool have = a > 0;
+                for (size_t i = a; i < z; ++i) {
+                    const uint32_t x = src[i], y = dst[i];
+                    const uint64_t l = lat[i];
+                    orx |= x | y;
+                    orl |= l;
+                    hl[i] = (uint32_t)l;
+                    if (!(have && x == ps && y == pd + 1u)) {
+                        ex.push_back((uint32_t)i);
+                        ex.push_back(x);
+                        ex.push_back(y);
+                        if (ex.size() > cap) {
+                            dense.store(true, std::memory_order_relaxed);  // (redone below with u16 endpoints)
+                            for (size_t k = i + 1; k < z; ++k) {  // finish the latencies and the checks
+                                const uint32_t x2 = src[k], y2 = dst[k];
+                                const uint64_t l2 = lat[k];
+                                orx |= x2 | y2;
+                                orl |= l2;
+                                hl[k] = (uint32_t)l2;
+                            }
+                            break;
+                        }
+                    }
+                    ps = x;
+                    pd = y;
+                    have = true;
+                }
+            } else {
+                for (size_t i = a; i < z; ++i) {
+                    const uint32_t x = src[i], y = dst[i];
+                    const uint64_t l = lat[i];
+                    orx |= x | y;
+                    orl |= l;
+                    hs[i] = (uint16_t)x;
+                    hd[i] = (uint16_t)y;
+                    hl[i] = (uint32_t)l;
+                }
             }
             if (with_loss) std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
             if ((orx >> 16) || (orl >> 32)) bad.store(true, std::memory_order_relaxed);
         });
+        if (seq_ch && dense.load() && !bad.load()) {
+            // not a row-ordered list: this chunk's endpoints narrowed after all, u16 from here on
+            seq = false;
+            c.pool->run([&](int w, int nw) {
+                const size_t a = ne * w / nw, z = ne * (w + 1) / nw;
+                for (size_t i = a; i < z; ++i) {
+                    hs[i] = (uint16_t)g->src[e0 + i];
+                    hd[i] = (uint16_t)g->dst[e0 + i];
+                }
+            });
+        }
+        const bool chunk_seq = seq_ch && !dense.load();
         const double dt = ms_since(tc);
         t_conv += dt;
         if (bad.load()) {
@@ -2369,13 +2453,37 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
         // ~55 GB/s): the remaining edges go plain, straight from the caller's arrays
         bool slow = ch + 1 < nch && dt > (double)ne * 20.0 / 55e9 * 1e3;
         if (const char* f = std::getenv("SRG_CODEC_SLOW_AFTER")) slow = ch + 1 < nch && ch >= (size_t)std::atoll(f);  // tests
-        HIP_CHECK(hipMemcpyAsync(s16 + e0, hs, ne * 2, hipMemcpyHostToDevice, st));
-        HIP_CHECK(hipMemcpyAsync(d16 + e0, hd, ne * 2, hipMemcpyHostToDevice, st));
-        HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
-        if (with_loss) HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, hb, ne * 4, hipMemcpyHostToDevice, st));
-        HIP_CHECK(hipEventRecord(c.ev_ring[b], st));
-        k_widen_edges<<<grid_for(ne), kThreads, 0, st>>>(ne, s16 + e0, d16 + e0, l32 + e0, (uint32_t*)dg.src + e0,
-                                                          (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
+        if (chunk_seq) {
+            // the workers' exception lists, in order, as SoA (index | src | dst) where the u16
+            // endpoints would have gone
+            size_t nexc = 0;
+            for (int w = 0; w < nwk; ++w) nexc += c.codec_ex[w].size() / 3;
+            uint32_t* hx = (uint32_t*)hs;
+            size_t q = 0;
+            for (int w = 0; w < nwk; ++w) {
+                const std::vector<uint32_t>& ex = c.codec_ex[w];
+                for (size_t k = 0; k + 2 < ex.size(); k += 3, ++q) {
+                    hx[q] = ex[k];
+                    hx[nexc + q] = ex[k + 1];
+                    hx[2 * nexc + q] = ex[k + 2];
+                }
+            }
+            HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync(dexc, hx, nexc * 12, hipMemcpyHostToDevice, st));
+            if (with_loss) HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, hb, ne * 4, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipEventRecord(c.ev_ring[b], st));
+            k_decode_seq<<<grid_for(ne), kThreads, 0, st>>>(ne, l32 + e0, dexc, (uint32_t)nexc, (uint32_t*)dg.src + e0,
+                                                             (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
+            ++seq_chunks;
+        } else {
+            HIP_CHECK(hipMemcpyAsync(s16 + e0, hs, ne * 2, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync(d16 + e0, hd, ne * 2, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
+            if (with_loss) HIP_CHECK(hipMemcpyAsync((float*)dg.loss + e0, hb, ne * 4, hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipEventRecord(c.ev_ring[b], st));
+            k_widen_edges<<<grid_for(ne), kThreads, 0, st>>>(ne, s16 + e0, d16 + e0, l32 + e0, (uint32_t*)dg.src + e0,
+                                                              (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
+        }
         HIP_CHECK(hipGetLastError());
         if (slow) {
             const size_t r0 = e0 + ne, rn = a1 - r0;
@@ -2389,8 +2497,9 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             break;
         }
     }
-    if (dbg) std::fprintf(stderr, "codec: %zu chunks, %d threads, convert %.2f ms, slot waits %.2f ms\n", nch,
-                          c.pool->size(), t_conv, t_wait);
+    if (seq_chunks) all_narrow = false;  // (the endpoints are not on the device narrowed)
+    if (dbg) std::fprintf(stderr, "codec: %zu chunks (%zu sequential-pair), %d threads, convert %.2f ms, slot waits %.2f ms\n",
+                          nch, seq_chunks, c.pool->size(), t_conv, t_wait);
     return true;
 }
 

@@ -509,6 +509,47 @@ def test_h2d_codec_matches_plain(router):
     assert np.array_equal(t.latency_ns, t0.latency_ns) and bits_equal(t.packet_loss, t0.packet_loss)
 
 
+@pytest.mark.parametrize("order", ["rows", "rows_gaps", "shuffled_tail", "shuffled"])
+def test_h2d_codec_sequential_pairs(router, monkeypatch, order):
+    """Sequential-pair codec (routing.hip codec_in): a row-ordered edge list crosses PCIe as u32
+    latencies + exceptions (row starts, gaps), decoded on the device (k_decode_seq); a chunk with
+    more than 1/8 exceptions is re-narrowed to u16 endpoints, and the rest of the list with it.
+    Every variant gives the plain transfer's bytes (SRG_CODEC_SEQ=0: u16 endpoints throughout;
+    SRG_OPT_H2D_CODEC 0: plain)."""
+    V = 2100 if order == "shuffled_tail" else 1600  # 2.2 M edges (two chunks) / 1.28 M
+    g = synth.atlas_like(V, seed=41)
+    src, dst, lat, loss = g.src.copy(), g.dst.copy(), g.latency_ns.copy(), g.packet_loss.copy()
+    rng = np.random.default_rng(5)
+    if order == "rows_gaps":  # ~5 % of the pairs missing: gaps are exceptions, still sequential mode
+        keep = np.ones(len(src), dtype=bool)
+        keep[V:] = rng.random(len(src) - V) > 0.05
+        src, dst, lat, loss = src[keep], dst[keep], lat[keep], loss[keep]
+    elif order == "shuffled_tail":  # chunk 0 in rows, chunk 1 shuffled: the switch mid-list
+        head = 2 << 20
+        perm = np.r_[np.arange(head), head + rng.permutation(len(src) - head)]
+        src, dst, lat, loss = src[perm], dst[perm], lat[perm], loss[perm]
+    elif order == "shuffled":
+        perm = rng.permutation(len(src))
+        src, dst, lat, loss = src[perm], dst[perm], lat[perm], loss[perm]
+    e = Edges(V, src, dst, lat, loss, directed=False)
+    nodes = list(range(V))
+    monkeypatch.setenv("SRG_CODEC_SEQ", "1")
+    t = router.compute_shortest_paths(e, nodes)
+    monkeypatch.setenv("SRG_CODEC_SEQ", "0")
+    t16 = router.compute_shortest_paths(e, nodes)
+    monkeypatch.delenv("SRG_CODEC_SEQ")
+    router.set_option(N.SRG_OPT_H2D_CODEC, 0)
+    try:
+        t0 = router.compute_shortest_paths(e, nodes)
+    finally:
+        router.set_option(N.SRG_OPT_H2D_CODEC, 1)
+    for o in (t16, t0):
+        assert np.array_equal(t.latency_ns, o.latency_ns) and bits_equal(t.packet_loss, o.packet_loss)
+    rows = [0, 801, V - 1]
+    rl, rs = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
+    assert np.array_equal(t.latency_ns[rows], rl) and bits_equal(t.packet_loss[rows], rs)
+
+
 def test_h2d_codec_host_slow_fallback(router, monkeypatch):
     """The codec's mid-transfer switch to plain arrays (taken when narrowing a chunk on the host
     is slower than shipping it plain; forced here after the first chunk) gives the same bytes."""
