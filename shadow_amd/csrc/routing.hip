@@ -35,6 +35,7 @@
 
 #include "../../include/shadow_routing.h"
 #include "kernels.hip.h"
+#include "edge_codec.h"
 #include "tight_sparse.hip.h"
 #include "comm.h"
 #include "sparse.hip.h"
@@ -2387,36 +2388,8 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             if (seq_ch) {
                 std::vector<uint32_t>& ex = c.codec_ex[w];
                 ex.clear();
-                const size_t cap = 3 * ((z - a) / 8 + 1);
-                // the previous edge of the slice (none at a chunk's start: an exception)
-                uint32_t ps = a ? src[a - 1] : 0u, pd = a ? dst[a - 1] : 0u;
-                bool have = a > 0;
-                for (size_t i = a; i < z; ++i) {
-                    const uint32_t x = src[i], y = dst[i];
-                    const uint64_t l = lat[i];
-                    orx |= x | y;
-                    orl |= l;
-                    hl[i] = (uint32_t)l;
-                    if (!(have && x == ps && y == pd + 1u)) {
-                        ex.push_back((uint32_t)i);
-                        ex.push_back(x);
-                        ex.push_back(y);
-                        if (ex.size() > cap) {
-                            dense.store(true, std::memory_order_relaxed);  // (redone below with u16 endpoints)
-                            for (size_t k = i + 1; k < z; ++k) {  // finish the latencies and the checks
-                                const uint32_t x2 = src[k], y2 = dst[k];
-                                const uint64_t l2 = lat[k];
-                                orx |= x2 | y2;
-                                orl |= l2;
-                                hl[k] = (uint32_t)l2;
-                            }
-                            break;
-                        }
-                    }
-                    ps = x;
-                    pd = y;
-                    have = true;
-                }
+                if (!seq_encode_slice(src, dst, lat, hl, a, z, ex, 3 * ((z - a) / 8 + 1), orx, orl))
+                    dense.store(true, std::memory_order_relaxed);  // (redone below with u16 endpoints)
             } else {
                 for (size_t i = a; i < z; ++i) {
                     const uint32_t x = src[i], y = dst[i];
