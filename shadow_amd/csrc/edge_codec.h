@@ -15,37 +15,54 @@ namespace srg {
 // Encodes edges [a, z) of a chunk (pointers at the chunk's first edge): narrows the latencies into
 // hl, ORs endpoints / latencies into orx / orl (the caller's range checks) and appends exception
 // triples to ex.  Returns false ("dense") once ex would exceed cap entries; the latencies and the
-// checks still cover the whole slice then.
+// checks still cover the whole slice then.  Blocks of 1 K edges: a vectorisable narrowing loop,
+// a vectorisable exception-flag loop, then a scan of the flags 8 at a time (a branchy one-pass
+// loop ran the host conversion at 7-9.5 ms for C3 against 5-7 ms for the u16 narrowing).
 inline bool seq_encode_slice(const uint32_t* src, const uint32_t* dst, const uint64_t* lat, uint32_t* hl, size_t a,
                              size_t z, std::vector<uint32_t>& ex, size_t cap, uint32_t& orx, uint64_t& orl) {
-    uint32_t ps = a ? src[a - 1] : 0u, pd = a ? dst[a - 1] : 0u;  // none before a chunk's first edge
-    bool have = a > 0;
-    for (size_t i = a; i < z; ++i) {
-        const uint32_t x = src[i], y = dst[i];
-        const uint64_t l = lat[i];
-        orx |= x | y;
-        orl |= l;
-        hl[i] = (uint32_t)l;
-        if (!(have && x == ps && y == pd + 1u)) {
-            ex.push_back((uint32_t)i);
-            ex.push_back(x);
-            ex.push_back(y);
+    constexpr size_t BLK = 1024;
+    alignas(64) uint8_t fl[BLK + 8];
+    uint32_t ox = 0;
+    uint64_t ol = 0;
+    bool dense = false;
+    for (size_t b0 = a; b0 < z; b0 += BLK) {
+        const size_t b1 = b0 + BLK < z ? b0 + BLK : z, nb = b1 - b0;
+        for (size_t i = b0; i < b1; ++i) {
+            const uint64_t l = lat[i];
+            hl[i] = (uint32_t)l;
+            ol |= l;
+            ox |= src[i] | dst[i];
+        }
+        if (dense) continue;  // (latencies and checks only)
+        // edge i is an exception unless it follows (src, dst - 1); a chunk's first edge always is
+        size_t s0 = b0;
+        if (b0 == 0) {
+            fl[0] = 1;
+            s0 = 1;
+        }
+        for (size_t i = s0; i < b1; ++i)
+            fl[i - b0] = (uint8_t)((src[i] != src[i - 1]) | (dst[i] != dst[i - 1] + 1u));
+        for (size_t k = nb; k < nb + 8; ++k) fl[k] = 0;
+        for (size_t k = 0; k < nb; k += 8) {
+            uint64_t w;
+            __builtin_memcpy(&w, fl + k, 8);
+            if (!w) continue;
+            for (size_t q = k; q < k + 8 && q < nb; ++q) {
+                if (!fl[q]) continue;
+                const size_t i = b0 + q;
+                ex.push_back((uint32_t)i);
+                ex.push_back(src[i]);
+                ex.push_back(dst[i]);
+            }
             if (ex.size() > cap) {
-                for (size_t k = i + 1; k < z; ++k) {
-                    const uint32_t x2 = src[k], y2 = dst[k];
-                    const uint64_t l2 = lat[k];
-                    orx |= x2 | y2;
-                    orl |= l2;
-                    hl[k] = (uint32_t)l2;
-                }
-                return false;
+                dense = true;
+                break;
             }
         }
-        ps = x;
-        pd = y;
-        have = true;
     }
-    return true;
+    orx |= ox;
+    orl |= ol;
+    return !dense;
 }
 
 }  // namespace srg

@@ -2359,7 +2359,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     double t_conv = 0, t_wait = 0;
     const size_t nch = (A + CE - 1) / CE;
     const char* sq = std::getenv("SRG_CODEC_SEQ");
-    bool seq = A == E && sq && std::strcmp(sq, "1") == 0;  // (opt-in until measured on the GPU)
+    bool seq = A == E && !(sq && std::strcmp(sq, "0") == 0);
     uint32_t* dexc = seq ? (uint32_t*)c.b_exc.get(CE * 4) : nullptr;
     const int nwk = c.pool->size();
     if ((int)c.codec_ex.size() < nwk) c.codec_ex.resize(nwk);
