@@ -252,10 +252,9 @@ def apply_options(router, args):
         router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
     if args.fw_tile:
         router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
-    router.set_option(N.SRG_OPT_FW_PACKED, args.fw_packed)
     for flag, opt in (("sparse_group", "SPARSE_GROUP"), ("sparse_delta_all", "SPARSE_DELTA_ALL"),
                       ("sparse_delta_div", "SPARSE_DELTA_DIV"), ("fw_symmetric", "FW_SYMMETRIC"),
-                      ("chain_prio", "CHAIN_PRIO"), ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
+                      ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
                       ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
                       ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT")):
         v = getattr(args, flag)
@@ -268,7 +267,7 @@ def workload_key(args, V, seed, world):
     # collected on an earlier kernel (fw_product_sym) is not attached to it
     return (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "")
             + ("lb:" if args.graph != "ba" else "")
-            + f"packed{args.fw_packed}:tile{args.fw_tile or 128}:"
+            + f"packed2:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
             f"w{args.sparse_wgs or 2}"
             + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
@@ -304,8 +303,7 @@ def roofline_for(agg, kind, args, edges, V, wkey, sym):
     elif sym:
         kname = "fw_bulk_lb<128,16> (FW phase 3 over the stored tiles I <= J, operands from the pivot's line buffer, pair-packed)"
     elif kind == 0:
-        kname = ("fw_product<u32,128,16,2> (FW phase 3, pair-packed, non-lookahead tiles)" if args.fw_packed else
-                 "fw_product<u32,128,32,0> (FW phase 3, add + min3, non-lookahead tiles)")
+        kname = "fw_product<u32,128,16,2> (FW phase 3, pair-packed, non-lookahead tiles)"
     else:
         kname = "fw_product<u64,64,32,0> (FW phase 3)"
     r = {"bound": "valu", "kernel": kname, "achieved": round(achieved, 3),
@@ -314,7 +312,7 @@ def roofline_for(agg, kind, args, edges, V, wkey, sym):
          "avg_launch_ms": round(avg_ms, 4), "relaxations_per_launch": int(relax),
          "ops_per_relaxation": OPS_PER_RELAX.get(kind, 2.0), "relax_per_s": round(relax / (avg_ms * 1e-3), 1),
          "traffic_source": tsrc, "workload_key": wkey}
-    if kind == 0 and args.fw_packed:
+    if kind == 0:
         # v_min* issue at half rate on gfx950: the pair-packed relaxation pair (v_lshl_add_u64 +
         # v_min3_u32) measured 0.187 wave-instr/SIMD/cycle = 2 relaxations per 10.7 cycles per
         # wave = 0.748 of the 2-op lane peak (profiles/r01_valu_rate_microbench.txt)
@@ -436,7 +434,7 @@ def bench_multi(args):
     ms = elapsed * 1e3 / args.steps
     kind = s["path_kind"]
     ver = verify_rows(edges, h_lat, h_loss, V) if not args.no_verify else None
-    roof = roofline_for(agg, kind, args, edges, V, workload_key(args, V, seed, G), kind == 0 and args.fw_packed
+    roof = roofline_for(agg, kind, args, edges, V, workload_key(args, V, seed, G), kind == 0
                         and args.fw_symmetric != 0 and not edges.directed)
     emit(args, V, gdesc, edges, kind, G, G and V * args.steps / elapsed, ms, agg, s, roof, None,
          {"parallelism": f"multi{G} (one process, srg_multi: in-process group, pull collectives over xGMI)",
@@ -498,7 +496,6 @@ def main():
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
     ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
-    ap.add_argument("--chain-prio", type=int, default=None, help="dense: 0 = FW chain kernels at normal wave priority")
     ap.add_argument("--d2h-mode", type=int, default=None, help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync")
     ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")
     ap.add_argument("--late-loss", type=int, default=None,
@@ -512,7 +509,6 @@ def main():
                     help="symmetric FW: sub-tiles per dimension of the chain's line launches (1/2/4; 0 = auto)")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
-    ap.add_argument("--fw-packed", type=int, default=2, help="u32 FW tile variant (SRG_OPT_FW_PACKED): 2 = packed pairs; 0 = add + min3")
     ap.add_argument("--simulate-rank", type=str, default=None,
                     help="TIMING AID 'G:r': run rank r's share of a G-rank build alone, collectives elided "
                          "(outputs invalid; prints a diagnostic line, never the bench result)")
@@ -648,7 +644,7 @@ def main():
         dev_ms = (time.perf_counter() - t1) * 1e3 / 2
         del ol, os_
     wkey = workload_key(args, V, seed, world)
-    sym = ((kind == 0 and args.fw_packed) or kind == 1) and args.fw_symmetric != 0 and not edges.directed
+    sym = kind in (0, 1) and args.fw_symmetric != 0 and not edges.directed
     roofline = roofline_for(agg, kind, args, edges, V, wkey, sym)
 
     if args.simulate_rank:

@@ -139,9 +139,8 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_SIMULATE_RANK 6   /* TIMING AID ONLY: value = nranks*1000 + rank runs this rank's share
                                      with every collective elided -- outputs are NOT valid; 0 detaches */
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
-#define SRG_OPT_FW_PACKED 8       /* dense u32 FW tiles (directed graphs / multi-rank): 2 (default) = two
-                                     relaxations per 64-bit add of packed key pairs + v_min3, 16-deep k-chunks;
-                                     0 = one add per relaxation */
+/* 8 (SRG_OPT_FW_PACKED) and 18 (SRG_OPT_CHAIN_PRIO) were A/B switches, removed in round 4: the u32 FW
+ * always runs the pair-packed tile and the chain kernels always raise their priority. */
 #define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) / 16 (one workgroup per CU) */
 #define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
@@ -153,7 +152,6 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_FW_SYMMETRIC 17     /* dense: 1 (default) = for an undirected graph, update only the FW tiles
                                        I <= J (D stays symmetric; u32 keys on 128-tiles, u64 keys on 64-tiles,
                                        one rank or many) and mirror at the end; 0 = the general FW */
-#define SRG_OPT_CHAIN_PRIO 18       /* dense: 1 (default) = the FW lookahead chain kernels raise their wave priority */
 #define SRG_OPT_D2H_MODE 20         /* host entry: how finished rows are shipped into the page-locked caller
                                      * arrays while kernels run: 1 (default) = an SDMA engine, 0 =
                                      * hipMemcpyAsync (a full-chip blit kernel: slows the overlapped kernels) */

@@ -101,6 +101,8 @@ struct Flags {
     uint32_t unreachable_used_pair;
     uint32_t bad_node;
     unsigned long long first_bad;  // direct paths: first (i*n+j) with edge count != 1
+    uint32_t wrap;                 // k_wrap_edges: a relaxation the reference would run wraps u64
+    uint32_t wrap_inf;             // k_wrap_edges: a relaxation from a vertex left at INF (unknown distance)
 };
 
 constexpr int kThreads = 256;
@@ -396,6 +398,42 @@ __global__ void k_loss_round(const uint32_t* __restrict__ PRED, const K* __restr
     if (changed) atomicOr(&flags->changed, 1u);
 }
 
+// Wrap check (graphs whose max edge latency x V reaches 2^64 ns only).  The reference
+// sums u64 latencies with wrapping arithmetic (mod.rs:327, release build): its Dijkstra from s
+// relaxes every edge (u, t) of a visited u towards a not-yet-visited t, i.e. with D[s][t] >= D[s][u]
+// (ties either way), and a sum D[s][u] + w >= 2^64 ns wraps and corrupts its result.  This kernel
+// flags such a relaxation for the local source rows (grid = (edge blocks, rows)): D is in latency
+// units (outputs are D * unit), w in ns.  A relaxation from a vertex whose key is INF can only be
+// judged when INF means unreachable; `inf_known` = 0 flags it instead (the caller reruns on wider
+// keys or reports the range).
+template <class K>
+__global__ void __launch_bounds__(256) k_wrap_edges(uint64_t E, const uint32_t* __restrict__ src,
+                                                    const uint32_t* __restrict__ dst, const uint64_t* __restrict__ lat,
+                                                    int directed, const K* __restrict__ D, size_t ld,
+                                                    const uint32_t* __restrict__ rows, uint64_t unit, int inf_known,
+                                                    Flags* flags) {
+    const K* Ds = D + (size_t)rows[blockIdx.y] * ld;
+    uint32_t wrap = 0, winf = 0;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[e], t = dst[e];
+        if (s == t) continue;
+        const uint64_t w = lat[e];
+        for (int dir = 0; dir < (directed ? 1 : 2); ++dir) {
+            const uint32_t u = dir ? t : s, v = dir ? s : t;
+            const K du = Ds[u], dv = Ds[v];
+            if (du == KeyOps<K>::INF) {
+                winf |= !inf_known;  // unknown distance: the relaxation may or may not wrap
+                continue;
+            }
+            if (dv < du) continue;  // v was visited before u: Dijkstra skips the edge
+            const unsigned __int128 sum = (unsigned __int128)du * unit + w;
+            wrap |= (uint32_t)(sum >> 64) != 0;
+        }
+    }
+    if (__ballot(wrap) && (threadIdx.x & 63) == 0) atomicOr(&flags->wrap, 1u);
+    if (__ballot(winf) && (threadIdx.x & 63) == 0) atomicOr(&flags->wrap_inf, 1u);
+}
+
 __global__ void __launch_bounds__(256) k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uint32_t V,
                                                      size_t ld, unsigned long long* out) {
     const uint32_t* row = PRED + (size_t)blockIdx.x * ld;
@@ -626,8 +664,6 @@ struct srg_ctx {
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
     int fw_tile = 0;                 // 0 = auto, 64 or 128
-    int fw_packed = 2;               // u32 FW tile variant (kernels.hip.h pk_kc): 0 add + min3, 2 pair-packed
-    int chain_prio = 1;              // FW lookahead chain kernels at raised wave priority (SRG_OPT_CHAIN_PRIO)
     bool fw_symmetric = true;        // undirected + one rank: FW over the tiles I <= J only (SRG_OPT_FW_SYMMETRIC)
     int d2h_mode = 1;                // host entry D2H: 1 = SDMA engine, 0 = hipMemcpyAsync (SRG_OPT_D2H_MODE)
     DevBuf b_DST2;                   // low words of the u64-key DST (the scan input)
@@ -808,6 +844,8 @@ struct Prelude {
     std::vector<uint32_t> nodes_h;  // host copy of `nodes` (partitioning, error text)
     bool range_risk = false;         // max_key * (V-1) >= 2^62: an INF used pair on the u64 keys may be a
                                      // path >= 2^62 units (SRG_ERR_LATENCY_RANGE), not an unreachable one
+    bool wrap_risk = false;          // max_lat * V >= 2^64 ns: a relaxation of the reference may wrap u64
+                                     // (checked after FW by k_wrap_edges; the sparse path is not taken)
     uint64_t unit = 1;               // latency unit in ns: keys = latency / unit (compute_device)
     unsigned long long max_key = 0;  // max_lat / unit
 };
@@ -1038,11 +1076,31 @@ std::map<int, int> g_dev_ctx;
 // (in-process rank groups: two waits could each block the queue holding the other's write), nor
 // under a profiler that serialises dispatches (rocprofv3 --pmc hung on it): those use events
 // (and SRG_STREAM_HOPS=events forces them).
+// The value form is a pair of one-wave kernels of our own instead of hipStreamWriteValue32 /
+// hipStreamWaitValue32 (the same mechanism: the runtime's wait is a polling blit kernel too), so
+// that the wait is bounded: past ~2 s it raises the FW timeout word and returns, and the host
+// reports SRG_ERR_HIP after FW instead of hanging on a mis-ordered enqueue.
+__global__ void k_hop_set(uint32_t* sig, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(sig, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_hop_wait(const uint32_t* sig, uint32_t v, uint32_t* timeout) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = wall_clock64();  // 100 MHz
+    while (__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - v > 0x7FFFFFFFu) {  // sig < v (mod 2^32)
+        if (wall_clock64() - t0 > 200000000ull || __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 void stream_hop(srg_ctx& c, int i, hipStream_t from, hipStream_t to, hipEvent_t ev) {
-    if (c.hop_values && c.sig[i]) {
+    if (c.hop_values && c.sig[i] && c.fw_timeout) {
         const uint32_t v = ++c.sig_val[i];
-        HIP_CHECK(hipStreamWriteValue32(from, c.sig[i], v, 0));
-        HIP_CHECK(hipStreamWaitValue32(to, c.sig[i], v, hipStreamWaitValueGte, 0xFFFFFFFFu));
+        k_hop_set<<<1, 64, 0, from>>>(c.sig[i], v);
+        k_hop_wait<<<1, 64, 0, to>>>(c.sig[i], v, c.fw_timeout);
+        HIP_CHECK(hipGetLastError());
         return;
     }
     HIP_CHECK(hipEventRecord(ev, from));
@@ -1090,6 +1148,10 @@ Plan make_plan(int G, int g, uint32_t V, int T, const std::vector<uint32_t>& nod
     }
     return p;
 }
+
+// FW lookahead chain kernels raise their wave priority (s_setprio 3) beside the bulk tiles: C3 FW
+// 24.1 -> 23.5 ms (profiles/r02/prio; the option that turned it off was A/B only and is gone)
+constexpr int kChainPrio = 1;
 
 #ifndef SRG_FW_KC
 #define SRG_FW_KC 32
@@ -1180,7 +1242,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
     const int r0 = pl.rb0, r1 = pl.rb1;
     // pivot 0
     if (pl.own(0)) {
-        fw_phase1<K, T><<<1, 512, 0, st>>>(D, Vp, 0, c.chain_prio);
+        fw_phase1<K, T><<<1, 512, 0, st>>>(D, Vp, 0, kChainPrio);
         fw_tiles<K, T, PK>(D, Vp, 0, 0, 1, {}, 0, nb, {0}, lds, st, pl.G > 1);
     }
     if (multi) {
@@ -1207,7 +1269,7 @@ void fw_blocked(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uin
         fw_tiles_pair<K, T, PK>(D, Vp, kb, rowr, make_rect(r0, r1, {kb, k1}, k1, k1 + 1, {}), lds, aux, sk);
         const Rect colp = make_rect(r0, r1, {k1}, k1, k1 + 1, {});  // own column panel of k1
         if (pl.own(k1)) {
-            fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1, c.chain_prio);
+            fw_phase1<K, T><<<1, 512, 0, aux>>>(D, Vp, k1, kChainPrio);
             // the column panel of k1 rewrites tile (kb, k1) of panel kb: its broadcast (still the
             // last one recorded in ev_c) must have left first
             if (multi) HIP_CHECK(hipStreamWaitEvent(aux, c.ev_c, 0));
@@ -1295,11 +1357,11 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
     auto line = [&](K* lbL, int L, K* lbK, int K1, int mode, int tiles, hipStream_t s) {
         if (!tiles) return;
         if (split == 4)
-            fw_line_lb<K, T, 4><<<dim3(tiles, 16), 256, lb_lds<K, T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+            fw_line_lb<K, T, 4><<<dim3(tiles, 16), 256, lb_lds<K, T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, kChainPrio);
         else if (split == 2)
-            fw_line_lb<K, T, 2><<<dim3(tiles, 4), 256, lb_lds<K, T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+            fw_line_lb<K, T, 2><<<dim3(tiles, 4), 256, lb_lds<K, T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, kChainPrio);
         else
-            fw_line_lb<K, T, 1><<<dim3(tiles, 1), 256, lb_lds<K, T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, c.chain_prio);
+            fw_line_lb<K, T, 1><<<dim3(tiles, 1), 256, lb_lds<K, T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, kChainPrio);
     };
     const bool prof = c.profiling && nb > 2;
     if (prof) {
@@ -1335,7 +1397,7 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
     int* tiles = (int*)c.b_tiles.get(std::max<size_t>(own_h.size(), 1) * 4);
     if (ntile) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
     hipStream_t aux = c.aux_stream, cs = c.comm_stream;
-    const int prio = c.chain_prio;
+    const int prio = kChainPrio;
     auto close_pivot = [&](K* lbk, int k, hipStream_t s) {
         fw_close_sq<K, T><<<dim3(T / 16, T / 16), 256, 0, s>>>(lbk + (size_t)lm.slot(k, k) * TT, cflags + 16 * k,
                                                              c.fw_timeout, prio);
@@ -1434,7 +1496,7 @@ void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t
 // the symmetric FW over line buffers applies: undirected, u32 pair-packed 128-tiles or u64 64-tiles
 template <class K, int T>
 bool sym_fw_for(const srg_ctx& c, const DevGraph& g) {
-    return ((sizeof(K) == 4 && T == 128 && c.fw_packed != 0) || (sizeof(K) == 8 && T == 64)) && c.fw_symmetric &&
+    return ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64)) && c.fw_symmetric &&
            !g.directed;
 }
 
@@ -1493,19 +1555,20 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64))
             fw_line_sym<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx);
     } else {
-        if constexpr (sizeof(K) == 4) {
-            if (c.fw_packed) fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n);
-            else fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
-        } else {
-            fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
-        }
+        // u32 keys: the pair-packed tile (two relaxations per 64-bit add + v_min3); the add + min3
+        // tile (PK = 0) ran the same C3 launch in 0.304 instead of 0.242 ms (profiles/r02c/fw_fold.txt)
+        // and is kept for u64 keys only
+        if constexpr (sizeof(K) == 4) fw_blocked<K, T, 2>(c, pl, D, Vp, st, prof_relax, prof_n);
+        else fw_blocked<K, T, 0>(c, pl, D, Vp, st, prof_relax, prof_n);
         if (multi) gather_rows<K>(c, pl, D, Vp, T, st, ms_dx);
     }
     HIP_CHECK(hipGetLastError());
     if (sym_fw_for<K, T>(c, g)) rb_async(c, MS_TIMEOUT, c.fw_timeout, st);  // read after FW, on its stream
     const double ms_fw = tm.lap();
     if (sym_fw_for<K, T>(c, g) && rb_get<uint32_t>(c, MS_TIMEOUT))
-        fail(SRG_ERR_HIP, "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
+        fail(SRG_ERR_HIP, rb_get<uint32_t>(c, MS_TIMEOUT) == 2
+                              ? "FW chain: a cross-stream hop waited more than 2 s (mis-ordered enqueue)"
+                              : "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
     if (wl_late) {
         // WL = min loss among the min-latency parallel edges (what k_w_split gives), from the
         // losses that crossed PCIe during FW.  Built here, after FW, rather than beside it: on a
@@ -1592,6 +1655,33 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         fail(SRG_ERR_UNREACHABLE,
              "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
              "from another used node)");
+    }
+    if (P.wrap_risk) {
+        // max edge latency x V reaches 2^64 ns: check that no relaxation the reference runs wraps
+        // its u64 sum (k_wrap_edges), and that outputs D * unit fit u64 (they are below such a sum)
+        const unsigned __int128 bound = (unsigned __int128)P.max_key * (V > 1 ? V - 1 : 1);
+        const bool inf_known = sizeof(K) == 4 ? bound < KeyOps<uint32_t>::INF : !P.range_risk;
+        HIP_CHECK(hipMemsetAsync(&P.flags->wrap, 0, 8, st));
+        for (uint32_t r0 = 0; r0 < nloc && g.E; r0 += 32768) {
+            const uint32_t nr = std::min<uint32_t>(32768, nloc - r0);
+            k_wrap_edges<K><<<dim3(grid_for(g.E, 64), nr), 256, 0, st>>>(g.E, g.src, g.dst, g.lat, g.directed, D, Vp,
+                                                                        lnodes + r0, P.unit, inf_known ? 1 : 0, P.flags);
+        }
+        HIP_CHECK(hipGetLastError());
+        const uint32_t wrapped = reduce_flag(&P.flags->wrap);
+        if (wrapped)
+            fail(SRG_ERR_LATENCY_RANGE, "a shortest-path relaxation sums past 2^64 ns (max edge latency " +
+                                            std::to_string(P.es.max_lat) +
+                                            " ns): the reference's u64 latency sum would wrap (mod.rs:327)");
+        if (reduce_flag(&P.flags->wrap_inf)) {
+            if (sizeof(K) == 4) {  // a vertex past the u32 keys: decide on the u64 keys
+                if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));
+                return false;
+            }
+            fail(SRG_ERR_LATENCY_RANGE, "a vertex has no path below 2^62 latency units on a graph whose u64 latency "
+                                        "sums can wrap (max edge latency " +
+                                            std::to_string(P.es.max_lat) + " ns)");
+        }
     }
 
     // latency outputs (+ diagonal self-loops) of the own rows, right after FW
@@ -2115,8 +2205,11 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     if (stats) stats->latency_unit_ns = P.unit;
     const unsigned __int128 bound = (unsigned __int128)P.max_key * (g.V > 1 ? g.V - 1 : 1);
     P.range_risk = bound >= ((unsigned __int128)1 << 62);
+    // every shortest path is at most max_lat * (V - 1) ns and every relaxation the reference runs
+    // at most max_lat * V: below 2^64 nothing wraps, and outputs D * unit fit u64
+    P.wrap_risk = (unsigned __int128)P.es.max_lat * g.V >= ((unsigned __int128)1 << 64);
     const int G = c.comm ? c.comm->nranks : 1, rk = c.comm ? c.comm->rank : 0;
-    if (choose_sparse(c, g) && P.max_key < 0xFFFFFFFFull) {
+    if (choose_sparse(c, g) && P.max_key < 0xFFFFFFFFull && !P.wrap_risk) {
         loss_arrive(g, P.selfloss, st);
         if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
     }
@@ -2354,7 +2447,8 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     dg.dst = (uint32_t*)c.b_dst.get(E * 4);
     dg.lat = (uint64_t*)c.b_lat.get(E * 8);
     dg.loss = (float*)c.b_loss.get(E * 4);
-    std::atomic<bool> bad{false};
+    std::atomic<bool> bad{false};     // a latency >= 2^32: the codec cannot carry the list
+    std::atomic<bool> bad_ep{false};  // an endpoint >= 65536: only the sequential-pair chunks can
     const bool dbg = std::getenv("SRG_DEBUG_CODEC") != nullptr;
     double t_conv = 0, t_wait = 0;
     const size_t nch = (A + CE - 1) / CE;
@@ -2402,8 +2496,12 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
                 }
             }
             if (with_loss) std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
-            if ((orx >> 16) || (orl >> 32)) bad.store(true, std::memory_order_relaxed);
+            if (orl >> 32) bad.store(true, std::memory_order_relaxed);
+            if (orx >> 16) bad_ep.store(true, std::memory_order_relaxed);
         });
+        // sequential-pair chunks never carry u16 endpoints (exceptions are u32): only the u16
+        // narrowing needs every endpoint below 65536
+        if (seq_ch && dense.load() && bad_ep.load()) bad.store(true);
         if (seq_ch && dense.load() && !bad.load()) {
             // not a row-ordered list: this chunk's endpoints narrowed after all, u16 from here on
             seq = false;
@@ -2416,6 +2514,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             });
         }
         const bool chunk_seq = seq_ch && !dense.load();
+        if (!chunk_seq && bad_ep.load()) bad.store(true);
         const double dt = ms_since(tc);
         t_conv += dt;
         if (bad.load()) {
@@ -2627,7 +2726,9 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // the W build and FW (dense u32 path: WL is built from them on c->loss_stream)
         const bool want_late = c->late_loss && !direct && !shard;
         bool all_narrow = false;
-        const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) && g->num_vertices <= 65536 &&
+        // (V > 65536: only a row-ordered list, through the sequential-pair chunks, can be narrowed)
+        const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) &&
+                           (g->num_vertices <= 65536 || a1 - a0 == E) &&
                            codec_in(*c, g, dg, st, a0, a1, !want_late, all_narrow);
         LateLoss late;
         late.ls = c->loss_stream;
@@ -2879,10 +2980,6 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SPARSE_LOCALITY:
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
-        case SRG_OPT_FW_PACKED:
-            if (value != 0 && value != 2) return SRG_ERR_ARG;
-            ctx->fw_packed = (int)value;
-            return SRG_OK;
         case SRG_OPT_SPARSE_GROUP:
             if (value != 4 && value != 8 && value != 16) return SRG_ERR_ARG;  // 16: one workgroup per CU only
             ctx->sparse_group = (int)value;
@@ -2903,9 +3000,6 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             return SRG_OK;
         case SRG_OPT_FW_SYMMETRIC:
             ctx->fw_symmetric = value != 0.0;
-            return SRG_OK;
-        case SRG_OPT_CHAIN_PRIO:
-            ctx->chain_prio = value != 0.0 ? 1 : 0;
             return SRG_OK;
         case SRG_OPT_LATE_LOSS:
             if (value != 0 && value != 1) return SRG_ERR_ARG;
@@ -2954,14 +3048,12 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_ALGORITHM: *value = ctx->algorithm; break;
         case SRG_OPT_SPARSE_LOCALITY: *value = ctx->sparse_locality; break;
         case SRG_OPT_FW_TILE: *value = ctx->fw_tile; break;
-        case SRG_OPT_FW_PACKED: *value = ctx->fw_packed; break;
         case SRG_OPT_SPARSE_GROUP: *value = ctx->sparse_group; break;
         case SRG_OPT_SPARSE_WGS_PER_CU: *value = ctx->sparse_wgs_per_cu; break;
         case SRG_OPT_SPARSE_DELTA_DIV: *value = ctx->sparse_delta_div; break;
         case SRG_OPT_SPARSE_DELTA_ALL: *value = ctx->sparse_delta_all; break;
         case SRG_OPT_SPARSE_GLOBAL_BITMAPS: *value = ctx->sparse_global_bitmaps; break;
         case SRG_OPT_FW_SYMMETRIC: *value = ctx->fw_symmetric; break;
-        case SRG_OPT_CHAIN_PRIO: *value = ctx->chain_prio; break;
         case SRG_OPT_D2H_MODE: *value = ctx->d2h_mode; break;
         case SRG_OPT_LOSS_CHUNKS: *value = ctx->loss_chunks; break;
         case SRG_OPT_SCAN_GROUPS: *value = ctx->scan_groups; break;
@@ -3124,9 +3216,17 @@ int srg_multi_size(const srg_multi* m) { return m ? (int)m->ranks.size() : 0; }
 int srg_multi_set_option(srg_multi* m, int option, double value) {
     if (!m) return SRG_ERR_ARG;
     if (option == SRG_OPT_GATHER_OUTPUT || option == SRG_OPT_SIMULATE_RANK) return SRG_ERR_ARG;  // fixed by srg_multi
-    for (srg_ctx* c : m->ranks) {
-        const int rc = srg_set_option(c, option, value);
-        if (rc != SRG_OK) return rc;
+    // all or nothing: the ranks must keep one option set (a split FW tile or line split would run
+    // mismatched multi-rank schedules), so a rank that rejects the value rolls the others back
+    std::vector<double> old(m->ranks.size(), 0.0);
+    for (size_t r = 0; r < m->ranks.size(); ++r)
+        if (srg_get_option(m->ranks[r], option, &old[r]) != SRG_OK) return SRG_ERR_ARG;
+    for (size_t r = 0; r < m->ranks.size(); ++r) {
+        const int rc = srg_set_option(m->ranks[r], option, value);
+        if (rc != SRG_OK) {
+            for (size_t q = 0; q < r; ++q) (void)srg_set_option(m->ranks[q], option, old[q]);
+            return rc;
+        }
     }
     return SRG_OK;
 }

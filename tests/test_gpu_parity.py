@@ -91,15 +91,14 @@ def test_random_vs_oracle(scan_router, kw):
     assert_parity(tab, lat, loss)
 
 
-@pytest.mark.parametrize("packed", [0, 2])
 @pytest.mark.parametrize("kw", [dict(V=300, density=0.1, seed=111, lat_hi=40, parallel=0.1),
                                 dict(V=390, density=0.2, seed=112, directed=True, lat_lo=10**6, lat_hi=10**8)],
                          ids=["ties", "directed_wide"])
-def test_fw_kernels_match_oracle(router, packed, kw):
-    """Both u32 FW tile kernels (pair-packed 64-bit adds and add + min3) are bit-exact; V not a
-    multiple of the 128 tile exercises the padding."""
+def test_fw_kernels_match_oracle(router, kw):
+    """The u32 FW tile kernels (pair-packed 64-bit adds; general FW on the directed graph, the
+    symmetric line-buffer FW on the undirected one) are bit-exact; V not a multiple of the 128 tile
+    exercises the padding."""
     r = Router(0)
-    r.set_option(N.SRG_OPT_FW_PACKED, packed)
     kw = dict(kw)
     V, dens, seed = kw.pop("V"), kw.pop("density"), kw.pop("seed")
     g = synth.random_graph(V, dens, seed, **kw)
@@ -306,6 +305,42 @@ def test_u64_edge_past_key_range_is_an_error(router, monkeypatch):
     with pytest.raises(NetGraphError) as ei:
         router.compute_shortest_paths(e, [0, 1])
     assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
+
+
+def test_latency_unit_wrap_is_an_error(router):
+    """with a latency unit the keys are small, but the outputs are key x unit ns.  Where
+    a relaxation the reference's Dijkstra runs sums past 2^64 ns its release-build u64 `+` wraps
+    (mod.rs:327) and its result is garbage; the library reports SRG_ERR_LATENCY_RANGE instead of a
+    silently wrong table (k_wrap_edges).  Multi-hop paths with a unit >= 2^32 that stay below 2^64
+    come out exact."""
+    # 5-node path of 2^62-ns links: unit 2^62, key 1 per link; 0 -> 4 is 4 units = 2^64 ns
+    p = Edges(5, list(range(5)) + [0, 1, 2, 3], list(range(5)) + [1, 2, 3, 4],
+              np.array([1] * 5 + [2 ** 62] * 4, dtype=np.uint64), [0.0] * 9, False)
+    with pytest.raises(NetGraphError) as ei:
+        router.compute_shortest_paths(p, list(range(5)))
+    assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
+    # ADVICE's triangle {2^63, 2^63, 3 * 2^62}: 2^63 + 2^63 wraps to 0 in the reference
+    tri = Edges(3, [0, 1, 2, 0, 1, 0], [0, 1, 2, 1, 2, 2],
+                np.array([1, 1, 1, 2 ** 63, 2 ** 63, 3 * 2 ** 62], dtype=np.uint64), [0.0] * 6, False)
+    with pytest.raises(NetGraphError) as ei:
+        router.compute_shortest_paths(tri, [0, 1, 2])
+    assert ei.value.code == N.SRG_ERR_LATENCY_RANGE
+    # unit 2^40 (>= 2^32), 3-hop shortest paths beside a long direct link: exact, u32 keys
+    q = Edges(4, [0, 1, 2, 3, 0, 1, 2, 0], [0, 1, 2, 3, 1, 2, 3, 3],
+              np.array([7, 7, 7, 7, 2 ** 40, 2 ** 40, 2 ** 41, 2 ** 43], dtype=np.uint64),
+              np.array([0, 0, 0, 0, 0.01, 0.02, 0.0, 0.0], dtype=np.float32), False)
+    t = router.compute_shortest_paths(q, [0, 1, 2, 3])
+    assert t.stats["latency_unit_ns"] == 2 ** 40 and t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
+    assert t[(0, 3)].latency_ns == 2 ** 40 * 4
+    lat, loss = oracle.compute_shortest_paths(q.as_tuple(), [0, 1, 2, 3])
+    assert_parity(t, lat, loss)
+    # a wrap-risk graph (max latency x V >= 2^64) whose relaxations all stay below 2^64: exact
+    w = Edges(4, [0, 1, 2, 3, 0, 1, 2], [0, 1, 2, 3, 1, 2, 3],
+              np.array([5, 5, 5, 5, 2 ** 61, 2 ** 61, 2 ** 62], dtype=np.uint64), [0.0] * 7, False)
+    t = router.compute_shortest_paths(w, [0, 1, 2, 3])
+    lat, loss = oracle.compute_shortest_paths(w.as_tuple(), [0, 1, 2, 3])
+    assert t[(0, 3)].latency_ns == 2 ** 63
+    assert_parity(t, lat, loss)
 
 
 def test_deterministic_bytes(router):
