@@ -256,7 +256,8 @@ def apply_options(router, args):
                       ("sparse_delta_div", "SPARSE_DELTA_DIV"), ("fw_symmetric", "FW_SYMMETRIC"),
                       ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
                       ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
-                      ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT")):
+                      ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT"),
+                      ("fw_step", "FW_STEP")):
         v = getattr(args, flag)
         if v is not None:
             router.set_option(getattr(N, "SRG_OPT_" + opt), v)
@@ -507,6 +508,9 @@ def main():
     ap.add_argument("--loss-chunks", type=int, default=None, help="dense: k_loss_rows launches (0 = auto)")
     ap.add_argument("--fw-line-split", type=int, default=None,
                     help="symmetric FW: sub-tiles per dimension of the chain's line launches (1/2/4; 0 = auto)")
+    ap.add_argument("--fw-step", type=int, default=None,
+                    help="symmetric FW: 1 = one fused launch per pivot (chain + bulk, in-launch line exchange), "
+                         "0 = two-stream schedule, -1 = auto")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--simulate-rank", type=str, default=None,

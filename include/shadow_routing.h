@@ -174,6 +174,13 @@ void srg_destroy(srg_ctx* ctx);
                                      * launches, 1 (whole 128-tiles) / 2 / 4; 0 (default) = by the bulk a
                                      * pivot leaves this rank: >= 2048 tiles 1, >= 1024 tiles 2, else 4
                                      * (C3: 1 on one rank, 2 on two, 4 on more; C1/C2: 4) */
+#define SRG_OPT_FW_STEP 32           /* symmetric FW schedule: 1 = one fused launch per pivot (the next pivot's
+                                     * chain on the launch's first workgroups, its line exchange between ranks
+                                     * inside the launch: stores into the peers' line buffers + arrival flags);
+                                     * 0 = the bulk and the chain on two streams, the exchange a collective;
+                                     * -1 (default) = fused for simulated ranks and for in-process ranks on
+                                     * distinct devices (ranks sharing a GPU set 1 only when each rank's launch
+                                     * has a hardware queue of its own) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

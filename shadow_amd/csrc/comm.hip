@@ -159,6 +159,8 @@ struct LocalGroup {
         int device = 0;
         hipEvent_t ev_arrive = nullptr, ev_done = nullptr;
         std::vector<uint32_t> host;  // allreduce staging
+        void* xlb = nullptr;         // share_ptrs: line-buffer block, arrival flags
+        uint32_t* xflags = nullptr;
     };
     std::vector<Slot> slots;
     bool aborted = false;  // a rank failed outside the collective protocol: release the others
@@ -309,6 +311,27 @@ struct LocalComm final : Comm {
         launch_pull(batches, s);
         depart(s);
     }
+    int device_exchange() const override { return 2; }
+    bool distinct_devices() const override {
+        std::lock_guard<std::mutex> lk(g->mu);
+        for (int p = 0; p < g->n; ++p)
+            for (int q = p + 1; q < g->n; ++q)
+                if (g->slots[p].device == g->slots[q].device) return false;
+        return true;
+    }
+    void share_ptrs(void* lb, uint32_t* flags, void** lbs, uint32_t** fl, bool* sys) override {
+        g->slots[rank].xlb = lb;
+        g->slots[rank].xflags = flags;
+        g->barrier();
+        bool other = false;
+        for (int p = 0; p < nranks; ++p) {
+            lbs[p] = g->slots[p].xlb;
+            fl[p] = g->slots[p].xflags;
+            other |= g->slots[p].device != device;
+        }
+        *sys = other;
+        g->barrier();  // every rank has read every slot
+    }
     void allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t s) override {
         if (nranks == 1 || !count) return;
         auto& me = g->slots[rank];
@@ -342,7 +365,12 @@ __global__ void k_spin_ns(unsigned long long ns) {
 
 struct ModelComm final : Comm {
     double lat_ns = 15000.0, gbps = 64.0;
+    double flag_ns = 3000.0;  // device-side exchange: a peer's flag over xGMI (SRG_SIM_FLAG_US)
     const char* kind() const override { return "simulated"; }
+    int device_exchange() const override { return 1; }
+    // the device-side line exchange inside the fused FW launch: every peer's segment arrives over
+    // its own link (peers store while they compute, so this is a bound), then its flag
+    double model_xchg_ns(size_t max_seg_bytes) const override { return flag_ns + max_seg_bytes / gbps; }
     void wait(double ns, hipStream_t s) {
         if (ns <= 0) return;
         k_spin_ns<<<1, 64, 0, s>>>((unsigned long long)ns);
@@ -370,10 +398,12 @@ Comm* null_create(int nranks, int rank) {
     c->rank = rank;
     if (const char* e = std::getenv("SRG_SIM_COLL_US")) c->lat_ns = std::atof(e) * 1e3;
     if (const char* e = std::getenv("SRG_SIM_LINK_GBPS")) c->gbps = std::atof(e);
+    if (const char* e = std::getenv("SRG_SIM_FLAG_US")) c->flag_ns = std::atof(e) * 1e3;
     return c;
 }
 
 LocalGroup* local_group_create(int nranks) { return new LocalGroup(nranks); }
+
 
 void local_group_release(LocalGroup* g) {
     if (g && g->refs.fetch_sub(1) == 1) delete g;

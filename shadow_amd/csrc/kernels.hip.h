@@ -635,10 +635,12 @@ __device__ __forceinline__ void sym_store(const SymOp<T, KC>& o, u64p* __restric
 // B through LDS before C is stored; in-place line updates where A or B overlaps C across
 // workgroups read old or new values of C's row, and both give the same result once the pivot
 // is closed (min over k of C'[x][k] + P[k][y] = min over k of C[x][k] + P[k][y] for P closed).
-template <int TM, int TK, int KC>
-__device__ __forceinline__ void fw_core_lb(uint32_t* __restrict__ C, size_t ldc, const uint32_t* __restrict__ Ab,
-                                           bool acol, const uint32_t* __restrict__ Bb, bool bcol, size_t ldab,
-                                           uint32_t* __restrict__ C2, size_t ldc2) {
+// Epilogue functor epi(r, c, bits): the product's result, 8 bytes at element (r, c) of the tile (two
+// u32 keys (r, c), (r, c + 1) here; one u64 key in fw_core_lb64), for destinations beyond C.
+template <int TM, int TK, int KC, class Epi>
+__device__ __forceinline__ void fw_core_lb_e(uint32_t* __restrict__ C, size_t ldc, const uint32_t* __restrict__ Ab,
+                                             bool acol, const uint32_t* __restrict__ Bb, bool bcol, size_t ldab,
+                                             Epi&& epi) {
     using S = SymOp<TM, KC>;
     constexpr int M = TM / 16;
     constexpr int LDA = TM + 2;
@@ -705,8 +707,17 @@ __device__ __forceinline__ void fw_core_lb(uint32_t* __restrict__ C, size_t ldc,
             v.v[0] = c[a][2 * g];
             v.v[1] = c[a][2 * g + 1];
             stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ldc + 32 * g + 2 * tx, v);
-            if (C2) stv<uint32_t, 2>(C2 + (size_t)pk_rc(ty, a) * ldc2 + 32 * g + 2 * tx, v);
+            epi(pk_rc(ty, a), 32 * g + 2 * tx, (uint64_t)v.v[0] | ((uint64_t)v.v[1] << 32));
         }
+}
+
+template <int TM, int TK, int KC>
+__device__ __forceinline__ void fw_core_lb(uint32_t* __restrict__ C, size_t ldc, const uint32_t* __restrict__ Ab,
+                                           bool acol, const uint32_t* __restrict__ Bb, bool bcol, size_t ldab,
+                                           uint32_t* __restrict__ C2, size_t ldc2) {
+    fw_core_lb_e<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, [&](int r, int cc, uint64_t bits) {
+        if (C2) *reinterpret_cast<uint64_t*>(C2 + (size_t)r * ldc2 + cc) = bits;
+    });
 }
 
 template <int T, int KC>
@@ -759,10 +770,10 @@ __device__ __forceinline__ void sym_store64(const SymOp64<TM, KC>& o, uint64_t* 
 // reads are wave broadcasts: one 16-B read per two rows) and columns tx + 16 j (its B reads are 16
 // lanes x 8 B contiguous: conflict-free).  Per k: M x M relaxations of a 64-bit add, a 64-bit
 // compare and two selects (the u64 price of SURVEY §8d: 5 int32 ops).
-template <int TM, int TK, int KC>
-__device__ __forceinline__ void fw_core_lb64(uint64_t* __restrict__ C, size_t ldc, const uint64_t* __restrict__ Ab,
-                                             bool acol, const uint64_t* __restrict__ Bb, bool bcol, size_t ldab,
-                                             uint64_t* __restrict__ C2, size_t ldc2) {
+template <int TM, int TK, int KC, class Epi>
+__device__ __forceinline__ void fw_core_lb64_e(uint64_t* __restrict__ C, size_t ldc, const uint64_t* __restrict__ Ab,
+                                               bool acol, const uint64_t* __restrict__ Bb, bool bcol, size_t ldab,
+                                               Epi&& epi) {
     using S = SymOp64<TM, KC>;
     constexpr int M = TM / 16;
     constexpr int LDX = TM + 2;
@@ -825,8 +836,17 @@ __device__ __forceinline__ void fw_core_lb64(uint64_t* __restrict__ C, size_t ld
 #pragma unroll
         for (int j = 0; j < M; ++j) {
             C[(size_t)(ty * M + i) * ldc + tx + 16 * j] = c[i][j];
-            if (C2) C2[(size_t)(ty * M + i) * ldc2 + tx + 16 * j] = c[i][j];
+            epi(ty * M + i, tx + 16 * j, c[i][j]);
         }
+}
+
+template <int TM, int TK, int KC>
+__device__ __forceinline__ void fw_core_lb64(uint64_t* __restrict__ C, size_t ldc, const uint64_t* __restrict__ Ab,
+                                             bool acol, const uint64_t* __restrict__ Bb, bool bcol, size_t ldab,
+                                             uint64_t* __restrict__ C2, size_t ldc2) {
+    fw_core_lb64_e<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, [&](int r, int cc, uint64_t v) {
+        if (C2) C2[(size_t)r * ldc2 + cc] = v;
+    });
 }
 
 template <int T, int KC>
@@ -835,6 +855,14 @@ constexpr size_t lb_lds_bytes64() { return (size_t)2 * 2 * KC * (T + 2) * sizeof
 // LDS of a line-buffer product of TM-tiles: pair-packed u32 or u64 keys
 template <class K, int TM, int KC>
 constexpr size_t lb_lds() { return sizeof(K) == 4 ? lb_lds_bytes<TM, KC>() : lb_lds_bytes64<TM, KC>(); }
+
+// one product of the line-buffer schedule, for either key type, with an epilogue functor
+template <class K, int TM, int TK, int KC, class Epi>
+__device__ __forceinline__ void fw_core_e(K* __restrict__ C, size_t ldc, const K* __restrict__ Ab, bool acol,
+                                          const K* __restrict__ Bb, bool bcol, size_t ldab, Epi&& epi) {
+    if constexpr (sizeof(K) == 4) fw_core_lb_e<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, epi);
+    else fw_core_lb64_e<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, epi);
+}
 
 // one product of the line-buffer schedule, for either key type
 template <class K, int TM, int TK, int KC>
@@ -986,16 +1014,16 @@ __device__ __forceinline__ void st_wt(K* p, K v) {
 // the launch).  Keys <= INF = 2^31 - 1: no sum wraps.  P is read and written write-through
 // (grid_sync); the previous kernel's plain stores are visible at the launch boundary.  K = u64:
 // keys <= INF = 2^62, the same.
+// The closure's body for output block (by, bx) of nwg participating workgroups (the fused FW
+// step runs it on its first chain workgroups, fw_step.hip.h); A, B, sh: LDS scratch.
 template <class K, int T>
-__global__ void __launch_bounds__(256) fw_close_sq(K* __restrict__ P, uint32_t* __restrict__ sync,
-                                                   uint32_t* __restrict__ timeout, int prio) {
-    if (prio) __builtin_amdgcn_s_setprio(3);
-    __shared__ K A[16][T + 1];
-    __shared__ K B[T][17];
-    __shared__ uint32_t s_chg, s_ok, s_more;
+__device__ __forceinline__ void close_body(K* __restrict__ P, uint32_t* __restrict__ sync, uint32_t* __restrict__ timeout,
+                                           int by, int bx, uint32_t nwg, K (*A)[T + 1], K (*B)[17], uint32_t* sh) {
+    uint32_t& s_chg = sh[0];
+    uint32_t& s_ok = sh[1];
+    uint32_t& s_more = sh[2];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int r0 = blockIdx.y * 16, c0 = blockIdx.x * 16;
-    const uint32_t nwg = gridDim.x * gridDim.y;
+    const int r0 = by * 16, c0 = bx * 16;
     // write-through (sc1, aux = 16) 16-B loads of the 16 rows and 16 columns this workgroup needs
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)(T * T * sizeof(K)), 0x00027000);
@@ -1043,6 +1071,16 @@ __global__ void __launch_bounds__(256) fw_close_sq(K* __restrict__ P, uint32_t* 
         __syncthreads();
         if (!s_more) return;
     }
+}
+
+template <class K, int T>
+__global__ void __launch_bounds__(256) fw_close_sq(K* __restrict__ P, uint32_t* __restrict__ sync,
+                                                   uint32_t* __restrict__ timeout, int prio) {
+    if (prio) __builtin_amdgcn_s_setprio(3);
+    __shared__ K A[16][T + 1];
+    __shared__ K B[T][17];
+    __shared__ uint32_t sh[4];
+    close_body<K, T>(P, sync, timeout, (int)blockIdx.y, (int)blockIdx.x, gridDim.x * gridDim.y, A, B, sh);
 }
 
 // lb[slot(j)] <- stored tile (min(j, L), max(j, L)) of D, j = blockIdx.x

@@ -40,6 +40,7 @@
 #include "comm.h"
 #include "sparse.hip.h"
 #include "events.hip.h"
+#include "fw_step.hip.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -676,6 +677,8 @@ struct srg_ctx {
     DevBuf b_n16s, b_n16d, b_n32l;   // narrowed edge arrays on the device
     DevBuf b_exc;                    // sequential-pair codec: a chunk's exceptions (index, src, dst)
     std::vector<std::vector<uint32_t>> codec_ex;  // its per-worker exception lists
+    std::vector<uint32_t> slice_exc;    // the slice's exceptions (global index, src, dst), all chunks
+    DevBuf b_xexc;                      // edge-sharded exchange: every rank's exceptions, counts
     size_t own_row0 = 0, own_row1 = ~(size_t)0;  // the output rows this rank routed (multi-rank: [p0, p1))
     int late_loss = 1;               // host entry: edge losses shipped beside FW (SRG_OPT_LATE_LOSS)
     hipStream_t loss_stream = nullptr;  // = d2h_stream (see srg_create)
@@ -714,6 +717,10 @@ struct srg_ctx {
     uint32_t sig_val[2] = {0, 0};
     bool hop_values = false;            // this build's hops use the signals (stream_hop)
     int fw_line_split = 0;              // symmetric FW: line sub-tiles per dimension (0 = auto) (SRG_OPT_FW_LINE_SPLIT)
+    int fw_step = -1;                   // symmetric FW: 1 = one fused launch per pivot (fw_step.hip.h), 0 = the
+                                        // two-stream schedule, -1 = auto (SRG_OPT_FW_STEP)
+    DevBuf b_xlb, b_xflags;             // fused FW: three line buffers in one block, peers' arrival flags
+    uint32_t xepoch = 0;                // fused FW with a device-side exchange: this build's flag value
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -721,7 +728,7 @@ struct srg_ctx {
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
-                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst,
+                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc,
                           &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
@@ -1326,6 +1333,33 @@ __global__ void k_low_words(const uint64_t* __restrict__ x, size_t n, uint32_t* 
 // unpacked with the mirror, so that every rank holds the whole D.  shadow_amd/dist.py line_fw
 // restates this schedule in numpy (tests/test_dist_cpu.py runs it on gloo ranks).
 template <class K, int T>
+void fw_sym_finish(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, const std::vector<int>& own_h,
+                   const std::vector<int>& slot_h, const std::vector<int>& first, double& ms_xchg);
+
+// this rank's stored tiles (triangle indices, row-major; uploaded to c.b_tiles), and for the final
+// exchange every tile's slot in the packed buffer (owner-major, each owner's tiles in triangle order)
+inline void sym_tiles(srg_ctx& c, const Plan& pl, hipStream_t st, std::vector<int>& own_h, std::vector<int>& slot_h,
+                      std::vector<int>& first) {
+    const int nb = pl.nb, G = pl.G, g = pl.g;
+    const int ntri = nb * (nb + 1) / 2;
+    own_h.clear();
+    slot_h.assign(ntri, 0);
+    first.assign(G + 1, 0);
+    for (int t = 0, I = 0; I < nb; ++I)
+        for (int J = I; J < nb; ++J, ++t) {
+            const int r = (I + J) % G;
+            if (r == g) own_h.push_back(t);
+            ++first[r + 1];
+        }
+    for (int r = 0; r < G; ++r) first[r + 1] += first[r];
+    std::vector<int> fill(first.begin(), first.end() - 1);
+    for (int t = 0, I = 0; I < nb; ++I)
+        for (int J = I; J < nb; ++J, ++t) slot_h[t] = fill[(I + J) % G]++;
+    int* tiles = (int*)c.b_tiles.get(std::max<size_t>(own_h.size(), 1) * 4);
+    if (!own_h.empty()) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
+}
+
+template <class K, int T>
 void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
                  int& prof_n, double& ms_xchg) {
     constexpr int KCS = 16;
@@ -1377,25 +1411,10 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
     uint32_t* cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
     c.fw_timeout = cflags + (size_t)nb * 16;
     HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
-    // this rank's tiles (triangle indices, row-major), and for the final exchange every tile's
-    // slot in the packed buffer (owner-major, each owner's tiles in triangle order)
-    const int ntri = nb * (nb + 1) / 2;
-    std::vector<int> own_h, slot_h(ntri), first(G + 1, 0);
-    for (int t = 0, I = 0; I < nb; ++I)
-        for (int J = I; J < nb; ++J, ++t) {
-            const int r = (I + J) % G;
-            if (r == g) own_h.push_back(t);
-            ++first[r + 1];
-        }
-    for (int r = 0; r < G; ++r) first[r + 1] += first[r];
-    {
-        std::vector<int> fill(first.begin(), first.end() - 1);
-        for (int t = 0, I = 0; I < nb; ++I)
-            for (int J = I; J < nb; ++J, ++t) slot_h[t] = fill[(I + J) % G]++;
-    }
+    std::vector<int> own_h, slot_h, first;
+    sym_tiles(c, pl, st, own_h, slot_h, first);
     const int ntile = (int)own_h.size();
-    int* tiles = (int*)c.b_tiles.get(std::max<size_t>(own_h.size(), 1) * 4);
-    if (ntile) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
+    const int* tiles = (const int*)c.b_tiles.p;
     hipStream_t aux = c.aux_stream, cs = c.comm_stream;
     const int prio = kChainPrio;
     auto close_pivot = [&](K* lbk, int k, hipStream_t s) {
@@ -1445,12 +1464,25 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
         if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
     }
     HIP_CHECK(hipGetLastError());
+    fw_sym_finish<K, T>(c, pl, D, Vp, st, own_h, slot_h, first, ms_xchg);
+}
+
+// End of the symmetric FW: mirror the lower triangle (one rank), or every rank ends with the whole D:
+// pack the own tiles, all-gather, unpack with the mirror.
+template <class K, int T>
+void fw_sym_finish(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, const std::vector<int>& own_h,
+                   const std::vector<int>& slot_h, const std::vector<int>& first, double& ms_xchg) {
+    const int nb = pl.nb, G = pl.G, g = pl.g;
+    constexpr size_t TT = (size_t)T * T;
+    const bool multi = c.comm && c.comm->nranks > 1;
+    const int ntri = nb * (nb + 1) / 2, ntile = (int)own_h.size();
+    const int* tiles = (const int*)c.b_tiles.p;
+    hipStream_t cs = c.comm_stream;
     if (!multi) {
         const unsigned nb64 = (unsigned)(Vp / 64);
         k_sym_mirror<K><<<dim3(nb64, nb64), 256, 0, st>>>(D, Vp);
         return;
     }
-    // every rank ends with the whole D: pack the own tiles, all-gather, unpack with the mirror
     HIP_CHECK(hipStreamSynchronize(st));  // (FW done: the exchange is timed on its own)
     auto t0x = std::chrono::steady_clock::now();
     K* Pk = (K*)c.b_PRED.get((size_t)ntri * TT * sizeof(K));
@@ -1473,6 +1505,143 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
     ms_xchg += ms_since(t0x);
 }
 
+// The symmetric FW as one fused launch per pivot (fw_step.hip.h): pivot kb's bulk and the chain of
+// k1 = kb + 1 (line w.r.t. kb, exchange, closure, line w.r.t. k1) in one launch on `st`, so the
+// per-pivot critical path has no cross-stream hop and no separate collective: peers exchange their
+// line segments inside the launch (xmode 2: stores into every peer's line buffer + arrival flags;
+// xmode 1: a simulated rank waits the modelled link time; 0: one rank).
+template <class K, int T, int SB, int SL>
+void launch_step(const StepArgs<K>& a, int grid, hipStream_t st) {
+    constexpr size_t lds = step_lds<K, T, SB, SL>();
+    static bool attr = false;
+    if (!attr) {
+        set_lds(fw_step<K, T, SB, SL>, lds);
+        attr = true;
+    }
+    fw_step<K, T, SB, SL><<<grid, 256, lds, st>>>(a);
+}
+
+template <class K, int T>
+void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax, int& prof_n,
+                   double& ms_xchg, int xmode) {
+    const int nb = pl.nb, G = pl.G, g = pl.g;
+    constexpr size_t TT = (size_t)T * T;
+    const LineMap lm{nb, G};
+    const size_t lbb = (size_t)nb * TT * sizeof(K);
+    K* xlb = (K*)c.b_xlb.get(3 * lbb);
+    K* LB[3] = {xlb, xlb + (size_t)nb * TT, xlb + 2 * (size_t)nb * TT};
+    // sync words: 16 per pivot (fw_step StepSync; pivot 0's closure uses words 0..8), then the
+    // timeout word
+    uint32_t* cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
+    c.fw_timeout = cflags + (size_t)nb * 16;
+    HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
+    std::vector<int> own_h, slot_h, first;
+    sym_tiles(c, pl, st, own_h, slot_h, first);
+    const int ntile = (int)own_h.size();
+    const int* tiles = (const int*)c.b_tiles.p;
+    // device-side exchange: every rank's line-buffer block and arrival words (re-shared per build:
+    // a host rendezvous of the group; buffers may have moved)
+    std::vector<void*> plb(G, nullptr);
+    std::vector<uint32_t*> pfl(G, nullptr);
+    bool sys = false;
+    uint32_t* myflags = nullptr;
+    if (xmode == 2) {
+        const size_t fb = (size_t)nb * G * 4;
+        if (c.b_xflags.bytes < fb) {
+            myflags = (uint32_t*)c.b_xflags.get(fb);
+            HIP_CHECK(hipMemsetAsync(myflags, 0, fb, st));
+        }
+        myflags = (uint32_t*)c.b_xflags.p;
+        HIP_CHECK(hipStreamSynchronize(st));  // zeroed flags before any peer may raise one
+        c.comm->share_ptrs(xlb, myflags, plb.data(), pfl.data(), &sys);
+        ++c.xepoch;
+        if (c.xepoch == 0) ++c.xepoch;
+    }
+    // line 0: every rank holds the same initial D (no exchange)
+    const int bulk_tiles = nb * (nb + 1) / 2 / G;
+    int SL = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
+    int SB = bulk_tiles >= 768 ? 1 : 2;
+    if (const char* e = std::getenv("SRG_FW_SB")) SB = std::atoi(e) == 2 ? 2 : 1;  // experiments
+    // quadrant lines at least: a whole-tile line core beside the bulk's in one kernel spilled 110
+    // VGPRs (the 168-VGPR budget of three waves per SIMD)
+    if (SL == 1) SL = 2;
+    k_pack_line<K, T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
+    fw_close_sq<K, T><<<dim3(T / 16, T / 16), 256, 0, st>>>(LB[0] + (size_t)lm.slot(0, 0) * TT, cflags, c.fw_timeout,
+                                                           kChainPrio);
+    set_lds(fw_line_lb<K, T, 1>, lb_lds<K, T, line_kc<1>()>());
+    fw_line_lb<K, T, 1><<<dim3(nb, 1), 256, lb_lds<K, T, line_kc<1>()>(), st>>>(D, Vp, LB[0], 0, LB[0], 0, 1, lm, g,
+                                                                              kChainPrio);
+    HIP_CHECK(hipGetLastError());
+    constexpr int NC = (T / 16) * (T / 16);
+    int CH = std::max(NC, std::min(256, nb * SL * SL));
+    if (const char* e = std::getenv("SRG_FW_CH")) CH = std::max(NC, std::atoi(e));  // experiments
+    const bool prof = c.profiling && nb > 2;
+    if (prof) {
+        while (c.prof_events.size() < (size_t)2 * nb) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            c.prof_events.push_back(e);
+        }
+    }
+    for (int kb = 0; kb < nb; ++kb) {
+        const int k1 = kb + 1 < nb ? kb + 1 : -1;
+        StepArgs<K> a{};
+        a.D = D;
+        a.ld = Vp;
+        a.lbk = LB[kb % 3];
+        a.lbn = k1 >= 0 ? LB[k1 % 3] : nullptr;
+        a.kb = kb;
+        a.k1 = k1;
+        a.lm = lm;
+        a.g = g;
+        a.tiles = tiles;
+        a.ntile = ntile;
+        a.CH = k1 >= 0 ? CH : 0;
+        a.sync = cflags + (size_t)16 * (k1 >= 0 ? k1 : 0);
+        a.timeout = c.fw_timeout;
+        a.xmode = G > 1 ? xmode : 0;
+        a.sys = sys ? 1 : 0;
+        a.epoch = c.xepoch;
+        a.myflags = myflags;
+        if (const char* e = std::getenv("SRG_FW_DBG")) a.dbg = std::atoi(e);  // experiments
+        if (a.dbg & 4) a.sys = 1;
+        if (xmode == 1 && k1 >= 0) {
+            size_t mx = 0;  // the largest segment a peer sends this rank
+            for (int r = 0; r < G; ++r)
+                if (r != g) mx = std::max(mx, (size_t)lm.count(r, k1) * TT * sizeof(K));
+            a.model_ns = (uint32_t)c.comm->model_xchg_ns(mx);
+        }
+        if (xmode == 2 && k1 >= 0)
+            for (int r = 0; r < G && r < kMaxPeers; ++r)
+                if (r != g) {
+                    a.peer_lbn[r] = (K*)plb[r] + (size_t)(k1 % 3) * nb * TT;
+                    a.peer_flags[r] = pfl[r];
+                }
+        const int grid = a.CH + ntile * SB * SB;
+        const bool timed = prof && ntile > 0 && k1 >= 0;
+        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
+        if (grid > 0) {
+            if (SB == 1 && SL == 2) launch_step<K, T, 1, 2>(a, grid, st);
+            else if (SB == 1) launch_step<K, T, 1, 4>(a, grid, st);
+            else if (SL == 2) launch_step<K, T, 2, 2>(a, grid, st);
+            else launch_step<K, T, 2, 4>(a, grid, st);
+        }
+        HIP_CHECK(hipGetLastError());
+        if (timed) {
+            int64_t m = 0;  // bulk relaxations of this launch: own tiles off lines kb and k1
+            for (int t : own_h) {
+                int I, J;
+                tri_tile_h(nb, t, I, J);
+                if (I != kb && I != k1 && J != kb && J != k1) ++m;
+            }
+            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
+            prof_relax += (uint64_t)m * T * T * T;
+            ++prof_n;
+        }
+    }
+    fw_sym_finish<K, T>(c, pl, D, Vp, st, own_h, slot_h, first, ms_xchg);
+}
+
 // General FW, several ranks: every rank ends with the whole D (row blocks all-gathered)
 template <class K>
 void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t st, double& ms_xchg) {
@@ -1491,6 +1660,27 @@ void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t
     HIP_CHECK(hipStreamWaitEvent(st, c.ev_c, 0));
     HIP_CHECK(hipStreamSynchronize(st));
     ms_xchg += ms_since(t0x);
+}
+
+// Which symmetric FW schedule runs: -1 = the two-stream schedule (fw_line_sym), else the fused
+// launch per pivot with that exchange mode (fw_line_fused): 0 one rank, 1 simulated rank, 2 peers.
+// SRG_OPT_FW_STEP: 1 = fused wherever possible, 0 = never, -1 (auto) = fused for a simulated rank
+// and for in-process ranks on distinct devices; one rank by the environment switch
+// SRG_FW_FUSED (A/B while the default is measured).  RCCL ranks keep the two-stream schedule (their
+// exchange is a collective on the chain's stream).
+int fw_step_mode(const srg_ctx& c) {
+    const bool multi = c.comm && c.comm->nranks > 1;
+    if (c.fw_step == 0) return -1;
+    if (!multi) {
+        if (c.fw_step == 1) return 0;
+        const char* e = std::getenv("SRG_FW_FUSED");
+        return e && std::strcmp(e, "1") == 0 ? 0 : -1;
+    }
+    if (c.comm->nranks > kMaxPeers) return -1;
+    const int dx = c.comm->device_exchange();
+    if (dx == 1) return 1;
+    if (dx == 2 && (c.fw_step == 1 || c.comm->distinct_devices())) return 2;
+    return -1;
 }
 
 // the symmetric FW over line buffers applies: undirected, u32 pair-packed 128-tiles or u64 64-tiles
@@ -1552,8 +1742,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     int prof_n = 0;
     double ms_dx = 0;  // multi-rank: D exchange at the end of FW (inside ms_fw, also in ms_exchange)
     if (sym_fw_for<K, T>(c, g)) {
-        if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64))
-            fw_line_sym<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx);
+        if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64)) {
+            const int xm = fw_step_mode(c);
+            if (xm >= 0) fw_line_fused<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx, xm);
+            else fw_line_sym<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx);
+        }
     } else {
         // u32 keys: the pair-packed tile (two relaxations per 64-bit add + v_min3); the add + min3
         // tile (PK = 0) ran the same C3 launch in 0.304 instead of 0.242 ms (profiles/r02c/fw_fold.txt)
@@ -2377,7 +2570,7 @@ __global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const 
 // Returns false (nothing usable staged) when an endpoint >= 65536 or a latency >= 2^32 is seen:
 // the caller then ships the plain arrays, whose checks report such edges as the reference does.
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
-              bool& all_narrow);
+              bool& all_narrow, bool& all_seq);
 
 // Sequential-pair codec, device side: edge i of a chunk is (src, dst) = (es[j], ed[j] + i - ei[j])
 // for the last exception j with ei[j] <= i (ei[0] = 0: a chunk starts with one), latency = l32[i].
@@ -2400,6 +2593,25 @@ __global__ void k_decode_seq(size_t ne, const uint32_t* __restrict__ l32, const 
     }
 }
 
+// The edge-sharded exchange's sequential-pair form: edges [e0, e1) of the whole list from every
+// slice's exceptions ex = (global index, src, dst) x nexc in index order (each slice starts with
+// one, so index 0 is covered) and the u32 latencies.
+__global__ void k_decode_seq_global(size_t e0, size_t e1, const uint32_t* __restrict__ l32,
+                                    const uint32_t* __restrict__ ex, uint32_t nexc, uint32_t* __restrict__ src,
+                                    uint32_t* __restrict__ dst, uint64_t* __restrict__ lat) {
+    for (size_t i = e0 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < e1; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = nexc - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (ex[3 * (size_t)mid] <= (uint32_t)i) lo = mid;
+            else hi = mid - 1;
+        }
+        src[i] = ex[3 * (size_t)lo + 1];
+        dst[i] = ex[3 * (size_t)lo + 2] + ((uint32_t)i - ex[3 * (size_t)lo]);
+        lat[i] = l32[i];
+    }
+}
+
 template <class T>
 T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
     T* d = (T*)b.get(std::max<size_t>(count, 1) * sizeof(T));
@@ -2417,9 +2629,14 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
 // u16 endpoints and the rest of the list stays in that mode.
 // all_narrow: every edge of the slice also stays narrowed on the device (b_n16s / b_n16d / b_n32l),
 // false when the host-slow switch shipped the rest of the slice plain.
+// all_seq: every chunk of the slice went sequential-pair: its u32 latencies are in b_n32l and its
+// exceptions (GLOBAL edge index, src, dst) in c.slice_exc -- the edge-sharded exchange then ships
+// that form (4 B per edge) instead of the u16 narrowing (8 B).
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
-              bool& all_narrow) {
+              bool& all_narrow, bool& all_seq) {
     all_narrow = true;
+    all_seq = false;
+    c.slice_exc.clear();
     const size_t E = g->num_edges, A = a1 - a0;
     constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
     constexpr int NB = 3;                   // ring slots
@@ -2453,7 +2670,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     double t_conv = 0, t_wait = 0;
     const size_t nch = (A + CE - 1) / CE;
     const char* sq = std::getenv("SRG_CODEC_SEQ");
-    bool seq = A == E && !(sq && std::strcmp(sq, "0") == 0);
+    bool seq = !(sq && std::strcmp(sq, "0") == 0);  // (a slice of a row-ordered list is row-ordered too)
     uint32_t* dexc = seq ? (uint32_t*)c.b_exc.get(CE * 4) : nullptr;
     const int nwk = c.pool->size();
     if ((int)c.codec_ex.size() < nwk) c.codec_ex.resize(nwk);
@@ -2538,6 +2755,9 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
                     hx[q] = ex[k];
                     hx[nexc + q] = ex[k + 1];
                     hx[2 * nexc + q] = ex[k + 2];
+                    c.slice_exc.push_back((uint32_t)(e0 + ex[k]));  // global index, src, dst
+                    c.slice_exc.push_back(ex[k + 1]);
+                    c.slice_exc.push_back(ex[k + 2]);
                 }
             }
             HIP_CHECK(hipMemcpyAsync(l32 + e0, hl, ne * 4, hipMemcpyHostToDevice, st));
@@ -2570,6 +2790,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
         }
     }
     if (seq_chunks) all_narrow = false;  // (the endpoints are not on the device narrowed)
+    all_seq = seq_chunks == nch && nch > 0;
     if (dbg) std::fprintf(stderr, "codec: %zu chunks (%zu sequential-pair), %d threads, convert %.2f ms, slot waits %.2f ms\n",
                           nch, seq_chunks, c.pool->size(), t_conv, t_wait);
     return true;
@@ -2725,11 +2946,11 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // late loss: the losses follow the endpoints and latencies on their own stream, beside
         // the W build and FW (dense u32 path: WL is built from them on c->loss_stream)
         const bool want_late = c->late_loss && !direct && !shard;
-        bool all_narrow = false;
-        // (V > 65536: only a row-ordered list, through the sequential-pair chunks, can be narrowed)
+        bool all_narrow = false, all_seq = false;
+        // (V > 65536: only a row-ordered list, through the sequential-pair chunks, can be narrowed;
+        // codec_in gives up on the first chunk that is neither)
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) &&
-                           (g->num_vertices <= 65536 || a1 - a0 == E) &&
-                           codec_in(*c, g, dg, st, a0, a1, !want_late, all_narrow);
+                           codec_in(*c, g, dg, st, a0, a1, !want_late, all_narrow, all_seq);
         LateLoss late;
         late.ls = c->loss_stream;
         if (coded && want_late) start_late_loss(*c, g, dg, st, late);
@@ -2776,17 +2997,55 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 }
                 c->comm->allgatherv(const_cast<void*>(p), offs.data(), lens.data(), st);
             };
-            // every rank shipped its slice narrowed (the usual case): exchange the narrow arrays
-            // (12 B per edge with the loss instead of 20) and widen the other ranks' slices here;
-            // else the wide arrays, since a rank may have shipped its slice plain
+            // the narrowest form every rank has: 0 = sequential-pair (each slice's u32 latencies +
+            // exceptions: 4 B per edge with the loss 8), 1 = u16 narrowing (8 B, 12 with the loss),
+            // 2 = plain (a rank shipped its slice plain: 20 B)
             uint32_t* plain = (uint32_t*)c->b_red.get(16);
-            const uint32_t mine = coded && all_narrow ? 0u : 1u;
+            const uint32_t mine = !coded ? 2u : all_seq ? 0u : all_narrow ? 1u : 2u;
             HIP_CHECK(hipMemcpyAsync(plain, &mine, 4, hipMemcpyHostToDevice, st));
             c->comm->allreduce_max_u32(plain, 1, st);
-            uint32_t any_plain = 1;
-            HIP_CHECK(hipMemcpyAsync(&any_plain, plain, 4, hipMemcpyDeviceToHost, st));
+            uint32_t form = 2;
+            HIP_CHECK(hipMemcpyAsync(&form, plain, 4, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
-            if (!any_plain) {
+            if (form == 0) {
+                // every slice's exception count, then every slice's exceptions (global index, src,
+                // dst), the u32 latencies and the losses; the other slices are decoded here
+                const size_t xbase = ((size_t)nr * 4 + 255) / 256 * 256;
+                uint32_t* xc = (uint32_t*)c->b_xexc.get(xbase);
+                const uint32_t my_n = (uint32_t)(c->slice_exc.size() / 3);
+                HIP_CHECK(hipMemcpyAsync(xc + rk, &my_n, 4, hipMemcpyHostToDevice, st));
+                for (int q = 0; q < nr; ++q) {
+                    offs[q] = (size_t)q * 4;
+                    lens[q] = 4;
+                }
+                c->comm->allgatherv(xc, offs.data(), lens.data(), st);
+                std::vector<uint32_t> cnt(nr);
+                HIP_CHECK(hipMemcpyAsync(cnt.data(), xc, (size_t)nr * 4, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                if (sim)
+                    for (int q = 0; q < nr; ++q) cnt[q] = my_n;  // (a simulated rank hears nothing: its own size)
+                size_t tot = 0, mine_at = 0;
+                for (int q = 0; q < nr; ++q) {
+                    if (q == rk) mine_at = tot;
+                    offs[q] = xbase + tot * 12;
+                    lens[q] = (size_t)cnt[q] * 12;
+                    tot += cnt[q];
+                }
+                unsigned char* xb = (unsigned char*)c->b_xexc.get(xbase + std::max<size_t>(tot, 1) * 12);
+                if (my_n)
+                    HIP_CHECK(hipMemcpyAsync(xb + xbase + mine_at * 12, c->slice_exc.data(), (size_t)my_n * 12,
+                                             hipMemcpyHostToDevice, st));
+                c->comm->allgatherv(xb, offs.data(), lens.data(), st);
+                uint32_t* l32 = (uint32_t*)c->b_n32l.p;
+                gather(l32, 4);
+                gather(dg.loss, 4);
+                for (auto [e0, e1] : {std::pair<size_t, size_t>{0, a0}, std::pair<size_t, size_t>{a1, E}})
+                    if (e1 > e0 && !sim)
+                        k_decode_seq_global<<<grid_for(e1 - e0), kThreads, 0, st>>>(
+                            e0, e1, l32, (const uint32_t*)(xb + xbase), (uint32_t)tot, (uint32_t*)dg.src,
+                            (uint32_t*)dg.dst, (uint64_t*)dg.lat);
+                HIP_CHECK(hipGetLastError());
+            } else if (form == 1) {
                 uint16_t* s16 = (uint16_t*)c->b_n16s.p;
                 uint16_t* d16 = (uint16_t*)c->b_n16d.p;
                 uint32_t* l32 = (uint32_t*)c->b_n32l.p;
@@ -3029,6 +3288,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1 && value != 2 && value != 4) return SRG_ERR_ARG;
             ctx->fw_line_split = (int)value;
             return SRG_OK;
+        case SRG_OPT_FW_STEP:
+            if (value != 0 && value != 1 && value != -1) return SRG_ERR_ARG;
+            ctx->fw_step = (int)value;
+            return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
             ctx->algorithm = (int)value;
@@ -3061,6 +3324,7 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_EDGE_SHARD: *value = ctx->edge_shard; break;
         case SRG_OPT_LATE_LOSS: *value = ctx->late_loss; break;
         case SRG_OPT_FW_LINE_SPLIT: *value = ctx->fw_line_split; break;
+        case SRG_OPT_FW_STEP: *value = ctx->fw_step; break;
         default: return SRG_ERR_ARG;
     }
     return SRG_OK;

@@ -170,17 +170,24 @@ def test_edge_sharded_host_entry(G, shard):
         assert bits_equal(t.packet_loss, loss), f"rank {r} loss"
 
 
-def test_edge_sharded_codec_slices():
-    """Edge sharding with the H2D codec active on every rank's slice (>= 2^20 edges per slice):
-    the exchanged widened slices equal the single-GPU build."""
-    e = synth.atlas_like(2100, seed=2100)
-    assert e.num_edges >= 2 * (1 << 20) + 2
-    nodes = list(range(0, 2100, 7))
+@pytest.mark.parametrize("G,V,order", [(2, 2100, "rows"), (4, 3000, "rows"), (2, 2100, "shuffled")])
+def test_edge_sharded_codec_slices(G, V, order):
+    """Edge sharding with the H2D codec active on every rank's slice (>= 2^20 edges per slice): a
+    row-ordered list crosses and is exchanged in the sequential-pair form (u32 latencies + row-start
+    exceptions, decoded on every rank), a shuffled one in the u16 narrowing; both equal the
+    single-GPU build."""
+    e = synth.atlas_like(V, seed=V)
+    if order == "shuffled":
+        from shadow_amd.graph import Edges
+        p = np.random.default_rng(V).permutation(e.num_edges)
+        e = Edges(V, e.src[p], e.dst[p], e.latency_ns[p], e.packet_loss[p], False)
+    assert e.num_edges >= G * (1 << 20) + 2
+    nodes = list(range(0, V, 7))
     r1 = Router(0)
     ref = r1.compute_shortest_paths(e, nodes)
     r1.close()
-    out, errs = run_ranks(2, e, nodes, shard=1)
-    assert errs == [None] * 2, errs
+    out, errs = run_ranks(G, e, nodes, shard=1)
+    assert errs == [None] * G, errs
     for r, t in enumerate(out):
         assert np.array_equal(t.latency_ns, ref.latency_ns), f"rank {r} latency"
         assert bits_equal(t.packet_loss, ref.packet_loss), f"rank {r} loss"
