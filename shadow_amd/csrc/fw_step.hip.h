@@ -57,10 +57,20 @@ struct StepArgs {
     int sys;            // xmode 2: peers on other devices (system-scope fences and stores)
     uint32_t epoch;     // xmode 2: this build's flag value
     uint32_t* myflags;  // xmode 2: [pivot * G + from] arrival words that peers raise here
-    int dbg;            // experiments: bit 0 release fence per phase-A workgroup, bit 1 50-us delay before go
+    unsigned long long* trace;  // SRG_FW_TRACE: 8 wall-clock stamps of this launch (null = off), see TraceAt
     K* peer_lbn[kMaxPeers];          // xmode 2: each peer's LB(k1) (null for this rank)
     uint32_t* peer_flags[kMaxPeers]; // xmode 2: each peer's arrival words
 };
+
+// trace stamps (wall_clock64, 100 MHz) of one launch: first workgroup start, all phase-A arrivals
+// seen, go, closure done, last chain workgroup done, last bulk workgroup done
+enum TraceAt { TR_START = 0, TR_ARRIVED = 1, TR_GO = 2, TR_CDONE = 3, TR_CHAIN_END = 4, TR_BULK_END = 5 };
+__device__ __forceinline__ void trace_min(unsigned long long* t, int at) {
+    if (t && threadIdx.x == 0) atomicMin(t + at, wall_clock64());
+}
+__device__ __forceinline__ void trace_max(unsigned long long* t, int at) {
+    if (t && threadIdx.x == 0) atomicMax(t + at, wall_clock64());
+}
 
 // bounded poll of *p until pred(value) (one lane); false after ~2 s (raises *timeout)
 template <class Pred>
@@ -90,9 +100,14 @@ __device__ __forceinline__ void st8_wt(void* p, uint64_t v, int sys) {
     else __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One (T/S) x (T/S) sub-tile q of line tile j: mode 0 = line K1 w.r.t. L (C = D tile, result also to
-// LB(K1) and the peers' LB(K1), write-through), mode 1 = line K1 w.r.t. its closed pivot (C = LB(K1)
-// tile in place, own tiles back to D).  fw_line_lb's work item (kernels.hip.h).
+// One (T/S) x (T/S) sub-tile q of line tile j: mode 0 = line K1 w.r.t. L (C read from the D tile, the
+// result to LB(K1) and the peers' LB(K1) only, write-through), mode 1 = line K1 w.r.t. its closed
+// pivot (C = LB(K1) tile in place, own tiles back to D).  fw_line_lb's work item (kernels.hip.h),
+// except that mode 0 does not write D: phase D writes the same D sub-tile later in the SAME launch,
+// from another workgroup, maybe on another XCD, and two plain stores of one line dirty in two XCD
+// L2s are written back in no particular order at the launch's end -- the stale phase-A value won
+// (measured: in-process ranks at line split 2 lost up to 5 % of their latencies).  Mode 1 is the
+// only D writer of a line tile.
 template <class K, int T, int S>
 __device__ __forceinline__ void line_item(const StepArgs<K>& a, int mode, int j, int q) {
     static_assert(S >= 2, "quadrant or smaller line items (a whole-tile line core beside the bulk's spills)");
@@ -146,7 +161,7 @@ __device__ __forceinline__ void line_item(const StepArgs<K>& a, int mode, int j,
     const K* Ab = lb + lm.slot(I, P) * TT + (acol ? (size_t)qi * TM : (size_t)qi * TM * T);
     const K* Bb = lb + lm.slot(J, P) * TT + (bcol ? (size_t)qj * TM : (size_t)qj * TM * T);
     if (mode == 0) {
-        fw_core_e<K, TM, T, KCL>(Dt, a.ld, Ab, acol, Bb, bcol, T, out_lb);
+        fw_core_e<K, TM, T, KCL, false>(Dt, a.ld, Ab, acol, Bb, bcol, T, out_lb);
     } else {
         K* Dd = own ? Dt : nullptr;
         fw_core_e<K, TM, T, KCL>(Lt, T, Ab, acol, Bb, bcol, T, [&](int r, int c, uint64_t bits) {
@@ -156,16 +171,10 @@ __device__ __forceinline__ void line_item(const StepArgs<K>& a, int mode, int j,
 }
 
 // arrival after a phase: every wave drains its stores, then one lane adds to the counter
-__device__ __forceinline__ void arrive(uint32_t* cnt, int rel = 0) {
+__device__ __forceinline__ void arrive(uint32_t* cnt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (rel) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // all threads of the workgroup wait until lane 0 saw *p satisfy pred, then acquire
@@ -190,12 +199,13 @@ __device__ __forceinline__ void chain(const StepArgs<K>& a, int w) {
         line_item<K, T, SL>(a, 0, j0 + G * (i / SS), i % SS);
         __syncthreads();  // the LDS image is reused by the next item
     }
-    arrive(&sy[SS_ARRIVE], a.dbg & 1);
+    arrive(&sy[SS_ARRIVE]);
     // ---- X: exchange (workgroup 0), then "go" -------------------------------------------------
     if (w == 0) {
         if (threadIdx.x == 0) {
             const uint32_t ch = (uint32_t)CH;
             if (poll_until(&sy[SS_ARRIVE], 0, a.timeout, [ch](uint32_t v) { return v >= ch; })) {
+                if (a.trace) a.trace[TR_ARRIVED] = wall_clock64();
                 if (a.xmode == 1) {
                     const unsigned long long t0 = wall_clock64(), ticks = a.model_ns / 10;  // 100 MHz
                     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
@@ -217,12 +227,9 @@ __device__ __forceinline__ void chain(const StepArgs<K>& a, int w) {
                                                     [ep](uint32_t v) { return v == ep; }))
                             break;
                     acquire_for(a.sys);
-                    if (a.dbg & 2) {
-                        const unsigned long long t1 = wall_clock64();
-                        while (wall_clock64() - t1 < 5000) __builtin_amdgcn_s_sleep(2);
-                    }
                 }
             }
+            if (a.trace) a.trace[TR_GO] = wall_clock64();
             __hip_atomic_store(&sy[SS_GO], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
@@ -239,7 +246,10 @@ __device__ __forceinline__ void chain(const StepArgs<K>& a, int w) {
         close_body<K, T>(a.lbn + (size_t)lm.slot(a.k1, a.k1) * T * T, sy + SS_CLOSE, a.timeout, w / NB16, w % NB16,
                          (uint32_t)NC, A, B, sh);
         __syncthreads();
-        if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&sy[SS_CDONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (w == 0 && threadIdx.x == 0) {
+            if (a.trace) a.trace[TR_CDONE] = wall_clock64();
+            __hip_atomic_store(&sy[SS_CDONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         acquire_for(0);
         __syncthreads();
     } else {
@@ -251,6 +261,7 @@ __device__ __forceinline__ void chain(const StepArgs<K>& a, int w) {
         line_item<K, T, SL>(a, 1, i / SS, i % SS);
         __syncthreads();
     }
+    trace_max(a.trace, TR_CHAIN_END);
 }
 
 // bulk item: this rank's stored tile (sub-tile q of SB x SB) off lines kb and k1, operands LB(kb)
@@ -283,8 +294,10 @@ constexpr size_t step_lds() {
 template <class K, int T, int SB, int SL>
 __global__ void __launch_bounds__(256, SB == 1 ? 3 : 4) fw_step(StepArgs<K> a) {
     const int w = (int)blockIdx.x;
+    trace_min(a.trace, TR_START);
     if (w >= a.CH) {
         bulk_item<K, T, SB>(a, w - a.CH);
+        trace_max(a.trace, TR_BULK_END);
         return;
     }
     __builtin_amdgcn_s_setprio(3);  // the chain is the launch's critical path

@@ -637,7 +637,8 @@ __device__ __forceinline__ void sym_store(const SymOp<T, KC>& o, u64p* __restric
 // is closed (min over k of C'[x][k] + P[k][y] = min over k of C[x][k] + P[k][y] for P closed).
 // Epilogue functor epi(r, c, bits): the product's result, 8 bytes at element (r, c) of the tile (two
 // u32 keys (r, c), (r, c + 1) here; one u64 key in fw_core_lb64), for destinations beyond C.
-template <int TM, int TK, int KC, class Epi>
+// STORE_C = false: C is only read (the result goes to the epilogue's destinations alone).
+template <int TM, int TK, int KC, bool STORE_C = true, class Epi>
 __device__ __forceinline__ void fw_core_lb_e(uint32_t* __restrict__ C, size_t ldc, const uint32_t* __restrict__ Ab,
                                              bool acol, const uint32_t* __restrict__ Bb, bool bcol, size_t ldab,
                                              Epi&& epi) {
@@ -706,7 +707,7 @@ __device__ __forceinline__ void fw_core_lb_e(uint32_t* __restrict__ C, size_t ld
             VecN<uint32_t, 2> v;
             v.v[0] = c[a][2 * g];
             v.v[1] = c[a][2 * g + 1];
-            stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ldc + 32 * g + 2 * tx, v);
+            if (STORE_C) stv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ldc + 32 * g + 2 * tx, v);
             epi(pk_rc(ty, a), 32 * g + 2 * tx, (uint64_t)v.v[0] | ((uint64_t)v.v[1] << 32));
         }
 }
@@ -770,7 +771,7 @@ __device__ __forceinline__ void sym_store64(const SymOp64<TM, KC>& o, uint64_t* 
 // reads are wave broadcasts: one 16-B read per two rows) and columns tx + 16 j (its B reads are 16
 // lanes x 8 B contiguous: conflict-free).  Per k: M x M relaxations of a 64-bit add, a 64-bit
 // compare and two selects (the u64 price of SURVEY §8d: 5 int32 ops).
-template <int TM, int TK, int KC, class Epi>
+template <int TM, int TK, int KC, bool STORE_C = true, class Epi>
 __device__ __forceinline__ void fw_core_lb64_e(uint64_t* __restrict__ C, size_t ldc, const uint64_t* __restrict__ Ab,
                                                bool acol, const uint64_t* __restrict__ Bb, bool bcol, size_t ldab,
                                                Epi&& epi) {
@@ -835,7 +836,7 @@ __device__ __forceinline__ void fw_core_lb64_e(uint64_t* __restrict__ C, size_t 
     for (int i = 0; i < M; ++i)
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            C[(size_t)(ty * M + i) * ldc + tx + 16 * j] = c[i][j];
+            if (STORE_C) C[(size_t)(ty * M + i) * ldc + tx + 16 * j] = c[i][j];
             epi(ty * M + i, tx + 16 * j, c[i][j]);
         }
 }
@@ -857,11 +858,11 @@ template <class K, int TM, int KC>
 constexpr size_t lb_lds() { return sizeof(K) == 4 ? lb_lds_bytes<TM, KC>() : lb_lds_bytes64<TM, KC>(); }
 
 // one product of the line-buffer schedule, for either key type, with an epilogue functor
-template <class K, int TM, int TK, int KC, class Epi>
+template <class K, int TM, int TK, int KC, bool STORE_C = true, class Epi>
 __device__ __forceinline__ void fw_core_e(K* __restrict__ C, size_t ldc, const K* __restrict__ Ab, bool acol,
                                           const K* __restrict__ Bb, bool bcol, size_t ldab, Epi&& epi) {
-    if constexpr (sizeof(K) == 4) fw_core_lb_e<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, epi);
-    else fw_core_lb64_e<TM, TK, KC>(C, ldc, Ab, acol, Bb, bcol, ldab, epi);
+    if constexpr (sizeof(K) == 4) fw_core_lb_e<TM, TK, KC, STORE_C>(C, ldc, Ab, acol, Bb, bcol, ldab, epi);
+    else fw_core_lb64_e<TM, TK, KC, STORE_C>(C, ldc, Ab, acol, Bb, bcol, ldab, epi);
 }
 
 // one product of the line-buffer schedule, for either key type

@@ -1583,9 +1583,19 @@ void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, 
             c.prof_events.push_back(e);
         }
     }
+    // SRG_FW_TRACE=1: per-launch wall-clock stamps of the chain phases (fw_step TraceAt), printed to
+    // stderr after FW (a diagnostic, tools/README.md)
+    unsigned long long* trace = nullptr;
+    if (std::getenv("SRG_FW_TRACE")) {
+        trace = (unsigned long long*)c.b_scantmp.get((size_t)nb * 8 * 8);
+        std::vector<unsigned long long> init((size_t)nb * 8, 0);
+        for (int k = 0; k < nb; ++k) init[(size_t)k * 8 + TR_START] = ~0ull;
+        HIP_CHECK(hipMemcpyAsync(trace, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
+    }
     for (int kb = 0; kb < nb; ++kb) {
         const int k1 = kb + 1 < nb ? kb + 1 : -1;
         StepArgs<K> a{};
+        a.trace = trace ? trace + (size_t)kb * 8 : nullptr;
         a.D = D;
         a.ld = Vp;
         a.lbk = LB[kb % 3];
@@ -1603,8 +1613,6 @@ void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, 
         a.sys = sys ? 1 : 0;
         a.epoch = c.xepoch;
         a.myflags = myflags;
-        if (const char* e = std::getenv("SRG_FW_DBG")) a.dbg = std::atoi(e);  // experiments
-        if (a.dbg & 4) a.sys = 1;
         if (xmode == 1 && k1 >= 0) {
             size_t mx = 0;  // the largest segment a peer sends this rank
             for (int r = 0; r < G; ++r)
@@ -1638,6 +1646,27 @@ void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, 
             prof_relax += (uint64_t)m * T * T * T;
             ++prof_n;
         }
+    }
+    if (trace) {
+        std::vector<unsigned long long> t((size_t)nb * 8);
+        HIP_CHECK(hipMemcpyAsync(t.data(), trace, t.size() * 8, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        double sum[6] = {0, 0, 0, 0, 0, 0}, gap = 0;
+        int cnt = 0;
+        for (int k = 0; k + 1 < nb; ++k) {
+            const unsigned long long* r = &t[(size_t)k * 8];
+            const double us[6] = {0, (r[1] - r[0]) * 0.01, (r[2] - r[0]) * 0.01, (r[3] - r[0]) * 0.01,
+                                  (r[4] - r[0]) * 0.01, (r[5] > r[0] ? r[5] - r[0] : 0) * 0.01};
+            const double g2 = k + 2 < nb ? (t[(size_t)(k + 1) * 8] - std::max(r[4], r[5])) * 0.01 : 0;
+            std::fprintf(stderr, "fw_step %d: arrived %.1f go %.1f cdone %.1f chain_end %.1f bulk_end %.1f gap %.1f us\n", k,
+                         us[1], us[2], us[3], us[4], us[5], g2);
+            for (int q = 1; q < 6; ++q) sum[q] += us[q];
+            gap += g2;
+            ++cnt;
+        }
+        if (cnt)
+            std::fprintf(stderr, "fw_step mean (G=%d SB=%d SL=%d CH=%d): arrived %.1f go %.1f cdone %.1f chain_end %.1f bulk_end %.1f gap %.1f us\n",
+                         G, SB, SL, CH, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt, gap / cnt);
     }
     fw_sym_finish<K, T>(c, pl, D, Vp, st, own_h, slot_h, first, ms_xchg);
 }

@@ -57,12 +57,11 @@ def main():
         dict(G=3, V=900, seed=12, split=2),
         dict(G=4, V=1100, seed=13, split=4),
         dict(G=2, V=400, seed=14, split=0, u64=True),
+        dict(G=2, V=900, seed=15, split=2, env={"SRG_FW_SB": "1"}),
     ]
     if len(sys.argv) > 1 and sys.argv[1] == "diag":
-        cases = [dict(G=2, V=900, seed=12, split=2), dict(G=2, V=900, seed=12, split=2, env={"SRG_FW_DBG": "1"}),
-                 dict(G=2, V=900, seed=12, split=2, env={"SRG_FW_DBG": "2"}),
-                 dict(G=2, V=900, seed=12, split=2, env={"SRG_FW_DBG": "4"}),
-                 dict(G=2, V=900, seed=12, split=2, env={"SRG_FW_DBG": "7"})]
+        cases = [dict(G=2, V=900, seed=12, split=2), dict(G=3, V=1000, seed=15, split=2),
+                 dict(G=2, V=900, seed=12, split=2, env={"SRG_FW_SB": "1"}), dict(G=5, V=1300, seed=16, split=0)]
     res = []
     for c in cases:
         kw = dict(lat_lo=2 ** 31, lat_hi=2 ** 33) if c.get("u64") else {}

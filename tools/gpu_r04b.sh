@@ -21,3 +21,5 @@ for st in 1 0; do
 done
 timeout -k 10 600 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_multi_gpu.py > $out/pytest_multi.log 2>&1 || { echo "multi tests failed"; tail -60 $out/pytest_multi.log; exit 1; }
 tail -5 $out/pytest_multi.log
+timeout -k 10 400 python -u -m pytest -m gpu -x -v --timeout 250 --timeout-method thread tests/test_fw_step.py > $out/pytest_fw_step.log 2>&1 || { echo "fw_step tests failed"; tail -60 $out/pytest_fw_step.log; exit 1; }
+tail -5 $out/pytest_fw_step.log
