@@ -257,7 +257,7 @@ def apply_options(router, args):
                       ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
                       ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
                       ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT"),
-                      ("fw_step", "FW_STEP")):
+                      ("fw_step", "FW_STEP"), ("fw_overlap", "FW_OVERLAP")):
         v = getattr(args, flag)
         if v is not None:
             router.set_option(getattr(N, "SRG_OPT_" + opt), v)
@@ -511,6 +511,8 @@ def main():
     ap.add_argument("--fw-step", type=int, default=None,
                     help="symmetric FW: 1 = one fused launch per pivot (chain + bulk, in-launch line exchange), "
                          "0 = two-stream schedule, -1 = auto")
+    ap.add_argument("--fw-overlap", type=int, default=None,
+                    help="host entry, one rank: 1 = FW starts while the edge list arrives (default), 0 = after it")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")
     ap.add_argument("--fw-tile", type=int, default=0, help="dense FW tile (0 = auto)")
     ap.add_argument("--simulate-rank", type=str, default=None,

@@ -181,6 +181,11 @@ void srg_destroy(srg_ctx* ctx);
                                      * -1 (default) = fused for simulated ranks and for in-process ranks on
                                      * distinct devices (ranks sharing a GPU set 1 only when each rank's launch
                                      * has a hardware queue of its own) */
+#define SRG_OPT_FW_OVERLAP 33        /* host entry, one rank: 1 (default) = FW starts while the edge list is still
+                                     * crossing PCIe (an undirected list ordered by source row with every edge
+                                     * (s, d), s <= d -- a GML complete graph: each block-row of W is split and
+                                     * caught up on the pivots already run as soon as its edges have landed);
+                                     * 0 = FW after the whole list (any list falls back to that by itself) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

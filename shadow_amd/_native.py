@@ -49,6 +49,7 @@ SRG_OPT_EDGE_SHARD = 29
 SRG_OPT_LATE_LOSS = 30
 SRG_OPT_FW_LINE_SPLIT = 31
 SRG_OPT_FW_STEP = 32
+SRG_OPT_FW_OVERLAP = 33
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

@@ -903,15 +903,43 @@ struct LineMap {
 // Bulk of pivot L: this rank's stored tiles (triangle indices tiles[0 .. gridDim.x)) except
 // those in lines x0, x1 (the pivot's own line, final, and the next pivot's line, updated by the
 // chain).  C in D (row stride ld), operands from line L's buffer.
+// maxI: tiles of block-rows past it have not received their edges yet (the host entry's FW beside
+// the H2D, routing.hip FwOverlap): skipped, they catch up on this pivot when they arrive.
 template <class K, int T, int KC>
 __global__ void __launch_bounds__(256, 3) fw_bulk_lb(K* __restrict__ D, size_t ld, const K* __restrict__ lb, int L,
-                                                     int x0, int x1, LineMap lm, const int* __restrict__ tiles) {
+                                                     int x0, int x1, LineMap lm, const int* __restrict__ tiles,
+                                                     int maxI) {
     int I, J;
     tri_tile(lm.nb, tiles[blockIdx.x], I, J);
-    if (I == x0 || I == x1 || J == x0 || J == x1) return;  // whole workgroup
+    if (I == x0 || I == x1 || J == x0 || J == x1 || I > maxI) return;  // whole workgroup
     constexpr size_t TT = (size_t)T * T;
     fw_core<K, T, T, KC>(D + (size_t)I * T * ld + (size_t)J * T, ld, lb + lm.slot(I, L) * TT, I > L,
                          lb + lm.slot(J, L) * TT, J >= L, T, nullptr, 0);
+}
+
+// Late tiles (the host entry's FW beside the H2D, routing.hip FwOverlap; one rank, u32 keys): the
+// tiles (I, J >= I) of block-row I, whose edges landed after the bulks of pivots [0, P) ran without
+// them, catch up on pivot p = blockIdx.y:  D(I, J) = min(D(I, J), LB(p)[I] (x) LB(p)[J]), LB(p) the
+// FINAL line of p (kept for every pivot).  Blocked FW's bulk updates of a tile are independent of
+// one another once the lines are final, so this is exactly the skipped work, merged with atomicMin
+// (exact: min is associative; a read of D that already holds another pivot's contribution only
+// lowers this product's operand C, never below the true result).  I, J > p: both operands are
+// stored tiles (p, I), (p, J) read transposed / plain (acol, bcol as the bulk's).
+template <int T>
+__global__ void __launch_bounds__(256, 3) fw_catchup(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lball,
+                                                     size_t lb_stride, int I, int nb) {
+    constexpr int KC = 16;
+    constexpr size_t TT = (size_t)T * T;
+    const int J = I + (int)blockIdx.x, p = (int)blockIdx.y;
+    const uint32_t* lb = lball + (size_t)p * lb_stride;  // line p: tile j at slot j (one rank)
+    uint32_t* C = D + (size_t)I * T * ld + (size_t)J * T;
+    (void)nb;
+    fw_core_lb_e<T, T, KC, false>(C, ld, lb + (size_t)I * TT, true, lb + (size_t)J * TT, true, T,
+                                  [&](int r, int c, uint64_t bits) {
+                                      uint32_t* q = C + (size_t)r * ld + c;
+                                      atomicMin(q, (uint32_t)bits);
+                                      atomicMin(q + 1, (uint32_t)(bits >> 32));
+                                  });
 }
 
 // Line launches of the FW critical chain, one (T/S) x (T/S) sub-tile of a line tile per

@@ -267,12 +267,13 @@ __global__ void k_w_loss(uint64_t E, const uint32_t* __restrict__ src, const uin
 // u32 keys: one pass over the edges with a packed lexicographic key
 //   KW[s][t] = min over parallel edges of (latency << 32 | loss bits)    (mod.rs:305-313)
 // (loss in [0,1] is non-negative, so its f32 bit order is its numeric order).
+// (V: endpoints past it are skipped -- the FW beside the H2D builds W before the edge checks run)
 __global__ void k_w_key(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                         const uint64_t* __restrict__ lat, uint64_t unit, const float* __restrict__ loss,
-                        unsigned long long* __restrict__ KW, size_t ld) {
+                        unsigned long long* __restrict__ KW, size_t ld, uint32_t V = 0xFFFFFFFFu) {
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
-        if (s == t) continue;  // self-loops never shorten a path; kept for the diagonal only
+        if (s == t || s >= V || t >= V) continue;  // self-loops never shorten a path; kept for the diagonal only
         // null loss: latency only (WL is then built by k_w_loss once the losses have arrived)
         const uint64_t l = unit != 1 ? lat[e] / unit : lat[e];  // < 2^32-1: the u32 path's precondition
         const unsigned long long k = ((unsigned long long)l << 32) | (loss ? __float_as_uint(loss[e] + 0.0f) : 0u);
@@ -284,12 +285,13 @@ __global__ void k_w_key(uint64_t E, const uint32_t* __restrict__ src, const uint
 // and D (= W with a zero diagonal).  grid = (nb64, nb64) over the upper triangle incl. diagonal
 // blocks when undirected (each block pair handled once), all blocks when directed.
 // WL_ONLY: only WL is written (late loss: W and D were split from latency-only keys before FW)
+// (bi0: first 64-block row of the launch -- the FW beside the H2D splits a block-row at a time)
 template <bool WL_ONLY = false>
 __global__ void __launch_bounds__(256) k_w_split(const unsigned long long* __restrict__ KW, size_t ld, int directed,
                                                  uint32_t* __restrict__ W, uint32_t* __restrict__ WL,
-                                                 uint32_t* __restrict__ D) {
+                                                 uint32_t* __restrict__ D, uint32_t bi0 = 0) {
     __shared__ unsigned long long tb[64][65];
-    const uint32_t bi = blockIdx.y, bj = blockIdx.x;
+    const uint32_t bi = bi0 + blockIdx.y, bj = blockIdx.x;
     if (!directed && bj < bi) return;
     const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     if (!directed) {
@@ -721,6 +723,8 @@ struct srg_ctx {
                                         // two-stream schedule, -1 = auto (SRG_OPT_FW_STEP)
     DevBuf b_xlb, b_xflags;             // fused FW: three line buffers in one block, peers' arrival flags
     uint32_t xepoch = 0;                // fused FW with a device-side exchange: this build's flag value
+    hipEvent_t ev_ov = nullptr;         // FW beside the H2D: chunk landed
+    int fw_overlap = 1;                 // host entry: FW starts while the edge list arrives (SRG_OPT_FW_OVERLAP)
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -735,7 +739,7 @@ struct srg_ctx {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         for (uint32_t* p : sig)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate, ev_ov})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
             if (e) (void)hipEventDestroy(e);
@@ -1359,78 +1363,110 @@ inline void sym_tiles(srg_ctx& c, const Plan& pl, hipStream_t st, std::vector<in
     if (!own_h.empty()) HIP_CHECK(hipMemcpyAsync(tiles, own_h.data(), own_h.size() * 4, hipMemcpyHostToDevice, st));
 }
 
+// The schedule as a stepper: begin() builds line 0, pivot(kb, maxI) enqueues the chain of kb + 1 and
+// the bulk of kb (tiles of block-rows <= maxI), end() mirrors or exchanges.  fw_line_sym runs it
+// straight through; the host entry's FW beside the H2D (FwOverlap) runs pivots as block-rows of the
+// edge list land, with every line kept (keep_lines) for the late tiles' catch-up.
 template <class K, int T>
-void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
-                 int& prof_n, double& ms_xchg) {
-    constexpr int KCS = 16;
-    const int nb = pl.nb, G = pl.G, g = pl.g;
-    constexpr size_t TT = (size_t)T * T;
-    const bool multi = c.comm && c.comm->nranks > 1;
-    const LineMap lm{nb, G};
-    {
-        const char* hv = std::getenv("SRG_STREAM_HOPS");
-        std::lock_guard<std::mutex> lk(g_dev_mu);
-        c.hop_values = g_dev_ctx[c.device] == 1 && !(hv && std::strcmp(hv, "events") == 0);
-    }
-    const size_t lds_bulk = lb_lds<K, T, KCS>();
-    set_lds(fw_bulk_lb<K, T, KCS>, lds_bulk);
-    // The chain's line launches.  A large bulk (C3 on one rank: ~nb^2/2 = 3 160 tiles, four rounds
-    // of the chip's 768 slots) hides the chain, so the lines take whole tiles (the fewest CU slots
-    // taken from the bulk).  A bulk below ~2 rounds (several ranks, or a small graph) leaves the
-    // chain as the critical path: sub-tiles, S^2 x the workgroups at a fraction of the latency
-    // (SRG_OPT_FW_LINE_SPLIT; FW at sim 2:0 / 4:0 / 8:0 with whole tiles, quadrants, 32 x 32:
-    // 17.9 / 15.1 / 15.6, 14.9 / 12.2 / 12.1, 11.0 / 7.7 / 7.2 ms, profiles/r03c/, r03k/; one rank,
-    // C2 (nb = 32) 3.6 / 2.8 / 2.6 ms, C1 (nb = 8) 0.79 / 0.48 / 0.47 ms, profiles/r03x/).  The
-    // pivot closure is one launch of 64 workgroups either way (fw_close_sq; eight squaring launches
-    // took 45-117 us per pivot, the one-workgroup FW closure 159 us beside the bulk: r03b/).
-    const int bulk_tiles = nb * (nb + 1) / 2 / G;
-    const int split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
-    set_lds(fw_line_lb<K, T, 1>, lb_lds<K, T, line_kc<1>()>());
-    set_lds(fw_line_lb<K, T, 2>, lb_lds<K, T / 2, line_kc<2>()>());
-    set_lds(fw_line_lb<K, T, 4>, lb_lds<K, T / 4, line_kc<4>()>());
-    auto line = [&](K* lbL, int L, K* lbK, int K1, int mode, int tiles, hipStream_t s) {
-        if (!tiles) return;
-        if (split == 4)
-            fw_line_lb<K, T, 4><<<dim3(tiles, 16), 256, lb_lds<K, T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, kChainPrio);
-        else if (split == 2)
-            fw_line_lb<K, T, 2><<<dim3(tiles, 4), 256, lb_lds<K, T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, kChainPrio);
-        else
-            fw_line_lb<K, T, 1><<<dim3(tiles, 1), 256, lb_lds<K, T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, kChainPrio);
-    };
-    const bool prof = c.profiling && nb > 2;
-    if (prof) {
-        while (c.prof_events.size() < (size_t)2 * nb) {
-            hipEvent_t e;
-            HIP_CHECK(hipEventCreate(&e));
-            c.prof_events.push_back(e);
-        }
-    }
-    K* LB[2] = {(K*)c.b_L0.get(nb * TT * sizeof(K)), (K*)c.b_L1.get(nb * TT * sizeof(K))};
-    // closure barrier words: 16 per pivot (arrival counter, changed flag per step), then the
-    // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
-    uint32_t* cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
-    c.fw_timeout = cflags + (size_t)nb * 16;
-    HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
+struct SymFw {
+    static constexpr int KCS = 16;
+    static constexpr size_t TT = (size_t)T * T;
+    srg_ctx& c;
+    const Plan& pl;
+    K* D;
+    size_t Vp;
+    hipStream_t st;
+    int nb, G, g, split = 1, ntile = 0, prio = kChainPrio;
+    bool multi = false, prof = false, keep_lines = false;
+    LineMap lm{1, 1};
+    size_t lds_bulk = 0;
+    uint32_t* cflags = nullptr;
+    const int* tiles = nullptr;
     std::vector<int> own_h, slot_h, first;
-    sym_tiles(c, pl, st, own_h, slot_h, first);
-    const int ntile = (int)own_h.size();
-    const int* tiles = (const int*)c.b_tiles.p;
-    hipStream_t aux = c.aux_stream, cs = c.comm_stream;
-    const int prio = kChainPrio;
-    auto close_pivot = [&](K* lbk, int k, hipStream_t s) {
-        fw_close_sq<K, T><<<dim3(T / 16, T / 16), 256, 0, s>>>(lbk + (size_t)lm.slot(k, k) * TT, cflags + 16 * k,
-                                                             c.fw_timeout, prio);
-    };
-    // line 0: every rank holds the same initial D
-    k_pack_line<K, T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
-    close_pivot(LB[0], 0, st);
-    line(LB[0], 0, LB[0], 0, 1, nb, st);  // (with nb == 1 this only copies the closed pivot tile back to D)
-    HIP_CHECK(hipGetLastError());
-    for (int kb = 0; kb < nb; ++kb) {
+    K* lbuf[2] = {nullptr, nullptr};
+    K* lball = nullptr;  // keep_lines: line p at lball + p * nb * TT
+    uint64_t* prof_relax = nullptr;
+    int* prof_n = nullptr;
+
+    SymFw(srg_ctx& c_, const Plan& pl_, K* D_, size_t Vp_, hipStream_t st_) : c(c_), pl(pl_), D(D_), Vp(Vp_), st(st_) {
+        nb = pl.nb;
+        G = pl.G;
+        g = pl.g;
+        multi = c.comm && c.comm->nranks > 1;
+        lm = LineMap{nb, G};
+    }
+    K* lb(int p) const { return keep_lines ? lball + (size_t)p * nb * TT : lbuf[p & 1]; }
+    void line(const K* lbL, int L, K* lbK, int K1, int mode, int ntiles, hipStream_t s) const {
+        if (!ntiles) return;
+        if (split == 4)
+            fw_line_lb<K, T, 4><<<dim3(ntiles, 16), 256, lb_lds<K, T / 4, line_kc<4>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, prio);
+        else if (split == 2)
+            fw_line_lb<K, T, 2><<<dim3(ntiles, 4), 256, lb_lds<K, T / 2, line_kc<2>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, prio);
+        else
+            fw_line_lb<K, T, 1><<<dim3(ntiles, 1), 256, lb_lds<K, T, line_kc<1>()>(), s>>>(D, Vp, lbL, L, lbK, K1, mode, lm, g, prio);
+    }
+    void close_pivot(K* lbk, int k, hipStream_t s) const {
+        fw_close_sq<K, T><<<dim3(T / 16, T / 16), 256, 0, s>>>(lbk + (size_t)lm.slot(k, k) * TT, cflags + 16 * k, c.fw_timeout,
+                                                             prio);
+    }
+    void begin(uint64_t& relax, int& n) {
+        prof_relax = &relax;
+        prof_n = &n;
+        {
+            const char* hv = std::getenv("SRG_STREAM_HOPS");
+            std::lock_guard<std::mutex> lk(g_dev_mu);
+            c.hop_values = g_dev_ctx[c.device] == 1 && !(hv && std::strcmp(hv, "events") == 0);
+        }
+        lds_bulk = lb_lds<K, T, KCS>();
+        set_lds(fw_bulk_lb<K, T, KCS>, lds_bulk);
+        // The chain's line launches.  A large bulk (C3 on one rank: ~nb^2/2 = 3 160 tiles, four rounds
+        // of the chip's 768 slots) hides the chain, so the lines take whole tiles (the fewest CU slots
+        // taken from the bulk).  A bulk below ~2 rounds (several ranks, or a small graph) leaves the
+        // chain as the critical path: sub-tiles, S^2 x the workgroups at a fraction of the latency
+        // (SRG_OPT_FW_LINE_SPLIT; FW at sim 2:0 / 4:0 / 8:0 with whole tiles, quadrants, 32 x 32:
+        // 17.9 / 15.1 / 15.6, 14.9 / 12.2 / 12.1, 11.0 / 7.7 / 7.2 ms, profiles/r03c/, r03k/; one rank,
+        // C2 (nb = 32) 3.6 / 2.8 / 2.6 ms, C1 (nb = 8) 0.79 / 0.48 / 0.47 ms, profiles/r03x/).  The
+        // pivot closure is one launch of 64 workgroups either way (fw_close_sq; eight squaring launches
+        // took 45-117 us per pivot, the one-workgroup FW closure 159 us beside the bulk: r03b/).
+        const int bulk_tiles = nb * (nb + 1) / 2 / G;
+        split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
+        set_lds(fw_line_lb<K, T, 1>, lb_lds<K, T, line_kc<1>()>());
+        set_lds(fw_line_lb<K, T, 2>, lb_lds<K, T / 2, line_kc<2>()>());
+        set_lds(fw_line_lb<K, T, 4>, lb_lds<K, T / 4, line_kc<4>()>());
+        prof = c.profiling && nb > 2;
+        if (prof) {
+            while (c.prof_events.size() < (size_t)2 * nb) {
+                hipEvent_t e;
+                HIP_CHECK(hipEventCreate(&e));
+                c.prof_events.push_back(e);
+            }
+        }
+        if (keep_lines) lball = (K*)c.b_xlb.get((size_t)nb * nb * TT * sizeof(K));
+        else {
+            lbuf[0] = (K*)c.b_L0.get(nb * TT * sizeof(K));
+            lbuf[1] = (K*)c.b_L1.get(nb * TT * sizeof(K));
+        }
+        // closure barrier words: 16 per pivot (arrival counter, changed flag per step), then the
+        // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
+        cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
+        c.fw_timeout = cflags + (size_t)nb * 16;
+        HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
+        sym_tiles(c, pl, st, own_h, slot_h, first);
+        ntile = (int)own_h.size();
+        tiles = (const int*)c.b_tiles.p;
+        // line 0: every rank holds the same initial D
+        k_pack_line<K, T><<<nb, 256, 0, st>>>(D, Vp, lb(0), 0, lm);
+        close_pivot(lb(0), 0, st);
+        line(lb(0), 0, lb(0), 0, 1, nb, st);  // (with nb == 1 this only copies the closed pivot tile back to D)
+        HIP_CHECK(hipGetLastError());
+    }
+    // the chain of k1 = kb + 1 (aux stream) and the bulk of kb over block-rows <= maxI (main stream)
+    void pivot(int kb, int maxI) {
         const int k1 = kb + 1;
-        K* lbk = LB[kb & 1];
+        hipStream_t aux = c.aux_stream;
+        K* lbk = lb(kb);
         if (k1 < nb) {
-            K* lbn = LB[k1 & 1];
+            K* lbn = lb(k1);
             stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
             if (multi) {  // on the chain's own stream: no cross-queue hop around it
@@ -1446,9 +1482,10 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
             HIP_CHECK(hipGetLastError());
         }
         // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
-        const bool timed = prof && ntile > 0 && k1 < nb;
-        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        if (ntile > 0) fw_bulk_lb<K, T, KCS><<<ntile, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, tiles);
+        const bool timed = prof && ntile > 0 && k1 < nb && maxI >= nb - 1;
+        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * *prof_n], st));
+        if (ntile > 0)
+            fw_bulk_lb<K, T, KCS><<<ntile, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, tiles, maxI);
         HIP_CHECK(hipGetLastError());
         if (timed) {
             int64_t m = 0;  // relaxations of this launch: own tiles off lines kb and k1
@@ -1457,14 +1494,25 @@ void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, ui
                 tri_tile_h(nb, t, I, J);
                 if (I != kb && I != k1 && J != kb && J != k1) ++m;
             }
-            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
-            prof_relax += (uint64_t)m * T * T * T;
-            ++prof_n;
+            HIP_CHECK(hipEventRecord(c.prof_events[2 * *prof_n + 1], st));
+            *prof_relax += (uint64_t)m * T * T * T;
+            ++*prof_n;
         }
         if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
     }
-    HIP_CHECK(hipGetLastError());
-    fw_sym_finish<K, T>(c, pl, D, Vp, st, own_h, slot_h, first, ms_xchg);
+    void end(double& ms_xchg) {
+        HIP_CHECK(hipGetLastError());
+        fw_sym_finish<K, T>(c, pl, D, Vp, st, own_h, slot_h, first, ms_xchg);
+    }
+};
+
+template <class K, int T>
+void fw_line_sym(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax,
+                 int& prof_n, double& ms_xchg) {
+    SymFw<K, T> f(c, pl, D, Vp, st);
+    f.begin(prof_relax, prof_n);
+    for (int kb = 0; kb < f.nb; ++kb) f.pivot(kb, f.nb);
+    f.end(ms_xchg);
 }
 
 // End of the symmetric FW: mirror the lower triangle (one rank), or every rank ends with the whole D:
@@ -1719,10 +1767,117 @@ bool sym_fw_for(const srg_ctx& c, const DevGraph& g) {
            !g.directed;
 }
 
+// The host entry's FW beside the H2D (one rank, undirected graph, symmetric FW on u32
+// keys counted in ns).  A GML complete graph lists its edges by source row, each (s, d) with s <= d;
+// then block-row I of W (rows [128 I, 128 (I + 1))) is complete once the chunk holding the last edge
+// of its rows has landed, and block-row I is all that line I and the rows' tiles need.  Per chunk:
+// the chunk's latency-only keys into KW (k_w_key, on the H2D stream); per newly complete block-row:
+// its tiles split from KW into W / D (k_w_split) and caught up on the pivots whose bulks already ran
+// without them (fw_catchup, from the kept final lines); then every pivot whose line is complete is
+// enqueued (SymFw::pivot, bulk over the complete block-rows only).  FW thus starts while the list
+// is still arriving instead of after it (C3: the H2D is ~8 ms, host-bound on the codec's encoding).
+// Speculative: the keys are nanoseconds (latency unit 1) -- exact whatever the unit -- and the edge
+// checks run after the H2D as before (a failed check or certification discards this FW).  Any chunk
+// that is not sequential-pair, or an edge (s, d) with s > d or a source row going backwards,
+// abandons the overlap (ok = false): the build then runs from the landed edge list as usual.
+struct FwOverlap {
+    static constexpr int T = 128;
+    static constexpr size_t TT = (size_t)T * T;
+    srg_ctx* c = nullptr;
+    hipStream_t st = nullptr;   // FW (c.stream)
+    hipStream_t hs = nullptr;   // H2D chunks (c.comm_stream)
+    hipEvent_t ev = nullptr;
+    uint32_t V = 0;
+    size_t Vp = 0;
+    int nb = 0;
+    Plan pl;
+    std::unique_ptr<SymFw<uint32_t, T>> fw;
+    uint32_t *W = nullptr, *WL = nullptr, *D = nullptr;
+    unsigned long long* KW = nullptr;
+    int A = -1, next = 0;       // block-rows complete; pivots enqueued
+    bool on = false, ok = false, begun = false, ended = false;
+    uint32_t prev_src = 0;
+    uint64_t prof_relax = 0;
+    int prof_n = 0;
+    double ms_xchg = 0;
+
+    void init(srg_ctx& cc, uint32_t V_, const std::vector<uint32_t>& nodes_h) {
+        c = &cc;
+        st = cc.stream;
+        hs = cc.comm_stream;
+        V = V_;
+        Vp = ((size_t)V + T - 1) / T * T;
+        nb = (int)(Vp / T);
+        pl = make_plan(1, 0, V, T, nodes_h);
+        const size_t VV = Vp * Vp;
+        W = (uint32_t*)cc.b_W.get(VV * 4);
+        WL = (uint32_t*)cc.b_WL.get(VV * 4);
+        D = (uint32_t*)cc.b_D.get(VV * 4);
+        KW = (unsigned long long*)cc.b_PRED.get(VV * 8);
+        HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, hs));
+        if (!cc.ev_ov) HIP_CHECK(hipEventCreateWithFlags(&cc.ev_ov, hipEventDisableTiming));
+        ev = cc.ev_ov;
+        fw.reset(new SymFw<uint32_t, T>(cc, pl, D, Vp, st));
+        fw->keep_lines = true;
+        on = ok = true;
+    }
+    // a chunk's edges [e0, e0 + ne) are on the device (in hs order); exc = its exceptions (global
+    // index, src, dst) when sequential-pair, null otherwise
+    void chunk(const DevGraph& dg, size_t e0, size_t ne, const uint32_t* exc, size_t nexc, bool last) {
+        if (!ok) return;
+        bool good = exc != nullptr;
+        for (size_t k = 0; good && k < nexc; ++k) {
+            const uint32_t s = exc[3 * k + 1], d = exc[3 * k + 2];
+            good = s >= prev_src && s <= d;
+            prev_src = s;
+        }
+        if (!good) {
+            ok = false;
+            return;
+        }
+        k_w_key<<<grid_for(ne), kThreads, 0, hs>>>(ne, dg.src + e0, dg.dst + e0, dg.lat + e0, 1, nullptr, KW, Vp, V);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(ev, hs));
+        HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
+        // rows below the chunk's last source row are complete (all of them after the last chunk)
+        const int newA = last ? nb - 1 : std::min(nb - 1, (int)(prev_src / T) - 1);
+        advance(newA);
+    }
+    void advance(int newA) {
+        for (int I = A + 1; I <= newA; ++I) {
+            const unsigned nb64 = (unsigned)(Vp / 64);
+            k_w_split<false><<<dim3(nb64, 2), 256, 0, st>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
+            if (next > 0) {
+                set_lds(fw_catchup<T>, lb_lds<uint32_t, T, 16>());
+                fw_catchup<T><<<dim3(nb - I, next), 256, lb_lds<uint32_t, T, 16>(), st>>>(D, Vp, fw->lball, (size_t)nb * TT,
+                                                                                          I, nb);
+            }
+            HIP_CHECK(hipGetLastError());
+        }
+        A = std::max(A, newA);
+        if (A < 0) return;
+        if (!begun) {
+            fw->begin(prof_relax, prof_n);
+            begun = true;
+        }
+        while (next < nb && (next + 1 < nb ? A >= next + 1 : A >= nb - 1)) {
+            fw->pivot(next, A);
+            ++next;
+        }
+        if (next == nb && !ended) {
+            fw->end(ms_xchg);
+            ended = true;
+        }
+    }
+};
+
 // Dense path for key type K. Returns false (u32 only) when certification fails.
 template <class K, int T>
 bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
-               float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats, HostSink* sink) {
+               float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats, HostSink* sink,
+               FwOverlap* ov = nullptr) {
+    // the FW already ran beside the H2D (FwOverlap): W, D and the closed D are in place
+    const bool pre = ov && ov->on && ov->ok && ov->ended && sizeof(K) == 4 && T == FwOverlap::T;
     const uint32_t V = g.V;
     const size_t Vp = ((size_t)V + T - 1) / T * T;
     const size_t VV = Vp * Vp;
@@ -1735,7 +1890,9 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint32_t* WL = (uint32_t*)c.b_WL.get(VV * 4);
     K* D = (K*)c.b_D.get(VV * sizeof(K));
     bool wl_late = false;  // late loss: WL is built after FW, once the losses have landed
-    if constexpr (sizeof(K) == 4) {
+    if (pre) {
+        wl_late = g.late && !g.late->applied;
+    } else if constexpr (sizeof(K) == 4) {
         // packed (latency, loss) keys: one atomic pass, then a tiled symmetrize + split pass
         static_assert(T % 64 == 0, "tile");
         unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
@@ -1770,7 +1927,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     uint64_t prof_relax = 0;
     int prof_n = 0;
     double ms_dx = 0;  // multi-rank: D exchange at the end of FW (inside ms_fw, also in ms_exchange)
-    if (sym_fw_for<K, T>(c, g)) {
+    if (pre) {
+        prof_relax = ov->prof_relax;
+        prof_n = ov->prof_n;
+    } else if (sym_fw_for<K, T>(c, g)) {
         if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64)) {
             const int xm = fw_step_mode(c);
             if (xm >= 0) fw_line_fused<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx, xm);
@@ -2407,7 +2567,8 @@ bool choose_sparse(const srg_ctx& c, const DevGraph& g) {
 }
 
 void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
-                    float* out_loss, hipStream_t st, srg_stats* stats, HostSink* sink = nullptr) {
+                    float* out_loss, hipStream_t st, srg_stats* stats, HostSink* sink = nullptr,
+                    FwOverlap* ov = nullptr) {
     HIP_CHECK(hipStreamSynchronize(c.aux_stream));  // nothing of an aborted call still writes WL / PRED
     if (g.V == 0) {
         if (n) fail(SRG_ERR_ARG, "nodes given for an empty graph");
@@ -2423,6 +2584,10 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     // are key * unit -- exact.  SRG_LATENCY_UNIT=1 keeps nanosecond keys (tests, A/B).
     const char* lu = std::getenv("SRG_LATENCY_UNIT");
     P.unit = (P.es.unit > 1 && !(lu && std::strcmp(lu, "1") == 0)) ? P.es.unit : 1;
+    // the FW that ran beside the H2D counted nanoseconds (exact for any unit; its certification
+    // decides as usual, a failure reruns on the u64 keys)
+    const bool pre = ov && ov->on && ov->ok && ov->ended && P.es.max_lat < 0xFFFFFFFFull;
+    if (pre) P.unit = 1;
     P.max_key = P.es.max_lat / P.unit;
     if (stats) stats->latency_unit_ns = P.unit;
     const unsigned __int128 bound = (unsigned __int128)P.max_key * (g.V > 1 ? g.V - 1 : 1);
@@ -2435,7 +2600,9 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
         loss_arrive(g, P.selfloss, st);
         if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
     }
-    if (P.max_key < 0xFFFFFFFFull) {
+    if (pre) {
+        if (run_dense<uint32_t, FwOverlap::T>(c, g, ov->pl, nodes, n, out_lat, out_loss, st, P, stats, sink, ov)) return;
+    } else if (P.max_key < 0xFFFFFFFFull) {
         // FW tile: 128 (more work per launch) on one GPU; the multi-rank schedule is bound by
         // the per-pivot chain (close pivot -> panels), whose latency scales with T^3
         const int tile = c.fw_tile ? c.fw_tile : 128;
@@ -2598,8 +2765,11 @@ __global__ void k_widen_edges(size_t n, const uint16_t* __restrict__ s16, const 
 // the device.  Host threads narrow chunk i+1 into a page-locked ring while chunk i is in flight.
 // Returns false (nothing usable staged) when an endpoint >= 65536 or a latency >= 2^32 is seen:
 // the caller then ships the plain arrays, whose checks report such edges as the reference does.
+// on_chunk(e0, ne, exc, nexc, last): edges [e0, e0 + ne) are decoded on the device (in st order); exc =
+// their exceptions (global index, src, dst) when the chunk went sequential-pair, else null
+using ChunkFn = std::function<void(size_t, size_t, const uint32_t*, size_t, bool)>;
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
-              bool& all_narrow, bool& all_seq);
+              bool& all_narrow, bool& all_seq, const ChunkFn& on_chunk = nullptr);
 
 // Sequential-pair codec, device side: edge i of a chunk is (src, dst) = (es[j], ed[j] + i - ei[j])
 // for the last exception j with ei[j] <= i (ei[0] = 0: a chunk starts with one), latency = l32[i].
@@ -2662,7 +2832,7 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
 // exceptions (GLOBAL edge index, src, dst) in c.slice_exc -- the edge-sharded exchange then ships
 // that form (4 B per edge) instead of the u16 narrowing (8 B).
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
-              bool& all_narrow, bool& all_seq) {
+              bool& all_narrow, bool& all_seq, const ChunkFn& on_chunk) {
     all_narrow = true;
     all_seq = false;
     c.slice_exc.clear();
@@ -2778,6 +2948,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             for (int w = 0; w < nwk; ++w) nexc += c.codec_ex[w].size() / 3;
             uint32_t* hx = (uint32_t*)hs;
             size_t q = 0;
+            const size_t x0 = c.slice_exc.size();
             for (int w = 0; w < nwk; ++w) {
                 const std::vector<uint32_t>& ex = c.codec_ex[w];
                 for (size_t k = 0; k + 2 < ex.size(); k += 3, ++q) {
@@ -2796,6 +2967,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             k_decode_seq<<<grid_for(ne), kThreads, 0, st>>>(ne, l32 + e0, dexc, (uint32_t)nexc, (uint32_t*)dg.src + e0,
                                                              (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
             ++seq_chunks;
+            if (on_chunk) on_chunk(e0, ne, c.slice_exc.data() + x0, nexc, ch + 1 == nch && !slow);
         } else {
             HIP_CHECK(hipMemcpyAsync(s16 + e0, hs, ne * 2, hipMemcpyHostToDevice, st));
             HIP_CHECK(hipMemcpyAsync(d16 + e0, hd, ne * 2, hipMemcpyHostToDevice, st));
@@ -2804,6 +2976,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             HIP_CHECK(hipEventRecord(c.ev_ring[b], st));
             k_widen_edges<<<grid_for(ne), kThreads, 0, st>>>(ne, s16 + e0, d16 + e0, l32 + e0, (uint32_t*)dg.src + e0,
                                                               (uint32_t*)dg.dst + e0, (uint64_t*)dg.lat + e0);
+            if (on_chunk) on_chunk(e0, ne, nullptr, 0, ch + 1 == nch && !slow);
         }
         HIP_CHECK(hipGetLastError());
         if (slow) {
@@ -2814,6 +2987,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             if (with_loss)
                 HIP_CHECK(hipMemcpyAsync((float*)dg.loss + r0, g->packet_loss + r0, rn * 4, hipMemcpyHostToDevice, st));
             if (dbg) std::fprintf(stderr, "codec: host slow after chunk %zu (%.2f ms), rest plain\n", ch, dt);
+            if (on_chunk) on_chunk(r0, rn, nullptr, 0, true);
             all_narrow = false;
             break;
         }
@@ -2976,13 +3150,37 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // the W build and FW (dense u32 path: WL is built from them on c->loss_stream)
         const bool want_late = c->late_loss && !direct && !shard;
         bool all_narrow = false, all_seq = false;
+        // FW beside the H2D (FwOverlap): one rank, undirected, the dense symmetric two-stream FW on
+        // 128-tiles, the codec with late losses; the chunks then cross on the comm stream (idle on
+        // one rank) while FW runs on the main stream
+        FwOverlap ov;
+        {
+            DevGraph probe{g->num_vertices, (int)g->directed, E};
+            const bool ov_want = c->fw_overlap && !direct && nr == 1 && want_late && c->h2d_codec && E >= ((size_t)1 << 20) &&
+                                 !g->directed && c->fw_symmetric && (c->fw_tile == 0 || c->fw_tile == 128) &&
+                                 g->num_vertices >= 256 && n > 0 && !choose_sparse(*c, probe) && fw_step_mode(*c) < 0;
+            if (ov_want) {
+                HIP_CHECK(hipStreamSynchronize(c->aux_stream));  // nothing of an aborted call still runs
+                ov.init(*c, g->num_vertices, std::vector<uint32_t>(nodes, nodes + n));
+            }
+        }
+        const hipStream_t hst = ov.on ? c->comm_stream : st;
+        ChunkFn on_chunk = nullptr;
+        if (ov.on) on_chunk = [&](size_t e0, size_t ne, const uint32_t* exc, size_t nexc, bool last) {
+            ov.chunk(dg, e0, ne, exc, nexc, last);
+        };
         // (V > 65536: only a row-ordered list, through the sequential-pair chunks, can be narrowed;
         // codec_in gives up on the first chunk that is neither)
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) &&
-                           codec_in(*c, g, dg, st, a0, a1, !want_late, all_narrow, all_seq);
+                           codec_in(*c, g, dg, hst, a0, a1, !want_late, all_narrow, all_seq, on_chunk);
+        if (ov.on && !coded) ov.ok = false;
+        const int ov_early = ov.next;  // pivots enqueued while chunks were still crossing
+        if (ov.on && ov.ok && !ov.ended) ov.advance(ov.nb - 1);
+        if (ov.on && std::getenv("SRG_DEBUG_OVERLAP"))
+            std::fprintf(stderr, "fw-overlap: ok=%d pivots_during_h2d=%d of %d\n", ov.ok ? 1 : 0, ov_early, ov.nb);
         LateLoss late;
         late.ls = c->loss_stream;
-        if (coded && want_late) start_late_loss(*c, g, dg, st, late);
+        if (coded && want_late) start_late_loss(*c, g, dg, hst, late);
         if (!coded) {
             const size_t cnt = std::max<size_t>(E, 1);
             dg.src = (uint32_t*)c->b_src.get(cnt * 4);
@@ -3096,7 +3294,11 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 gather(dg.loss, 4);
             }
         }
-        const uint32_t* dn = stage_in(c->b_nodes, nodes, n, st);
+        const uint32_t* dn = stage_in(c->b_nodes, nodes, n, hst);
+        if (hst != st) {  // the main stream's later work reads the landed edges and nodes
+            HIP_CHECK(hipEventRecord(c->ev_c, hst));
+            HIP_CHECK(hipStreamWaitEvent(st, c->ev_c, 0));
+        }
         // multi-rank without the output exchange: the device holds only this rank's rows [p0, p1)
         // (the plan's split, make_plan / run_sparse); dol / dos then point p0 rows before that
         // allocation, so the kernels' absolute row indices land in it (C4 at 8 ranks: 3.75 GB per
@@ -3109,7 +3311,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                                                     q0 * n * 8);
         float* dos = reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(c->b_oloss.get(std::max<size_t>(dev_nn, 1) * 4)) -
                                               q0 * n * 4);
-        HIP_CHECK(hipStreamSynchronize(st));
+        HIP_CHECK(hipStreamSynchronize(hst));  // (beside FW when it started early: st still runs it)
         const double ms_h2d = ms_since(t0);
         HostSink sink;
         sink.lat = out_lat;
@@ -3142,7 +3344,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         c->own_row0 = 0;
         c->own_row1 = ~(size_t)0;
         if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
-        else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr);
+        else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr, ov.on ? &ov : nullptr);
         if (dg.late) {  // a path that never read the losses (error-free early return): drain
             dg.late->join();
             HIP_CHECK(hipStreamSynchronize(c->loss_stream));
@@ -3321,6 +3523,10 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1 && value != -1) return SRG_ERR_ARG;
             ctx->fw_step = (int)value;
             return SRG_OK;
+        case SRG_OPT_FW_OVERLAP:
+            if (value != 0 && value != 1) return SRG_ERR_ARG;
+            ctx->fw_overlap = (int)value;
+            return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
             ctx->algorithm = (int)value;
@@ -3354,6 +3560,7 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_LATE_LOSS: *value = ctx->late_loss; break;
         case SRG_OPT_FW_LINE_SPLIT: *value = ctx->fw_line_split; break;
         case SRG_OPT_FW_STEP: *value = ctx->fw_step; break;
+        case SRG_OPT_FW_OVERLAP: *value = ctx->fw_overlap; break;
         default: return SRG_ERR_ARG;
     }
     return SRG_OK;

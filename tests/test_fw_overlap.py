@@ -1,0 +1,117 @@
+"""The host entry's FW beside the H2D (routing.hip FwOverlap, SRG_OPT_FW_OVERLAP): on an edge list
+ordered by source row with s <= d on every edge (a GML complete graph), FW pivots run while later
+chunks are still crossing, and block-rows that land late catch up on the pivots already run.  The
+table must be byte-identical to the build that starts FW after the H2D, and every list that breaks
+the preconditions (shuffled, disordered late, a bad endpoint, keys past the u32 range) must fall
+back to it by itself."""
+import numpy as np
+import pytest
+
+import oracle
+from shadow_amd import NetGraphError, Router, synth
+from shadow_amd import _native as N
+from shadow_amd.graph import Edges
+from helpers import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def build(e, nodes, overlap):
+    r = Router(0)
+    r.set_option(N.SRG_OPT_FW_OVERLAP, overlap)
+    try:
+        return r.compute_shortest_paths(e, nodes)
+    finally:
+        r.close()
+
+
+def same(a, b):
+    return np.array_equal(a.latency_ns, b.latency_ns) and bits_equal(a.packet_loss, b.packet_loss)
+
+
+@pytest.mark.parametrize("V", [2100, 3000])
+def test_overlap_matches_after_h2d(V, monkeypatch, capfd):
+    e = synth.atlas_like(V, seed=V + 1)
+    nodes = list(range(V))
+    monkeypatch.setenv("SRG_DEBUG_OVERLAP", "1")
+    t1 = build(e, nodes, 1)
+    err = capfd.readouterr().err
+    assert "fw-overlap: ok=1" in err, err
+    t0 = build(e, nodes, 0)
+    assert same(t1, t0)
+    rows = [0, V // 2, V - 1]
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, mode=2)
+    assert np.array_equal(t1.latency_ns[rows], lat) and bits_equal(t1.packet_loss[rows], loss)
+
+
+def test_overlap_subset_nodes_and_pivots_during_h2d(monkeypatch, capfd):
+    """A scrambled subset of used nodes; some pivots must have been enqueued before the last chunk."""
+    V = 3000
+    e = synth.atlas_like(V, seed=77)
+    nodes = np.random.default_rng(5).permutation(V)[: V // 3].tolist()
+    monkeypatch.setenv("SRG_DEBUG_OVERLAP", "1")
+    t1 = build(e, nodes, 1)
+    err = capfd.readouterr().err
+    early = int(err.split("pivots_during_h2d=")[1].split()[0])
+    assert "ok=1" in err and early > 0, err
+    assert same(t1, build(e, nodes, 0))
+
+
+@pytest.mark.parametrize("how", ["shuffled", "late_reversed", "late_backwards_row"])
+def test_overlap_falls_back(how, monkeypatch, capfd):
+    V = 2100
+    e = synth.atlas_like(V, seed=9)
+    src, dst, lat, loss = e.src.copy(), e.dst.copy(), e.latency_ns.copy(), e.packet_loss.copy()
+    if how == "shuffled":
+        p = np.random.default_rng(1).permutation(e.num_edges)
+        src, dst, lat, loss = src[p], dst[p], lat[p], loss[p]
+    elif how == "late_reversed":  # the last 1000 edges listed as (d, s): a lower-triangle entry
+        src[-1000:], dst[-1000:] = e.dst[-1000:], e.src[-1000:]
+    else:  # the last row block moved in front of an earlier one (rows going backwards)
+        k = e.num_edges - 5000
+        src = np.r_[src[:k - 5000], src[k:], src[k - 5000:k]]
+        dst = np.r_[dst[:k - 5000], dst[k:], dst[k - 5000:k]]
+        lat = np.r_[lat[:k - 5000], lat[k:], lat[k - 5000:k]]
+        loss = np.r_[loss[:k - 5000], loss[k:], loss[k - 5000:k]]
+    g = Edges(V, src, dst, lat, loss, False)
+    nodes = list(range(0, V, 3))
+    monkeypatch.setenv("SRG_DEBUG_OVERLAP", "1")
+    t1 = build(g, nodes, 1)
+    err = capfd.readouterr().err
+    assert "ok=0" in err or "fw-overlap" not in err, err
+    assert same(t1, build(g, nodes, 0))
+    rows = [0, 5]
+    ref_lat, ref_loss = oracle.compute_shortest_paths(g.as_tuple(), nodes, rows=rows, mode=2)
+    assert np.array_equal(t1.latency_ns[rows], ref_lat) and bits_equal(t1.packet_loss[rows], ref_loss)
+
+
+def test_overlap_error_in_last_chunk():
+    """An endpoint out of range in the last chunk: the edge checks after the H2D report the reference's
+    error exactly as without the overlap (the FW already enqueued is discarded)."""
+    V = 2100
+    e = synth.atlas_like(V, seed=10)
+    dst = e.dst.copy()
+    dst[-1] = V
+    g = Edges(V, e.src, dst, e.latency_ns, e.packet_loss, False)
+    codes = []
+    for ov in (1, 0):
+        r = Router(0)
+        r.set_option(N.SRG_OPT_FW_OVERLAP, ov)
+        with pytest.raises(NetGraphError) as ei:
+            r.compute_shortest_paths(g, list(range(V)))
+        codes.append((ei.value.code, str(ei.value)))
+        r.close()
+    assert codes[0] == codes[1] and codes[0][0] == N.SRG_ERR_ARG
+
+
+def test_overlap_u32_range_rerun():
+    """Latencies x 1000: nanosecond keys saturate (used paths past 2^31 ns), so the overlapped build's
+    certification fails and it reruns on the u64 keys; the table equals the build after the H2D
+    (which keeps u32 keys in units of the latencies' gcd)."""
+    V = 2100
+    e = synth.atlas_like(V, seed=11)
+    e.latency_ns = e.latency_ns * np.uint64(1000)
+    nodes = list(range(0, V, 5))
+    t1 = build(e, nodes, 1)
+    t0 = build(e, nodes, 0)
+    assert same(t1, t0)
