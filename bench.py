@@ -84,21 +84,40 @@ def cpu_rate(edges, target_s, threads, mode, seed=12345):
     return done / spent, done, spent, setup
 
 
-def cpu_baselines(edges, target_s, desc):
+def cpu_fixed(edges, k, threads, mode, seed=12345, step=32):
+    """Sources/s of an oracle pipeline over a FIXED seeded sample of k sources (256),
+    timed in slices of `step` sources so that progress is logged; setup excluded."""
+    import numpy as np
+    import oracle
+    g = edges.as_tuple()
+    V = edges.num_vertices
+    nodes = np.arange(V, dtype=np.uint32)
+    sample = np.random.default_rng(seed).choice(V, size=min(k, V), replace=False).astype(np.uint32)
+    spent = 0.0
+    for i in range(0, len(sample), step):
+        t, _ = oracle.time_sources_mode(g, nodes, sample[i:i + step], nthreads=threads, mode=mode)
+        spent += t
+        log(f"cpu baseline mode {mode}: {min(i + step, len(sample))}/{len(sample)} sources in {spent:.1f}s")
+    return len(sample) / spent, len(sample), spent
+
+
+def cpu_baselines(edges, target_s, desc, sources=256):
     """SURVEY §8(d) CPU baseline on the box's host cores: the reference-equivalent pipeline
     (HashMap-score petgraph Dijkstra + linear nodes.contains + HashMap merge, like rayon x
-    petgraph, mod.rs:190-208) and a CPU-best variant (dense scores, O(1) membership, dense rows;
-    the dense-matrix Dijkstra on dense graphs).  Both on a bounded random sample of sources,
-    extrapolated to all sources at the measured per-source rate."""
+    petgraph, mod.rs:190-208) on a fixed seeded sample of `sources` sources (256, as §8(d) asks),
+    and a CPU-best variant (dense scores, O(1) membership, dense rows; the dense-matrix Dijkstra
+    on dense graphs) on a bounded sample; both extrapolated to all sources at the measured
+    per-source rate."""
     info = cpu_info()
     th = info["threads"]
     V = edges.num_vertices
     dense = edges.num_edges * 8 > V * V
-    ref, k0, s0, _ = cpu_rate(edges, target_s, th, 0)
+    ref, k0, s0 = cpu_fixed(edges, sources, th, 0)
     best, k1, s1, setup1 = cpu_rate(edges, max(3.0, target_s / 2), th, 2 if dense else 1)
     return {"value": round(ref, 3), "unit": "source-SSSPs/s", "cores": th, "kind": "port",
-            "sample": f"{k0} random sources of {desc}, reference-equivalent pipeline (HashMap-score petgraph "
-                      f"Dijkstra + linear nodes.contains + HashMap merge, mod.rs:190-208) on {th} threads, {s0:.1f}s",
+            "sample": f"fixed seeded sample of {k0} sources of {desc} (SURVEY §8d), reference-equivalent pipeline "
+                      f"(HashMap-score petgraph Dijkstra + linear nodes.contains + HashMap merge, mod.rs:190-208) on "
+                      f"{th} threads, {s0:.1f}s",
             "extrapolated": True, "full_run_estimate_s": round(V / ref, 1),
             **info,
             "best": {"value": round(best, 3), "unit": "source-SSSPs/s", "cores": th,
@@ -476,7 +495,9 @@ def main():
                     help="multiply every edge latency by this factor (e.g. 1000 puts C3's used paths past "
                          "2^31 ns; the latency unit then keeps u32 keys in units of the latencies' gcd, and "
                          "SRG_LATENCY_UNIT=1 in the environment forces nanosecond keys: the u64 path benchmark)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-best baseline: time budget of its sample")
+    ap.add_argument("--cpu-sources", type=int, default=256,
+                    help="reference-equivalent CPU baseline: fixed seeded sample of sources (SURVEY §8d: 256)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the 4 oracle rows checked after the timed steps")
@@ -666,7 +687,7 @@ def main():
         return
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baselines(edges, args.cpu_seconds, gdesc.split(":")[0])
+        cpu = cpu_baselines(edges, args.cpu_seconds, gdesc.split(":")[0], args.cpu_sources)
     ver = None
     if world > 1:
         dist.barrier()  # every rank's rows are in the shared table

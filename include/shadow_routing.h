@@ -83,7 +83,9 @@ typedef struct srg_stats {
     uint64_t relaxations;       /* min-plus relaxations issued by the FW kernels */
     uint64_t essential_edges;   /* edges with W[u][t] == D[u][t] (candidates for tightness) */
     int32_t scan_kind;          /* SRG_SCAN_* below */
-    int32_t reserved;
+    int32_t table_keys;         /* srg_routing_info_build: 1 = the table kept the build's u32 latency keys
+                                   (latency = key x latency_unit_ns; 0.4 GB less D2H and host memory at C3),
+                                   0 = u64 ns (u64-key builds, several ranks, direct paths) */
     /* filled only when profiling is enabled (SRG_OPT_PROFILING): HIP events recorded on the
      * launch stream around every launch of the dominant kernel (FW phase-3 product).      */
     uint64_t prof_launches;     /* profiled launches */

@@ -121,7 +121,7 @@ class Stats(ctypes.Structure):
         ("relaxations", ctypes.c_uint64),
         ("essential_edges", ctypes.c_uint64),
         ("scan_kind", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("table_keys", ctypes.c_int32),
         ("prof_launches", ctypes.c_uint64),
         ("prof_kernel_ms", ctypes.c_double),
         ("prof_relaxations", ctypes.c_uint64),

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../../include/shadow_routing.h"
+#include "internal.h"
 #include "kernels.hip.h"
 #include "edge_codec.h"
 #include "tight_sparse.hip.h"
@@ -455,7 +456,10 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
                                                  const uint32_t* __restrict__ rowpos,
                                                  const uint64_t* __restrict__ self_lat, const float* __restrict__ self_loss,
                                                  uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags,
-                                                 int mode, uint64_t unit) {
+                                                 int mode, uint64_t unit, uint32_t* __restrict__ out_key = nullptr,
+                                                 uint64_t* __restrict__ out_diag = nullptr) {
+    // out_key (RoutingInfo's key table, srg_internal_compute_keys): latencies as u32 keys instead of
+    // ns (0xFFFFFFFF on the diagonal, whose raw self-loop latency goes to out_diag)
     // mode bit 0: latency (+ unreachable check), bit 1: loss from L; one workgroup per local row a,
     // U columns per thread in flight (the gathers are latency-bound)
     const uint32_t a = blockIdx.x;
@@ -463,6 +467,7 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
     const K* Ds = D + (size_t)s * ld;
     const float* La = L ? L + (size_t)a * ld : nullptr;
     uint64_t* ol = out_lat + (size_t)p * ncols;
+    uint32_t* ok = out_key ? out_key + (size_t)p * ncols : nullptr;
     float* os = out_loss + (size_t)p * ncols;
     uint32_t unreach = 0;
     constexpr uint32_t U = 4;
@@ -486,12 +491,20 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
             if (b >= ncols) break;
             if (p == b) {
                 // raw self-loop weight, no 1-(1-p) rounding (mod.rs:211-217)
-                if (mode & 1) ol[b] = self_lat[s];
+                if (mode & 1) {
+                    if (ok) {
+                        ok[b] = 0xFFFFFFFFu;
+                        out_diag[p] = self_lat[s];
+                    } else {
+                        ol[b] = self_lat[s];
+                    }
+                }
                 if (mode & 2) os[b] = self_loss[s];
             } else {
                 if (mode & 1) {
                     unreach |= d[u] == KeyOps<K>::INF;
-                    ol[b] = (uint64_t)d[u] * unit;
+                    if (ok) ok[b] = (uint32_t)d[u];
+                    else ol[b] = (uint64_t)d[u] * unit;
                 }
                 if (mode & 2) os[b] = l[u];
             }
@@ -511,6 +524,18 @@ __global__ void k_min_u64(const uint64_t* __restrict__ a, size_t count, unsigned
         m = o < m ? o : m;
     }
     if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(out, m);
+}
+
+// min over a key table (the diagonal's 0xFFFFFFFF excluded by being the maximum)
+__global__ void k_min_u32(const uint32_t* __restrict__ a, size_t count, unsigned long long* out) {
+    uint32_t m = 0xFFFFFFFFu;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+        m = a[i] < m ? a[i] : m;
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = __shfl_down(m, off, 64);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != 0xFFFFFFFFu) atomicMin(out, (unsigned long long)m);
 }
 
 __global__ void k_positions(const uint32_t* __restrict__ nodes, uint32_t n, int32_t* __restrict__ pos) {
@@ -724,6 +749,9 @@ struct srg_ctx {
     DevBuf b_xlb, b_xflags;             // fused FW: three line buffers in one block, peers' arrival flags
     uint32_t xepoch = 0;                // fused FW with a device-side exchange: this build's flag value
     hipEvent_t ev_ov = nullptr;         // FW beside the H2D: chunk landed
+    uint32_t* kout_key = nullptr;       // this call's RoutingInfo key table on the device (key mode), and
+    uint64_t* kout_diag = nullptr;      // its diagonal (raw self-loop latencies per position)
+    DevBuf b_odiag;
     int fw_overlap = 1;                 // host entry: FW starts while the edge list arrives (SRG_OPT_FW_OVERLAP)
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
@@ -732,7 +760,7 @@ struct srg_ctx {
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
-                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc,
+                          &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc, &b_odiag,
                           &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
@@ -1878,6 +1906,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                FwOverlap* ov = nullptr) {
     // the FW already ran beside the H2D (FwOverlap): W, D and the closed D are in place
     const bool pre = ov && ov->on && ov->ok && ov->ended && sizeof(K) == 4 && T == FwOverlap::T;
+    if (sizeof(K) == 8 && c.kout_key)  // a key table needs the u32 keys
+        fail(SRG_INTERNAL_NEED_U64, "the build needs u64 latency keys: no u32 key table");
     const uint32_t V = g.V;
     const size_t Vp = ((size_t)V + T - 1) / T * T;
     const size_t VV = Vp * Vp;
@@ -2071,7 +2101,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     if (nloc)
         k_extract<K><<<nloc, kThreads, 0, st>>>(D, nullptr, Vp, lnodes, nloc, nodes, n, lpos,
                                                                       P.selflat, P.selfloss, out_lat, out_loss,
-                                                                      P.flags, 1, P.unit);
+                                                                      P.flags, 1, P.unit, c.kout_key, c.kout_diag);
     HIP_CHECK(hipGetLastError());
     if (reduce_flag(&P.flags->unreachable_used_pair)) {
         if (sizeof(K) == 8 && P.range_risk)
@@ -2087,7 +2117,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // final -- they leave during the scan / loss pass
     const bool sink_rows = sink && !exchange && nloc && sink->ok();
     if (sink_rows) {
-        sink->send_rows(st, out_lat, sink->lat, pl.p0, nloc, 8);
+        if (c.kout_key) sink->send_rows(st, c.kout_key, sink->lat, pl.p0, nloc, 4);  // (sink->lat: the host key table)
+        else sink->send_rows(st, out_lat, sink->lat, pl.p0, nloc, 8);
         sink->lat_sent = true;
     }
 
@@ -2487,7 +2518,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         }
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
-                     selflat, selfloss, out_lat, out_loss, fl, P.unit, 0xFFFFFFFFu, 0u, gb};
+                     selflat, selfloss, out_lat, out_loss, fl, P.unit, 0xFFFFFFFFu, 0u, gb, c.kout_key, c.kout_diag};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
@@ -3065,9 +3096,17 @@ int guard(char* errbuf, size_t errlen, const std::function<void()>& body) {
     }
 }
 
+// out_key / out_diag (srg_internal_compute_keys, RoutingInfo's key table): non-null = the latencies
+// leave as the build's u32 keys plus the diagonal's raw self-loop latencies; out_lat is unused then
 int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32_t num_nodes, uint64_t* out_lat,
-               float* out_loss, srg_stats* stats, char* errbuf, size_t errlen, bool direct) {
-    if (!c || !g || (num_nodes && (!nodes || !out_lat || !out_loss)) ||
+               float* out_loss, srg_stats* stats, char* errbuf, size_t errlen, bool direct,
+               uint32_t* out_key = nullptr, uint64_t* out_diag = nullptr) {
+    const bool keys = out_key != nullptr;
+    if (keys && (direct || (c && c->comm && c->comm->nranks > 1) || !out_diag)) {
+        set_err(errbuf, errlen, "key table: one rank, shortest paths only");
+        return SRG_ERR_ARG;
+    }
+    if (!c || !g || (num_nodes && (!nodes || !(out_lat || keys) || !out_loss)) ||
         (g->num_edges && (!g->src || !g->dst || !g->latency_ns || !g->packet_loss))) {
         set_err(errbuf, errlen, "null argument");
         return SRG_ERR_ARG;
@@ -3109,9 +3148,11 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
     const bool rows_part = !direct && c->comm && c->comm->nranks > 1 && !c->gather_output;
     const size_t reg_r0 = rows_part ? (size_t)num_nodes * c->comm->rank / c->comm->nranks : 0;
     const size_t reg_r1 = rows_part ? (size_t)num_nodes * (c->comm->rank + 1) / c->comm->nranks : num_nodes;
+    const size_t lat_elem = keys ? 4 : 8;
+    unsigned char* out_lat_b = keys ? (unsigned char*)out_key : (unsigned char*)out_lat;  // the latency table
     if (early && !ext) {
-        reg.p[0] = out_lat + reg_r0 * num_nodes;
-        reg.b[0] = (reg_r1 - reg_r0) * num_nodes * 8;
+        reg.p[0] = out_lat_b + reg_r0 * num_nodes * lat_elem;
+        reg.b[0] = (reg_r1 - reg_r0) * num_nodes * lat_elem;
         reg.p[1] = out_loss + reg_r0 * num_nodes;
         reg.b[1] = (reg_r1 - reg_r0) * num_nodes * 4;
         reg.th = std::thread([&reg]() {
@@ -3313,8 +3354,18 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                                               q0 * n * 4);
         HIP_CHECK(hipStreamSynchronize(hst));  // (beside FW when it started early: st still runs it)
         const double ms_h2d = ms_since(t0);
+        // key mode: the device key table in the latency buffer's room, the diagonal beside it; the
+        // kernels see them through the context for this call
+        uint32_t* dkey = keys ? reinterpret_cast<uint32_t*>(dol) : nullptr;
+        uint64_t* ddiag = keys ? (uint64_t*)c->b_odiag.get(std::max<size_t>(n, 1) * 8) : nullptr;
+        struct KeyScope {
+            srg_ctx* c;
+            ~KeyScope() { c->kout_key = nullptr, c->kout_diag = nullptr; }
+        } key_scope{c};
+        c->kout_key = dkey;
+        c->kout_diag = ddiag;
         HostSink sink;
-        sink.lat = out_lat;
+        sink.lat = keys ? reinterpret_cast<uint64_t*>(out_key) : out_lat;  // (a host table pointer either way)
         sink.loss = out_loss;
         sink.n = n;
         sink.cs = c->d2h_stream;
@@ -3358,17 +3409,34 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         auto t1 = std::chrono::steady_clock::now();
         unsigned long long hmin = ~0ull;
         if (rows_nn && stats) {  // smallest latency over the table (feeds the runahead, manager.rs:238-243)
-            unsigned long long* dmin = (unsigned long long*)c->b_multi.get(8);
-            HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 8, st));
-            k_min_u64<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dol + rows_off, rows_nn, dmin);
-            rb_async(*c, MS_MIN, dmin, st);
+            unsigned long long* dmin = (unsigned long long*)c->b_multi.get(16);
+            HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 16, st));
+            if (keys) {  // smallest key (x unit below) and smallest diagonal latency
+                k_min_u32<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dkey + rows_off, rows_nn, dmin);
+                k_min_u64<<<grid_for(n, 1024), kThreads, 0, st>>>(ddiag, n, dmin + 1);
+            } else {
+                k_min_u64<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dol + rows_off, rows_nn, dmin);
+            }
+            HIP_CHECK(hipMemcpyAsync(c->hbox + 64 * MS_MIN, dmin, 16, hipMemcpyDeviceToHost, st));
         }
-        if (rows_nn && !sink.lat_sent)
-            HIP_CHECK(hipMemcpyAsync(out_lat + rows_off, dol + rows_off, rows_nn * 8, hipMemcpyDeviceToHost, st));
+        if (rows_nn && !sink.lat_sent) {
+            if (keys)
+                HIP_CHECK(hipMemcpyAsync(out_key + rows_off, dkey + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
+            else
+                HIP_CHECK(hipMemcpyAsync(out_lat + rows_off, dol + rows_off, rows_nn * 8, hipMemcpyDeviceToHost, st));
+        }
+        if (keys && n) HIP_CHECK(hipMemcpyAsync(out_diag, ddiag, n * 8, hipMemcpyDeviceToHost, st));
         if (rows_nn && !sink.loss_sent)
             HIP_CHECK(hipMemcpyAsync(out_loss + rows_off, dos + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
-        if (rows_nn && stats) hmin = rb_get<unsigned long long>(*c, MS_MIN);
+        if (rows_nn && stats) {
+            hmin = rb_get<unsigned long long>(*c, MS_MIN);
+            if (keys) {
+                const unsigned long long dmin = *reinterpret_cast<const unsigned long long*>(c->hbox + 64 * MS_MIN + 8);
+                const uint64_t unit = stats->latency_unit_ns ? stats->latency_unit_ns : 1;
+                hmin = std::min<unsigned long long>(hmin == ~0ull ? ~0ull : hmin * unit, dmin);
+            }
+        }
         sink.finish();
         if (stats) {
             stats->ms_h2d = ms_h2d;
@@ -3574,6 +3642,16 @@ void srg_destroy(srg_ctx* ctx) {
         --g_dev_ctx[ctx->device];
     }
     delete ctx;
+}
+
+int srg_internal_compute_keys(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
+                              uint32_t* out_key, uint64_t* out_diag, float* out_loss, uint64_t* unit_ns,
+                              srg_stats* stats, char* errbuf, size_t errlen) {
+    srg_stats local{};
+    srg_stats* st = stats ? stats : &local;
+    const int rc = host_entry(ctx, graph, nodes, num_nodes, nullptr, out_loss, st, errbuf, errlen, false, out_key, out_diag);
+    if (unit_ns) *unit_ns = st->latency_unit_ns ? st->latency_unit_ns : 1;
+    return rc;
 }
 
 int srg_compute_shortest_paths(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/shadow_routing.h"
+#include "internal.h"
 
 namespace {
 
@@ -49,9 +50,16 @@ struct Counters {
 struct srg_routing_info {
     uint32_t n = 0;
     std::vector<uint32_t> ids;       // GML id per position
-    // [n x n] tables, left uninitialised (every entry is written by the build; no 1.2 GB memset)
+    // [n x n] tables, left uninitialised (every entry is written by the build; no 1.2 GB memset).
+    // Latencies are kept either as the build's certified u32 keys (key = latency / unit, exact; the
+    // diagonal's raw self-loop latencies in diag) -- 0.4 GB less D2H and host memory at C3 -- or,
+    // when the build needed u64 keys or ran on several ranks, as u64 ns in lat.
     std::unique_ptr<uint64_t[]> lat;
+    std::unique_ptr<uint32_t[]> key;
+    std::vector<uint64_t> diag;
+    uint64_t unit = 1;
     std::unique_ptr<float[]> loss;
+    std::once_flag widened;          // tables(): the u64 view of a key table, built on first use
     uint64_t min_lat = UINT64_MAX;
     // GML id -> position: a direct table when the ids are dense enough, else a hash map
     std::vector<uint32_t> pos_direct;
@@ -69,9 +77,13 @@ namespace {
 
 // compute(nodes, n, out_lat, out_loss, stats, errbuf, errlen): one of the host entry points
 using Compute = std::function<int(const uint32_t*, uint32_t, uint64_t*, float*, srg_stats*, char*, size_t)>;
+// compute_keys(nodes, n, out_key, out_diag, out_loss, unit, stats, errbuf, errlen): the key-table entry
+using ComputeKeys = std::function<int(const uint32_t*, uint32_t, uint32_t*, uint64_t*, float*, uint64_t*, srg_stats*,
+                                      char*, size_t)>;
 
-int build_routing_info(const Compute& compute, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
-                       int use_shortest_paths, srg_routing_info** out, srg_stats* stats, char* errbuf, size_t errlen) {
+int build_routing_info(const Compute& compute, const ComputeKeys& compute_keys, const srg_edge_list* graph,
+                       const uint32_t* gml_ids, uint32_t num_ids, int use_shortest_paths, srg_routing_info** out,
+                       srg_stats* stats, char* errbuf, size_t errlen) {
     *out = nullptr;
     try {
         // node_id_to_index (mod.rs:126-128): GML id -> NodeIndex, later duplicate ids win (:161)
@@ -94,11 +106,25 @@ int build_routing_info(const Compute& compute, const srg_edge_list* graph, const
         ri->n = num_ids;
         ri->ids.assign(gml_ids, gml_ids + num_ids);
         const size_t nn = (size_t)num_ids * num_ids;
-        ri->lat.reset(new uint64_t[std::max<size_t>(nn, 1)]);
         ri->loss.reset(new float[std::max<size_t>(nn, 1)]);
         srg_stats local{};
         srg_stats* st = stats ? stats : &local;
-        const int rc = compute(nodes.data(), num_ids, ri->lat.get(), ri->loss.get(), st, errbuf, errlen);
+        int rc = SRG_INTERNAL_NEED_U64;
+        if (compute_keys) {
+            ri->key.reset(new uint32_t[std::max<size_t>(nn, 1)]);
+            ri->diag.resize(num_ids);
+            rc = compute_keys(nodes.data(), num_ids, ri->key.get(), ri->diag.data(), ri->loss.get(), &ri->unit, st,
+                              errbuf, errlen);
+            if (rc == SRG_INTERNAL_NEED_U64) {
+                ri->key.reset();
+                ri->diag.clear();
+                ri->unit = 1;
+            }
+        }
+        if (rc == SRG_INTERNAL_NEED_U64) {
+            ri->lat.reset(new uint64_t[std::max<size_t>(nn, 1)]);
+            rc = compute(nodes.data(), num_ids, ri->lat.get(), ri->loss.get(), st, errbuf, errlen);
+        }
         if (rc != SRG_OK) {
             delete ri;
             // .context("Failed to compute shortest paths between graph nodes") (sim_config.rs:446-447)
@@ -113,6 +139,7 @@ int build_routing_info(const Compute& compute, const srg_edge_list* graph, const
         }
         ri->min_lat = st->min_latency_ns;
         if (!use_shortest_paths) ri->min_lat = nn ? *std::min_element(ri->lat.get(), ri->lat.get() + nn) : UINT64_MAX;
+        if (stats) stats->table_keys = ri->key ? 1 : 0;
         uint32_t max_id = 0;
         for (uint32_t id : ri->ids) max_id = std::max(max_id, id);
         if (num_ids && (uint64_t)max_id < std::max<uint64_t>(1u << 20, 16ull * num_ids)) {
@@ -171,7 +198,14 @@ int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint3
         return use_shortest_paths ? srg_compute_shortest_paths(ctx, graph, nodes, n, lat, loss, st, eb, el)
                                   : srg_get_direct_paths(ctx, graph, nodes, n, lat, loss, st, eb, el);
     };
-    return build_routing_info(f, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
+    // one rank, shortest paths: the table stays in the build's u32 keys
+    ComputeKeys fk = nullptr;
+    if (use_shortest_paths && nr == 1)
+        fk = [&](const uint32_t* nodes, uint32_t n, uint32_t* key, uint64_t* diag, float* loss, uint64_t* unit,
+                 srg_stats* st, char* eb, size_t el) {
+            return srg_internal_compute_keys(ctx, graph, nodes, n, key, diag, loss, unit, st, eb, el);
+        };
+    return build_routing_info(f, fk, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
 }
 
 int srg_routing_info_build_multi(srg_multi* m, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
@@ -185,7 +219,7 @@ int srg_routing_info_build_multi(srg_multi* m, const srg_edge_list* graph, const
         return use_shortest_paths ? srg_multi_compute_shortest_paths(m, graph, nodes, n, lat, loss, st, eb, el)
                                   : srg_multi_get_direct_paths(m, graph, nodes, n, lat, loss, st, eb, el);
     };
-    return build_routing_info(f, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
+    return build_routing_info(f, nullptr, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
 }
 
 void srg_routing_info_free(srg_routing_info* ri) { delete ri; }
@@ -198,7 +232,7 @@ int srg_routing_info_path(const srg_routing_info* ri, uint32_t start, uint32_t e
     const uint32_t a = ri->pos(start), b = ri->pos(end);
     if (a == NO_POS || b == NO_POS) return 0;  // paths.get(&(start, end)) == None
     const size_t k = (size_t)a * ri->n + b;
-    if (latency_ns) *latency_ns = ri->lat[k];
+    if (latency_ns) *latency_ns = !ri->key ? ri->lat[k] : a == b ? ri->diag[a] : (uint64_t)ri->key[k] * ri->unit;
     if (packet_loss) *packet_loss = ri->loss[k];
     return 1;
 }
@@ -229,6 +263,19 @@ int srg_routing_info_smallest_latency_ns(const srg_routing_info* ri, uint64_t* o
 
 void srg_routing_info_tables(const srg_routing_info* ri, const uint64_t** latency_ns, const float** packet_loss,
                              const uint32_t** gml_ids, uint32_t* n) {
+    if (latency_ns && ri && ri->key) {  // a key table: its u64 view, widened once (exact: key * unit)
+        auto* m = const_cast<srg_routing_info*>(ri);
+        std::call_once(m->widened, [m] {
+            const size_t nn = (size_t)m->n * m->n;
+            m->lat.reset(new uint64_t[std::max<size_t>(nn, 1)]);
+            for (uint32_t a = 0; a < m->n; ++a) {
+                const uint32_t* kr = m->key.get() + (size_t)a * m->n;
+                uint64_t* lr = m->lat.get() + (size_t)a * m->n;
+                for (uint32_t b = 0; b < m->n; ++b) lr[b] = (uint64_t)kr[b] * m->unit;
+                lr[a] = m->diag[a];
+            }
+        });
+    }
     if (latency_ns) *latency_ns = ri ? ri->lat.get() : nullptr;
     if (packet_loss) *packet_loss = ri ? ri->loss.get() : nullptr;
     if (gml_ids) *gml_ids = ri ? ri->ids.data() : nullptr;

@@ -127,6 +127,8 @@ struct SparseArgs {
     uint32_t delta;              // bucket width in latency units (0xFFFFFFFF = one bucket: plain Bellman-Ford)
     uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
+    uint32_t* out_key;           // RoutingInfo key table (null: ns latencies into out_lat), diagonal 0xFFFFFFFF
+    uint64_t* out_diag;          // with out_key: the raw self-loop latency per output row
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
@@ -474,7 +476,12 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                     ol = (uint64_t)lat * a.unit;
                     os = __uint_as_float((uint32_t)l);
                 }
-                a.out_lat[(size_t)row * a.ncols + j] = ol;
+                if (a.out_key) {
+                    a.out_key[(size_t)row * a.ncols + j] = j == row ? 0xFFFFFFFFu : (uint32_t)(l >> 32);
+                    if (j == row) a.out_diag[row] = ol;
+                } else {
+                    a.out_lat[(size_t)row * a.ncols + j] = ol;
+                }
                 a.out_loss[(size_t)row * a.ncols + j] = os;
             }
             __syncthreads();

@@ -1,0 +1,67 @@
+"""RoutingInfo (mod.rs:428-477, sim_config.rs:425-462) kept in the build's certified u32 latency keys
+(srg_routing_info_build, one rank): path() widens key x latency unit exactly, the diagonal is the raw
+self-loop latency, get_smallest_latency_ns covers both, tables() gives the widened u64 view -- all
+equal to the u64 host-entry table.  Builds that need u64 keys keep a u64 table (table_keys = 0)."""
+import numpy as np
+import pytest
+
+from shadow_amd import Router, generate_routing_info, synth
+from shadow_amd import _native as N
+from shadow_amd.graph import Edges
+
+pytestmark = pytest.mark.gpu
+
+
+def check(e, ids, expect_keys, router=None):
+    r = router or Router(0)
+    t = r.compute_shortest_paths(e, ids)
+    ri = generate_routing_info(e, ids, True, r)
+    assert ri.stats["table_keys"] == expect_keys
+    tl, tf, tid = ri.tables()
+    pos = {int(x): i for i, x in enumerate(tid.tolist())}
+    order = [pos[i] for i in ids]
+    assert np.array_equal(tl[np.ix_(order, order)], t.latency_ns)
+    assert np.array_equal(tf[np.ix_(order, order)].view(np.uint32), t.packet_loss.view(np.uint32))
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        a, b = rng.choice(len(ids), 2)
+        p = ri.path(ids[a], ids[b])
+        assert p.latency_ns == int(t.latency_ns[a, b]) and np.float32(p.packet_loss) == t.packet_loss[a, b]
+    a = int(rng.integers(len(ids)))
+    assert ri.path(ids[a], ids[a]).latency_ns == int(t.latency_ns[a, a])  # raw self-loop
+    assert ri.get_smallest_latency_ns() == int(t.latency_ns.min())
+    return ri
+
+
+def test_keys_ms_unit_graph():
+    """Millisecond latencies (unit 10^6 ns): keys count ms, the self-loops are sub-ms (not multiples
+    of the unit) -- the diagonal must come from the raw self-loop latencies."""
+    e = synth.random_graph(400, 0.1, 5, lat_lo=1, lat_hi=300)
+    lat = e.latency_ns * np.uint64(10 ** 6)
+    lat[e.src == e.dst] = 123_457  # raw self-loop latency, not a multiple of the unit
+    g = Edges(400, e.src, e.dst, lat, e.packet_loss, False)
+    ri = check(g, list(range(0, 400, 2)), 1)
+    assert ri.get_smallest_latency_ns() == 123_457
+
+
+def test_keys_large_dense_table():
+    """C2-sized atlas table through the early-D2H path (u32 rows shipped while the scan runs)."""
+    e = synth.atlas_like(2600, seed=26)
+    ids = np.random.default_rng(3).permutation(2600).tolist()
+    check(e, ids, 1)
+
+
+def test_keys_sparse_path():
+    """Sparse graphs (V >= 2048, batched Bellman-Ford) write the key table from the sparse kernel."""
+    e = synth.barabasi_albert(3000, 3, seed=30)
+    r = Router(0)
+    t = r.compute_shortest_paths(e, list(range(3000)))
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U32
+    check(e, list(range(0, 3000, 3)), 1, r)
+
+
+def test_u64_build_keeps_u64_table(monkeypatch):
+    """Nanosecond keys with paths past 2^31 units run on u64 keys: the table stays u64."""
+    monkeypatch.setenv("SRG_LATENCY_UNIT", "1")
+    e = synth.random_graph(300, 0.1, 7, lat_lo=2 ** 31, lat_hi=2 ** 33)
+    check(e, list(range(300)), 0)
