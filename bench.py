@@ -369,6 +369,34 @@ def cold_call(make, args, edges, V):
     return router, ms
 
 
+def routing_info_times(edges, V, args, steps=3):
+    """What Shadow's call site runs (sim_config.rs:425-462 -> RoutingInfo, mod.rs:428-477): one
+    srg_routing_info_build per simulation.  cold = srg_create + the first build (fresh context, fresh
+    host tables); steady = further builds on the same context, each into fresh tables (a RoutingInfo
+    owns its tables).  One rank: the table keeps the build's u32 keys (stats.table_keys)."""
+    import numpy as np
+    from shadow_amd import Router, generate_routing_info
+    ids = list(range(V))
+    t0 = time.perf_counter()
+    r = Router(0)
+    apply_options(r, args)
+    ri = generate_routing_info(edges, ids, True, r)
+    cold = (time.perf_counter() - t0) * 1e3
+    keys = ri.stats.get("table_keys")
+    ri.close()
+    ts = []
+    for _ in range(steps):
+        t1 = time.perf_counter()
+        ri = generate_routing_info(edges, ids, True, r)
+        ts.append((time.perf_counter() - t1) * 1e3)
+        st = ri.stats
+        ri.close()
+    r.close()
+    return {"cold_ms": round(cold, 1), "steady_ms": round(float(np.median(ts)), 2),
+            "steady_ms_all": [round(x, 2) for x in ts], "table_keys": keys,
+            "h2d_ms": round(st["ms_h2d"], 2), "d2h_tail_ms": round(st["ms_d2h"], 2)}
+
+
 def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg, extra):
     n = args.steps
     brk = ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")
@@ -501,6 +529,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the 4 oracle rows checked after the timed steps")
+    ap.add_argument("--no-ri", action="store_true", help="skip the RoutingInfo build times (cold / steady)")
     ap.add_argument("--graph", choices=["atlas", "complete", "ba", "events"], default="atlas",
                     help="atlas = C3 (headline; C2 with --vertices 4096), complete = C1, ba = C4, "
                          "events = C5 stretch (10^7 packet events)")
@@ -685,6 +714,11 @@ def main():
                           "breakdown_ms": {k: round(agg.get(k, 0) / n, 3) for k in brk},
                           "roofline": roofline}), flush=True)
         return
+    # RoutingInfo builds (Shadow's call site) beside the host-entry headline, one rank
+    ri_times = None
+    if args.entry == "host" and world == 1 and not args.simulate_rank and not args.no_ri:
+        ri_times = routing_info_times(edges, V, args)
+        log(f"[rank {rank}] routing info: {ri_times}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baselines(edges, args.cpu_seconds, gdesc.split(":")[0], args.cpu_sources)
@@ -708,7 +742,8 @@ def main():
         if cold_ms is not None:
             extra_cfg["cold_call_ms"] = round(cold_ms, 1)
         emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg,
-             {"device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None, "verified_rows": ver})
+             {"device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None, "verified_rows": ver,
+              "routing_info": ri_times})
     if world > 1:
         dist.barrier()
         if shm is not None and rank == 0:

@@ -796,6 +796,10 @@ struct LateLoss {
     hipEvent_t ev_done = nullptr;  // the losses and the self-loop losses are on the device
     bool joined = false, applied = false;
     std::string err;
+    // edge-sharded host entry: each rank shipped only its slice's losses; they are exchanged when
+    // first read (loss_arrive, at the same point on every rank): allgatherv with these segments
+    srg::Comm* comm = nullptr;
+    std::vector<size_t> offs, lens;
     void join() {
         if (!joined) {
             if (th.joinable()) th.join();
@@ -829,6 +833,7 @@ void loss_arrive(const DevGraph& g, float* self_loss, hipStream_t s) {
     L->join();  // every loss chunk is queued and ev_in recorded
     if (!L->applied) {
         HIP_CHECK(hipStreamWaitEvent(s, L->ev_in, 0));
+        if (L->comm) L->comm->allgatherv(const_cast<float*>(g.loss), L->offs.data(), L->lens.data(), s);
         if (g.E) k_self_loss<<<grid_for(g.E), kThreads, 0, s>>>(g.E, g.src, g.dst, g.loss, g.V, self_loss);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipEventRecord(L->ev_done, s));
@@ -2867,6 +2872,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     all_narrow = true;
     all_seq = false;
     c.slice_exc.clear();
+    const auto t_setup = std::chrono::steady_clock::now();
     const size_t E = g->num_edges, A = a1 - a0;
     constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
     constexpr int NB = 3;                   // ring slots
@@ -2894,6 +2900,7 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     dg.dst = (uint32_t*)c.b_dst.get(E * 4);
     dg.lat = (uint64_t*)c.b_lat.get(E * 8);
     dg.loss = (float*)c.b_loss.get(E * 4);
+    const double ms_setup = ms_since(t_setup);  // (first call: worker threads, pinned ring, device arrays)
     std::atomic<bool> bad{false};     // a latency >= 2^32: the codec cannot carry the list
     std::atomic<bool> bad_ep{false};  // an endpoint >= 65536: only the sequential-pair chunks can
     const bool dbg = std::getenv("SRG_DEBUG_CODEC") != nullptr;
@@ -3025,15 +3032,16 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     }
     if (seq_chunks) all_narrow = false;  // (the endpoints are not on the device narrowed)
     all_seq = seq_chunks == nch && nch > 0;
-    if (dbg) std::fprintf(stderr, "codec: %zu chunks (%zu sequential-pair), %d threads, convert %.2f ms, slot waits %.2f ms\n",
-                          nch, seq_chunks, c.pool->size(), t_conv, t_wait);
+    if (dbg) std::fprintf(stderr, "codec: %zu chunks (%zu sequential-pair), %d threads, setup %.2f ms, convert %.2f ms, slot waits %.2f ms\n",
+                          nch, seq_chunks, c.pool->size(), ms_setup, t_conv, t_wait);
     return true;
 }
 
 // Late loss H2D: a helper thread copies the losses chunk by chunk into a pinned ring and queues
 // each chunk's DMA on c.loss_stream behind the last endpoint/latency chunk (so the two never
 // share the PCIe link); loss_arrive() later joins it and orders the readers after the last DMA.
-void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, LateLoss& L) {
+void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, LateLoss& L, size_t a0 = 0,
+                     size_t a1 = ~(size_t)0) {
     constexpr size_t CE = (size_t)2 << 20;
     constexpr int NB = 3;
     if (!c.h_lring) HIP_CHECK(hipHostMalloc(&c.h_lring, CE * 4 * NB, hipHostMallocDefault));
@@ -3045,14 +3053,14 @@ void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream
     HIP_CHECK(hipStreamWaitEvent(c.loss_stream, c.ev_ledges, 0));
     dg.late = &L;
     const int device = c.device;
-    L.th = std::thread([&c, g, &dg, &L, device]() {
+    L.th = std::thread([&c, g, &dg, &L, device, a0, a1]() {
         constexpr size_t CE = (size_t)2 << 20;  // losses per chunk (8 MB)
         constexpr int NB = 3;
         try {
             HIP_CHECK(hipSetDevice(device));
-            const size_t E = g->num_edges;
+            const size_t E = std::min<size_t>(g->num_edges, a1);  // this rank's slice [a0, E)
             float* dloss = const_cast<float*>(dg.loss);
-            for (size_t ch = 0, e0 = 0; e0 < E; ++ch, e0 += CE) {
+            for (size_t ch = 0, e0 = a0; e0 < E; ++ch, e0 += CE) {
                 const int b = (int)(ch % NB);
                 if (ch >= (size_t)NB) HIP_CHECK(hipEventSynchronize(c.ev_lring[b]));
                 const size_t ne = std::min(CE, E - e0);
@@ -3189,7 +3197,9 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // narrowed edge list over PCIe when it fits (falls back to the plain arrays otherwise)
         // late loss: the losses follow the endpoints and latencies on their own stream, beside
         // the W build and FW (dense u32 path: WL is built from them on c->loss_stream)
-        const bool want_late = c->late_loss && !direct && !shard;
+        // (edge-sharded ranks ship their slices' losses late too; the slices are exchanged when
+        // the losses are first read, after FW -- loss_arrive)
+        const bool want_late = c->late_loss && !direct;
         bool all_narrow = false, all_seq = false;
         // FW beside the H2D (FwOverlap): one rank, undirected, the dense symmetric two-stream FW on
         // 128-tiles, the codec with late losses; the chunks then cross on the comm stream (idle on
@@ -3221,7 +3231,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             std::fprintf(stderr, "fw-overlap: ok=%d pivots_during_h2d=%d of %d\n", ov.ok ? 1 : 0, ov_early, ov.nb);
         LateLoss late;
         late.ls = c->loss_stream;
-        if (coded && want_late) start_late_loss(*c, g, dg, hst, late);
+        if (coded && want_late) start_late_loss(*c, g, dg, hst, late, a0, a1);
         if (!coded) {
             const size_t cnt = std::max<size_t>(E, 1);
             dg.src = (uint32_t*)c->b_src.get(cnt * 4);
@@ -3268,6 +3278,21 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             // the narrowest form every rank has: 0 = sequential-pair (each slice's u32 latencies +
             // exceptions: 4 B per edge with the loss 8), 1 = u16 narrowing (8 B, 12 with the loss),
             // 2 = plain (a rank shipped its slice plain: 20 B)
+            // forms 0 / 1: every rank is coded, so every rank ships its losses late -- exchanged when
+            // first read (loss_arrive); else now
+            auto late_or_gather_loss = [&]() {
+                if (dg.late) {
+                    dg.late->comm = c->comm;
+                    dg.late->offs.resize(nr);
+                    dg.late->lens.resize(nr);
+                    for (int q = 0; q < nr; ++q) {
+                        dg.late->offs[q] = E * q / nr * 4;
+                        dg.late->lens[q] = (E * (q + 1) / nr - E * q / nr) * 4;
+                    }
+                } else {
+                    gather(dg.loss, 4);
+                }
+            };
             uint32_t* plain = (uint32_t*)c->b_red.get(16);
             const uint32_t mine = !coded ? 2u : all_seq ? 0u : all_narrow ? 1u : 2u;
             HIP_CHECK(hipMemcpyAsync(plain, &mine, 4, hipMemcpyHostToDevice, st));
@@ -3306,7 +3331,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 c->comm->allgatherv(xb, offs.data(), lens.data(), st);
                 uint32_t* l32 = (uint32_t*)c->b_n32l.p;
                 gather(l32, 4);
-                gather(dg.loss, 4);
+                late_or_gather_loss();
                 for (auto [e0, e1] : {std::pair<size_t, size_t>{0, a0}, std::pair<size_t, size_t>{a1, E}})
                     if (e1 > e0 && !sim)
                         k_decode_seq_global<<<grid_for(e1 - e0), kThreads, 0, st>>>(
@@ -3320,7 +3345,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 gather(s16, 2);
                 gather(d16, 2);
                 gather(l32, 4);
-                gather(dg.loss, 4);
+                late_or_gather_loss();
                 // (a simulated rank received nothing: its other slices are the wide ones put once)
                 for (auto [e0, e1] : {std::pair<size_t, size_t>{0, a0}, std::pair<size_t, size_t>{a1, E}})
                     if (e1 > e0 && !sim)
@@ -3332,6 +3357,10 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                 gather(dg.src, 4);
                 gather(dg.dst, 4);
                 gather(dg.lat, 8);
+                if (dg.late) {  // (some rank shipped plain: no late exchange; this rank's losses first)
+                    dg.late->join();
+                    HIP_CHECK(hipStreamWaitEvent(st, dg.late->ev_in, 0));
+                }
                 gather(dg.loss, 4);
             }
         }
@@ -3461,8 +3490,16 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
     *out = nullptr;
     srg_ctx* c = nullptr;
     int rc = guard(errbuf, errlen, [&]() {
+        // SRG_DEBUG_CREATE: where srg_create's time goes (the cold call Shadow pays once)
+        const bool dbg = std::getenv("SRG_DEBUG_CREATE") != nullptr;
+        auto tc = std::chrono::steady_clock::now();
+        auto lap = [&](const char* what) {
+            if (dbg) std::fprintf(stderr, "srg_create: %-28s %7.2f ms\n", what, ms_since(tc));
+            tc = std::chrono::steady_clock::now();
+        };
         int count = 0;
         hipError_t e = hipGetDeviceCount(&count);
+        lap("hipGetDeviceCount");
         if (e != hipSuccess || count == 0)
             fail(SRG_ERR_HIP, std::string("no HIP device available (") + hipGetErrorString(e) +
                                   "); the routing builder has no CPU fallback");
@@ -3470,6 +3507,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c = new srg_ctx();
         c->device = device;
         HIP_CHECK(hipSetDevice(device));
+        lap("hipSetDevice");
         HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         // the FW lookahead chain (pivot close, row/col panels) is latency-critical: its workgroups
         // should be dispatched ahead of the bulk phase-3 tiles
@@ -3478,8 +3516,11 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+        lap("streams");
         HIP_CHECK(hipHostMalloc((void**)&c->hbox, 64 * kMailSlots, hipHostMallocDefault));
+        lap("mailbox");
         c->sdma.init(device);  // SDMA engine for the host entry's early D2H (else hipMemcpyAsync)
+        lap("sdma agents");
         // the late-loss H2D and WL build share the D2H stream (idle until FW ends): a fifth
         // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
         // serialise the W build and FW behind the loss DMAs (measured: build 1.0 -> 3.6 ms)
@@ -3493,6 +3534,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
             HIP_CHECK(hipStreamWriteValue32(c->stream, c->sig[1], 0, 0));
             HIP_CHECK(hipStreamSynchronize(c->stream));
         }
+        lap("events, signals");
         std::lock_guard<std::mutex> lk(g_dev_mu);
         ++g_dev_ctx[device];
     });

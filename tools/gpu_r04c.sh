@@ -13,3 +13,6 @@ for ov in 1 0 1 0; do
   grep "fw-overlap" $out/c3_ov$ov.err | tail -1
 done
 bash tools/gpu_trace_step.sh ${1:-r04c}_trace
+timeout -k 10 400 python -u -m pytest -m gpu -x -v --timeout 250 --timeout-method thread tests/test_routing_info_keys.py > $out/pytest_ri.log 2>&1 || { echo "ri tests failed"; tail -60 $out/pytest_ri.log; exit 1; }
+tail -4 $out/pytest_ri.log
+SRG_DEBUG_CREATE=1 SRG_DEBUG_CODEC=1 timeout -k 10 200 python3 -u tools/cold_probe2.py > $out/cold.json 2> $out/cold.err && cat $out/cold.json && grep -E "srg_create|codec" $out/cold.err | head -20
