@@ -36,7 +36,7 @@ constexpr int kMaxPeers = 16;
 
 // sync words of one pivot (16 u32, zeroed per build): closure barrier + changed flags, arrivals,
 // go, closure done
-enum StepSync { SS_CLOSE = 0, SS_ARRIVE = 9, SS_GO = 10, SS_CDONE = 11 };
+enum StepSync { SS_CLOSE = 0, SS_ARRIVE = 9, SS_GO = 10, SS_CDONE = 11, SS_DNEXT = 12 };
 
 template <class K>
 struct StepArgs {
@@ -187,6 +187,9 @@ __device__ __forceinline__ void wg_wait(const uint32_t* p, int sys, uint32_t* ti
 }
 
 template <class K, int T, int SL>
+__device__ __forceinline__ void help_d(const StepArgs<K>& a);
+
+template <class K, int T, int SL>
 __device__ __forceinline__ void chain(const StepArgs<K>& a, int w) {
     const LineMap& lm = a.lm;
     const int CH = a.CH, G = lm.G;
@@ -255,13 +258,28 @@ __device__ __forceinline__ void chain(const StepArgs<K>& a, int w) {
     } else {
         wg_wait(&sy[SS_CDONE], 0, a.timeout, [](uint32_t v) { return v != 0; });
     }
-    // ---- D: the whole line w.r.t. its closed pivot ---------------------------------------------
-    const int nD = lm.nb * SS;
-    for (int i = w; i < nD; i += CH) {
-        line_item<K, T, SL>(a, 1, i / SS, i % SS);
-        __syncthreads();
-    }
+    // ---- D: the whole line w.r.t. its closed pivot (shared with bulk workgroups that are free) ----
+    help_d<K, T, SL>(a);
     trace_max(a.trace, TR_CHAIN_END);
+}
+
+// Phase D's items are dealt from a counter: the chain workgroups take them once the pivot is closed,
+// and so does every bulk workgroup that finds the closure done when its own tile is finished -- the
+// line w.r.t. its closed pivot is the launch's critical path, the bulk is not.
+template <class K, int T, int SL>
+__device__ __forceinline__ void help_d(const StepArgs<K>& a) {
+    constexpr int SS = SL * SL;
+    __shared__ int s_item;
+    const int nD = a.lm.nb * SS;
+    for (;;) {
+        if (threadIdx.x == 0) s_item = (int)__hip_atomic_fetch_add(&a.sync[SS_DNEXT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int i = s_item;
+        __syncthreads();
+        if (i >= nD) break;
+        line_item<K, T, SL>(a, 1, i / SS, i % SS);
+        __syncthreads();  // the LDS image is reused by the next item
+    }
 }
 
 // bulk item: this rank's stored tile (sub-tile q of SB x SB) off lines kb and k1, operands LB(kb)
@@ -298,6 +316,17 @@ __global__ void __launch_bounds__(256, SB == 1 ? 3 : 4) fw_step(StepArgs<K> a) {
     if (w >= a.CH) {
         bulk_item<K, T, SB>(a, w - a.CH);
         trace_max(a.trace, TR_BULK_END);
+        // free now: help with the chain's last phase if the pivot is already closed
+        if (a.k1 >= 0) {
+            __shared__ uint32_t s_cd;
+            if (threadIdx.x == 0) s_cd = __hip_atomic_load(&a.sync[SS_CDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (s_cd) {
+                acquire_for(a.sys);
+                __syncthreads();
+                help_d<K, T, SL>(a);
+            }
+        }
         return;
     }
     __builtin_amdgcn_s_setprio(3);  // the chain is the launch's critical path
