@@ -112,6 +112,7 @@ typedef struct srg_stats {
 #define SRG_PATH_DENSE_U64 1    /* dense FW, u64 latency keys */
 #define SRG_PATH_DIRECT 2       /* get_direct_paths */
 #define SRG_PATH_SPARSE_U32 3   /* sparse: batched lexicographic Bellman-Ford, u32 latency keys */
+#define SRG_PATH_SPARSE_U64 4   /* sparse, u64 latency keys (used paths past 2^32-1 latency units) */
 
 #define SRG_SCAN_NONE 0         /* no used sources */
 #define SRG_SCAN_SPARSE 1       /* tight scan over the essential edges (default) */

@@ -27,6 +27,7 @@ SRG_PATH_DENSE_U32 = 0
 SRG_PATH_DENSE_U64 = 1
 SRG_PATH_DIRECT = 2
 SRG_PATH_SPARSE_U32 = 3
+SRG_PATH_SPARSE_U64 = 4
 
 SRG_OPT_PROFILING = 1
 SRG_OPT_SPARSE_THRESHOLD = 2

@@ -2388,9 +2388,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
 // ---- sparse path: batched lexicographic Bellman-Ford (sparse.hip.h) ----------------------
 // Rank r routes the used sources at positions [r*n/G, (r+1)*n/G) (contiguous output rows).
 // Returns false when a used pair came out saturated/unreachable and the graph's latencies
-// could exceed the u32 keys: the caller then decides on the dense u64 path.
+// could exceed the u32 keys: the caller then reruns on the wide (u64-key) labels.
 bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n, uint64_t* out_lat,
-                float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats) {
+                float* out_loss, hipStream_t st, const Prelude& P, srg_stats* stats, bool wide = false) {
+    if (wide && c.kout_key) fail(SRG_INTERNAL_NEED_U64, "the build needs u64 latency keys: no u32 key table");
     const uint32_t V = g.V;
     const bool multi = c.comm && c.comm->nranks > 1;
     const int G = multi ? c.comm->nranks : 1, rk = multi ? c.comm->rank : 0;
@@ -2415,10 +2416,11 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     uint32_t* in_src = (uint32_t*)c.b_entkey.get(std::max<size_t>(arcs, 1) * 4);
     uint32_t* in_w = (uint32_t*)c.b_entw.get(std::max<size_t>(arcs, 1) * 4);
     float* in_b = (float*)c.b_entb.get(std::max<size_t>(arcs, 1) * 4);
+    uint64_t* in_w64 = wide ? (uint64_t*)c.b_cscent.get(std::max<size_t>(arcs, 1) * 8) : nullptr;
     HIP_CHECK(hipMemsetAsync(cur, 0, ((size_t)V + 1) * 4, st));
     if (g.E)
         k_csr_fill<<<grid_for(g.E), kThreads, 0, st>>>(g.E, esrc, edst, g.lat, P.unit, g.loss, g.directed, off, cur,
-                                                       in_src, in_w, in_b);
+                                                       in_src, in_w, in_b, in_w64);
     // out-arcs for the work marks: the in-CSR itself when undirected
     const uint32_t* out_off = off;
     const uint32_t* out_dst = in_src;
@@ -2495,18 +2497,20 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
 
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
-    uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)c.sparse_wgs_per_cu));
+    // wide labels take the 128-VGPR budget: one workgroup per CU
+    const int wpc = wide ? 1 : c.sparse_wgs_per_cu;
+    uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)wpc));
 
-    // label slots (V x 64 x 8 B per resident batch) within about half of the free HBM
+    // label slots (V x 64 x 8 B per resident batch, + 4 B loss words when wide) within about half
+    // of the free HBM
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t slot_bytes = (size_t)V * 64 * 8;
+    const size_t slot_bytes = (size_t)V * 64 * (wide ? 12 : 8);
     grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
     const uint32_t nwv = (V + 63) / 64;
     const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
     // bitmaps in LDS while a CU still fits the requested workgroups, else in global memory
-    const bool gbits = c.sparse_global_bitmaps ||
-                       bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / c.sparse_wgs_per_cu;
+    const bool gbits = c.sparse_global_bitmaps || bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / wpc;
     const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
     if (nbatch) {
         unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
@@ -2521,12 +2525,15 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                          : (c.sparse_group == 16 ? k_sparse_bf<16, false, 4>
                             : c.sparse_group == 4 ? k_sparse_bf<4, false, 4> : k_sparse_bf<SP_G, false, 4>);
         }
+        if (wide) kern = gbits ? k_sparse_bf<SP_G, true, 4, LabelU64> : k_sparse_bf<SP_G, false, 4, LabelU64>;
         set_lds(kern, lds);
+        uint32_t* slots_loss = wide ? (uint32_t*)c.b_WL.get((size_t)grid * V * 64 * 4) : nullptr;
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
-                     selflat, selfloss, out_lat, out_loss, fl, P.unit, 0xFFFFFFFFu, 0u, gb, c.kout_key, c.kout_diag};
+                     selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, 0u, gb, c.kout_key, c.kout_diag,
+                     slots_loss, in_w64};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
-            a.delta = (uint32_t)std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
+            a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
         a.all_lanes = c.sparse_delta_all ? 1u : 0u;
         if (c.profiling) {
             while (c.prof_events.size() < 2) {
@@ -2556,7 +2563,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     if (hfl[0]) {
         // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
         // finite (>= 2^32-1 ns) path; otherwise the pair is unreachable -- the reference's panic
-        if (hfl[5]) return false;  // decide on the u64 path
+        if (hfl[5] && !wide) return false;  // rerun on the wide labels
         fail(SRG_ERR_UNREACHABLE,
              "assertion `left == right` failed: paths.len() != nodes.len().pow(2) (a used node is unreachable "
              "from another used node)");
@@ -2585,7 +2592,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         stats->ms_build += ms_build;
         stats->ms_fw += ms_sssp;
         stats->ms_exchange += ms_exchange;
-        stats->path_kind = SRG_PATH_SPARSE_U32;
+        stats->path_kind = wide ? SRG_PATH_SPARSE_U64 : SRG_PATH_SPARSE_U32;
         stats->loss_rounds = (int)hfl[1];
         stats->relaxations = (((uint64_t)hfl[3] << 32) | hfl[2]) * 64;
         stats->nranks = G;
@@ -2632,9 +2639,13 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     // at most max_lat * V: below 2^64 nothing wraps, and outputs D * unit fit u64
     P.wrap_risk = (unsigned __int128)P.es.max_lat * g.V >= ((unsigned __int128)1 << 64);
     const int G = c.comm ? c.comm->nranks : 1, rk = c.comm ? c.comm->rank : 0;
-    if (choose_sparse(c, g) && P.max_key < 0xFFFFFFFFull && !P.wrap_risk) {
+    if (choose_sparse(c, g) && !P.wrap_risk) {
+        // u32 latency keys first; a graph whose arcs or used paths pass 2^32-1 units takes the
+        // wide (u64-key) labels: exact, since max_lat * V < 2^64 (no wrap risk) bounds every sum
         loss_arrive(g, P.selfloss, st);
-        if (run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
+        if (P.max_key < 0xFFFFFFFFull && run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats)) return;
+        run_sparse(c, g, nodes, n, out_lat, out_loss, st, P, stats, true);
+        return;
     }
     if (pre) {
         if (run_dense<uint32_t, FwOverlap::T>(c, g, ov->pl, nodes, n, out_lat, out_loss, st, P, stats, sink, ov)) return;

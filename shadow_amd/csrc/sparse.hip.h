@@ -12,7 +12,7 @@
 // every label access is one coalesced 512-byte row.  A label is the lexicographic key
 //     (latency_u32 << 32) | float_bits(loss)        (loss >= +0: bit order == numeric order)
 // so lexmin is a single u64 min.  Latency keys saturate at 2^32-1 (= "unreachable or too
-// long"); the host re-runs such graphs on the dense u64 path.
+// long"); the host re-runs such graphs on the wide labels (LabelU64: u64 latency + u32 loss).
 //
 // Layout (HBM):
 //   in_off [V+1], in_src/in_w/in_b [arcs]  CSR of IN-arcs (self-loops dropped; undirected
@@ -50,6 +50,60 @@ __device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, u
     return nl == 0xFFFFFFFFu ? LBL_INF : c;
 }
 
+// Label policies.  Narrow (u32 latency keys): one u64 per lane, (key << 32) | loss bits, lexmin =
+// u64 min.  Wide (u64 latency keys, for graphs whose used paths pass 2^32-1 units): the latency
+// u64 and the loss bits u32 in two arrays of the same [V][64] shape, lexmin compares both words;
+// the host only takes it when max_lat * V < 2^64, so sums never wrap (saturation is a guard).
+struct LabelU32 {
+    using T = unsigned long long;
+    static constexpr bool wide = false;
+    static constexpr uint64_t LAT_MAX = 0xFFFFFFFFull;
+    unsigned long long* L;
+    __device__ static T inf() { return LBL_INF; }
+    __device__ static T zero() { return 0ull; }
+    __device__ static bool lt(T a, T b) { return a < b; }
+    __device__ static bool is_inf(T a) { return a == LBL_INF; }
+    __device__ static uint64_t lat(T a) { return a >> 32; }
+    __device__ static uint32_t loss_bits(T a) { return (uint32_t)a; }
+    __device__ T ld(size_t i) const { return __builtin_nontemporal_load(&L[i]); }
+    __device__ void st(size_t i, T v) const { L[i] = v; }
+    // arc weight: the list holds the u32 key itself
+    __device__ static T relax(T u, uint32_t wtag, float b, const uint64_t*) { return lbl_relax(u, wtag, b); }
+    __device__ static uint32_t wtag(uint32_t k, const uint32_t* in_w) { return in_w[k]; }
+};
+
+struct LabelU64 {
+    struct T {
+        uint64_t l;
+        uint32_t s;
+    };
+    static constexpr bool wide = true;
+    static constexpr uint64_t LAT_MAX = ~0ull;
+    unsigned long long* L;
+    uint32_t* S;
+    __device__ static T inf() { return T{~0ull, 0xFFFFFFFFu}; }
+    __device__ static T zero() { return T{0ull, 0u}; }
+    __device__ static bool lt(T a, T b) { return a.l < b.l || (a.l == b.l && a.s < b.s); }
+    __device__ static bool is_inf(T a) { return a.l == ~0ull; }
+    __device__ static uint64_t lat(T a) { return a.l; }
+    __device__ static uint32_t loss_bits(T a) { return a.s; }
+    __device__ T ld(size_t i) const {
+        return T{__builtin_nontemporal_load(&L[i]), __builtin_nontemporal_load(&S[i])};
+    }
+    __device__ void st(size_t i, T v) const {
+        L[i] = v.l;
+        S[i] = v.s;
+    }
+    // arc weight: the list holds the arc index, the u64 key is read per relaxation (wave-uniform)
+    __device__ static T relax(T u, uint32_t wtag, float b, const uint64_t* in_w64) {
+        const uint64_t w = in_w64[wtag];
+        const uint64_t nl = u.l + w;
+        if (nl < u.l || nl == ~0ull) return inf();
+        return T{nl, __float_as_uint(fold_loss(__uint_as_float(u.s), b))};
+    }
+    __device__ static uint32_t wtag(uint32_t k, const uint32_t*) { return k; }
+};
+
 // ---- CSR of in-arcs -------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lat_key32(uint64_t l) { return l >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)l; }
 
@@ -82,21 +136,25 @@ __global__ void k_csr_fill_out(uint64_t E, const uint32_t* __restrict__ src, con
 __global__ void k_csr_fill(uint64_t E, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                            const uint64_t* __restrict__ lat, uint64_t unit, const float* __restrict__ loss, int directed,
                            const uint32_t* __restrict__ off, uint32_t* __restrict__ cur, uint32_t* __restrict__ in_src,
-                           uint32_t* __restrict__ in_w, float* __restrict__ in_b) {
+                           uint32_t* __restrict__ in_w, float* __restrict__ in_b, uint64_t* __restrict__ in_w64) {
+    // in_w64 (wide labels): the u64 key per arc beside the saturated u32 one
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
         if (s == t) continue;
-        const uint32_t w = lat_key32(unit != 1 ? lat[e] / unit : lat[e]);  // latency units (compute_device)
+        const uint64_t w64 = unit != 1 ? lat[e] / unit : lat[e];  // latency units (compute_device)
+        const uint32_t w = lat_key32(w64);
         const float b = __fsub_rn(1.0f, loss[e] + 0.0f);
         uint32_t k = off[t] + atomicAdd(&cur[t], 1u);
         in_src[k] = s;
         in_w[k] = w;
         in_b[k] = b;
+        if (in_w64) in_w64[k] = w64;
         if (!directed) {
             k = off[s] + atomicAdd(&cur[s], 1u);
             in_src[k] = t;
             in_w[k] = w;
             in_b[k] = b;
+            if (in_w64) in_w64[k] = w64;
         }
     }
 }
@@ -124,22 +182,19 @@ struct SparseArgs {
     uint32_t* flags;             // [0] unreachable/saturated used pair, [1] max sweeps, [2..3] total evaluations,
                                  // [5] some relaxation saturated the u32 latency key (a path >= 2^32-1 ns)
     uint64_t unit;               // latency unit in ns (outputs = key * unit)
-    uint32_t delta;              // bucket width in latency units (0xFFFFFFFF = one bucket: plain Bellman-Ford)
+    uint64_t delta;              // bucket width in latency units (~0 = one bucket: plain Bellman-Ford)
     uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
     uint32_t* out_key;           // RoutingInfo key table (null: ns latencies into out_lat), diagonal 0xFFFFFFFF
     uint64_t* out_diag;          // with out_key: the raw self-loop latency per output row
+    uint32_t* slots_loss;        // wide labels: [gridDim.x][V][64] loss bits beside the u64 latencies in `slots`
+    const uint64_t* in_w64;      // wide labels: u64 arc keys
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
 // (all_lanes = 1) dropped lane's new latency is below the bucket bound
 __device__ __forceinline__ bool bucket_ready(bool dropped, bool below, uint32_t all_lanes) {
     return all_lanes ? __ballot(dropped && !below) == 0 : __ballot(dropped && below) != 0;
-}
-
-__device__ __forceinline__ unsigned long long ld_label(const unsigned long long* p) {
-    // L1-bypassing load: rows written by other waves of this workgroup in the previous sweep
-    return __builtin_nontemporal_load(p);
 }
 
 // Vertex bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
@@ -151,8 +206,10 @@ __device__ __forceinline__ unsigned long long ld_label(const unsigned long long*
 // WPE = waves per SIMD the register budget is sized for: 8 (two 1024-thread workgroups per CU,
 // <= 64 VGPRs: the kernel spills ~90 B per lane to scratch) or 4 (one workgroup per CU, <= 128
 // VGPRs, no spills; SRG_OPT_SPARSE_WGS_PER_CU = 1).
-template <int G, bool GB, int WPE = 8>
+// LB = label policy (LabelU32 / LabelU64 above).
+template <int G, bool GB, int WPE = 8, class LB = LabelU32>
 __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
+    using Lbl = typename LB::T;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
     const uint32_t nw = (V + 63) / 64;  // 64-vertex windows
@@ -173,9 +230,9 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
     uint32_t* w_w = w_u + SP_CAP;   // arc weight, or the window index of an own-row entry
     uint32_t* w_b = w_w + SP_CAP;   // 1 - arc loss, or SP_OWN
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
-    unsigned long long* L = a.slots + (size_t)blockIdx.x * V * 64;
-    auto st_label = [&](size_t idx, unsigned long long v) { L[idx] = v; };
-    auto ld_full = [&](size_t idx) -> unsigned long long { return ld_label(&L[idx]); };
+    LB lab;
+    lab.L = a.slots + (size_t)blockIdx.x * V * 64;
+    if constexpr (LB::wide) lab.S = a.slots_loss + (size_t)blockIdx.x * V * 64;
     uint32_t max_sweeps = 0;
     unsigned long long evals = 0;
     uint32_t saturated = 0;  // a finite label + arc reached 2^32-1: INF may then mean "too long", not unreachable
@@ -197,7 +254,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
         const uint32_t my_src = a.batch_src[bt * 64 + lane];
         // init: labels INF except the sources; changed = the sources; marks = their out-neighbours
         for (uint32_t v = wave; v < V; v += SP_WAVES)
-            st_label((size_t)v * 64 + lane, (v == my_src) ? 0ull : LBL_INF);
+            lab.st((size_t)v * 64 + lane, (v == my_src) ? LB::zero() : LB::inf());
         for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
             fprev[w] = 0;
             fcur[w] = 0;
@@ -210,7 +267,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
         // once some lane's new latency is below the bound; the others wait in `pend` until the
         // bucket is exhausted and the bound moves on.  Any push order reaches the same unique
         // lexicographic fixpoint; the order only changes the work.
-        uint32_t bound = a.delta;
+        uint64_t bound = a.delta >= LB::LAT_MAX ? LB::LAT_MAX : a.delta;
         __syncthreads();
         if (wave == 0) atomicOr(&fprev[my_src >> 6], 1ull << (my_src & 63));
         for (uint32_t q = wave; q < 64; q += SP_WAVES) {
@@ -260,12 +317,12 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                 auto process = [&](uint32_t cnt) {
                     // (3) consume the list in groups of G rows, all loads of a group in flight
                     int cur = -1;
-                    unsigned long long best = 0, old = 0;
+                    Lbl best = LB::zero(), old = LB::zero();
                     for (uint32_t j0 = 0; j0 < cnt; j0 += G) {
-                        unsigned long long row[G];
+                        Lbl row[G];
 #pragma unroll
                         for (int q = 0; q < G; ++q)
-                            if (j0 + q < cnt) row[q] = ld_label(&L[(size_t)w_u[j0 + q] * 64 + lane]);
+                            if (j0 + q < cnt) row[q] = lab.ld((size_t)w_u[j0 + q] * 64 + lane);
 #pragma unroll
                         for (int q = 0; q < G; ++q) {
                             const uint32_t e = j0 + q;
@@ -273,10 +330,10 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                             const uint32_t tagb = w_b[e];
                             if (tagb == SP_OWN) {  // a new vertex: its current label
                                 if (cur >= 0) {
-                                    const unsigned long long dm = __ballot(best < old);
-                                    if (dm) {
-                                        if (best < old) st_label((size_t)(w * 64 + cur) * 64 + lane, best);
-                                        if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
+                                    const bool dr = LB::lt(best, old);
+                                    if (__ballot(dr)) {
+                                        if (dr) lab.st((size_t)(w * 64 + cur) * 64 + lane, best);
+                                        if (bucket_ready(dr, LB::lat(best) < bound, a.all_lanes))
                                             changed |= 1ull << cur;
                                         else
                                             deferred |= 1ull << cur;
@@ -285,19 +342,19 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                                 cur = (int)(w_w[e] & 63u);
                                 old = best = row[q];
                             } else {
-                                const unsigned long long c =
-                                    row[q] == LBL_INF ? LBL_INF : lbl_relax(row[q], w_w[e], __uint_as_float(tagb));
-                                saturated |= (c == LBL_INF) & (row[q] != LBL_INF);
-                                best = c < best ? c : best;
+                                const bool rinf = LB::is_inf(row[q]);
+                                const Lbl c = rinf ? LB::inf() : LB::relax(row[q], w_w[e], __uint_as_float(tagb), a.in_w64);
+                                saturated |= LB::is_inf(c) & !rinf;
+                                best = LB::lt(c, best) ? c : best;
                                 ++evals;
                             }
                         }
                     }
                     if (cur >= 0) {
-                        const unsigned long long dm = __ballot(best < old);
-                        if (dm) {
-                            if (best < old) st_label((size_t)(w * 64 + cur) * 64 + lane, best);
-                            if (bucket_ready(best < old, (uint32_t)(best >> 32) < bound, a.all_lanes))
+                        const bool dr = LB::lt(best, old);
+                        if (__ballot(dr)) {
+                            if (dr) lab.st((size_t)(w * 64 + cur) * 64 + lane, best);
+                            if (bucket_ready(dr, LB::lat(best) < bound, a.all_lanes))
                                 changed |= 1ull << cur;
                             else
                                 deferred |= 1ull << cur;
@@ -332,7 +389,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                         w_u[pos] = u;
                         if (!(vi & 0x80000000u)) {
-                            w_w[pos] = a.in_w[k];
+                            w_w[pos] = LB::wtag(k, a.in_w);
                             w_b[pos] = __float_as_uint(a.in_b[k]);
                         } else {
                             w_w[pos] = k;  // window index of the vertex
@@ -427,7 +484,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                 // changed) and move the bound on.  Releasing only those below the new bound was
                 // measured slower on C4 (more, emptier sweeps).
                 __syncthreads();  // every thread has read s_pend
-                bound = bound > 0xFFFFFFFFu - a.delta ? 0xFFFFFFFFu : bound + a.delta;
+                bound = (a.delta >= LB::LAT_MAX || bound > LB::LAT_MAX - a.delta) ? LB::LAT_MAX : bound + a.delta;
                 for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
                     fprev[w] = pend[w];
                     pend[w] = 0;
@@ -452,39 +509,53 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
         }
         max_sweeps = sweeps > max_sweeps ? sweeps : max_sweeps;
         // ---- output rows: 64 targets x 64 sources tiles transposed through LDS ----
+        // narrow labels: one pass (the tile holds the packed label); wide: pass 0 the latencies,
+        // pass 1 the loss bits
         uint32_t bad = 0;
         for (uint32_t j0 = 0; j0 < a.ncols; j0 += 64) {
-            for (uint32_t i = wave; i < 64; i += SP_WAVES) {
-                const uint32_t j = j0 + i;
-                tile[i * 65 + lane] = j < a.ncols ? ld_full((size_t)a.cols[j] * 64 + lane) : 0ull;
-            }
-            __syncthreads();
-            for (uint32_t sl = wave; sl < 64; sl += SP_WAVES) {
-                const uint32_t row = a.batch_row[bt * 64 + sl];
-                const uint32_t j = j0 + lane;
-                if (row == 0xFFFFFFFFu || j >= a.ncols) continue;
-                const unsigned long long l = tile[lane * 65 + sl];
-                uint64_t ol;
-                float os;
-                if (j == row) {  // diagonal: the raw self-loop weight
+            for (int pass = 0; pass < (LB::wide ? 2 : 1); ++pass) {
+                for (uint32_t i = wave; i < 64; i += SP_WAVES) {
+                    const uint32_t j = j0 + i;
+                    unsigned long long v = 0;
+                    if (j < a.ncols) {
+                        const size_t idx = (size_t)a.cols[j] * 64 + lane;
+                        if constexpr (LB::wide)
+                            v = pass ? (unsigned long long)__builtin_nontemporal_load(&lab.S[idx])
+                                     : __builtin_nontemporal_load(&lab.L[idx]);
+                        else
+                            v = lab.ld(idx);
+                    }
+                    tile[i * 65 + lane] = v;
+                }
+                __syncthreads();
+                for (uint32_t sl = wave; sl < 64; sl += SP_WAVES) {
+                    const uint32_t row = a.batch_row[bt * 64 + sl];
+                    const uint32_t j = j0 + lane;
+                    if (row == 0xFFFFFFFFu || j >= a.ncols) continue;
+                    const unsigned long long l = tile[lane * 65 + sl];
+                    const size_t o = (size_t)row * a.ncols + j;
                     const uint32_t s = a.batch_src[bt * 64 + sl];
-                    ol = a.self_lat[s];
-                    os = a.self_loss[s];
-                } else {
-                    const uint32_t lat = (uint32_t)(l >> 32);
-                    bad |= lat == 0xFFFFFFFFu;
-                    ol = (uint64_t)lat * a.unit;
-                    os = __uint_as_float((uint32_t)l);
+                    if (!LB::wide || pass == 0) {  // latency
+                        uint64_t ol;
+                        if (j == row) {  // diagonal: the raw self-loop weight
+                            ol = a.self_lat[s];
+                        } else {
+                            const uint64_t lat = LB::wide ? l : l >> 32;
+                            bad |= lat == LB::LAT_MAX;
+                            ol = lat * a.unit;
+                        }
+                        if (a.out_key) {  // narrow only (the host never asks wide labels for keys)
+                            a.out_key[o] = j == row ? 0xFFFFFFFFu : (uint32_t)(l >> 32);
+                            if (j == row) a.out_diag[row] = ol;
+                        } else {
+                            a.out_lat[o] = ol;
+                        }
+                    }
+                    if (!LB::wide || pass == 1)  // loss
+                        a.out_loss[o] = j == row ? a.self_loss[s] : __uint_as_float((uint32_t)l);
                 }
-                if (a.out_key) {
-                    a.out_key[(size_t)row * a.ncols + j] = j == row ? 0xFFFFFFFFu : (uint32_t)(l >> 32);
-                    if (j == row) a.out_diag[row] = ol;
-                } else {
-                    a.out_lat[(size_t)row * a.ncols + j] = ol;
-                }
-                a.out_loss[(size_t)row * a.ncols + j] = os;
+                __syncthreads();
             }
-            __syncthreads();
         }
         if (bad) atomicOr(&a.flags[0], 1u);
     }

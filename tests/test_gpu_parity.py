@@ -509,7 +509,8 @@ def test_latency_unit_keys(router, algo, monkeypatch):
     unit = t.stats["latency_unit_ns"]
     assert unit % 3_000_000 == 0 and t1.stats["latency_unit_ns"] == 1
     want = N.SRG_PATH_SPARSE_U32 if algo == "sparse" else N.SRG_PATH_DENSE_U32
-    assert t.stats["path_kind"] == want and t1.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+    want1 = N.SRG_PATH_SPARSE_U64 if algo == "sparse" else N.SRG_PATH_DENSE_U64
+    assert t.stats["path_kind"] == want and t1.stats["path_kind"] == want1
     assert np.array_equal(t.latency_ns, t1.latency_ns) and bits_equal(t.packet_loss, t1.packet_loss)
     rows = [0, 1, len(nodes) - 1]
     rl, rs = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)

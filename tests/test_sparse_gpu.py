@@ -148,14 +148,45 @@ def test_bf_unreachable_panics(bf_router):
     assert t[(0, 1)].latency_ns == 3
 
 
-def test_bf_large_latency_falls_back_exactly(bf_router):
-    """Latencies whose sums may pass 2^32: saturated u32 keys hand over to the u64 dense path."""
+def test_bf_large_latency_takes_wide_labels(bf_router):
+    """Latencies whose sums pass 2^32: saturated u32 keys hand over to the wide (u64-key) labels."""
     g = synth.random_graph(120, 0.05, 209, lat_lo=2**30, lat_hi=2**31)
     nodes = list(range(120))
     lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes)
     t = bf_router.compute_shortest_paths(g, nodes)
-    assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U64
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U64
+    assert int(lat.max()) >= 2 ** 32
     assert np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss)
+
+
+@pytest.mark.parametrize("case", ["arcs_past_u32", "paths_past_u32", "delta"])
+def test_ba_wide_labels(case):
+    """A Barabasi-Albert graph with nanosecond latencies (unit 1) whose used paths pass 2^32 ns stays
+    on the sparse path with u64 latency keys (SRG_PATH_SPARSE_U64): seeded oracle rows, symmetry,
+    diagonal.  arcs_past_u32: single arcs above 2^32 (the u32 pass is skipped); paths_past_u32: arcs
+    below 2^32, paths above (the u32 pass saturates and reruns wide); delta: with buckets."""
+    V = 6000
+    e0 = synth.barabasi_albert(V, 4, seed=V + 7)
+    rng = np.random.default_rng(V)
+    if case == "arcs_past_u32":
+        lat = rng.integers(2 ** 32, 2 ** 34, size=len(e0.src), dtype=np.uint64) | np.uint64(1)
+    else:
+        lat = rng.integers(2 ** 29, 2 ** 31, size=len(e0.src), dtype=np.uint64) | np.uint64(1)
+    lat[e0.src == e0.dst] = e0.latency_ns[e0.src == e0.dst]
+    e = Edges(V, e0.src, e0.dst, lat, e0.packet_loss, directed=False)
+    r = Router(0)
+    if case == "delta":
+        r.set_option(N.SRG_OPT_SPARSE_DELTA_DIV, 8)
+    nodes = list(range(V))
+    t = r.compute_shortest_paths(e, nodes)
+    assert t.stats["path_kind"] == N.SRG_PATH_SPARSE_U64 and t.stats["latency_unit_ns"] == 1
+    assert int(t.latency_ns.max()) >= 2 ** 32
+    rows = rng.choice(V, 8, replace=False).tolist()
+    rl, rs = oracle.compute_shortest_paths(e.as_tuple(), nodes, rows=rows, nthreads=16)
+    assert np.array_equal(t.latency_ns[rows], rl) and bits_equal(t.packet_loss[rows], rs)
+    off = ~np.eye(V, dtype=bool)
+    assert np.array_equal(t.latency_ns[off], t.latency_ns.T[off])
+    r.close()
 
 
 @pytest.mark.parametrize("V", [3000, 12000])
