@@ -271,9 +271,8 @@ def apply_options(router, args):
         router.set_option(N.SRG_OPT_SPARSE_LOCALITY, 0)
     if args.fw_tile:
         router.set_option(N.SRG_OPT_FW_TILE, args.fw_tile)
-    for flag, opt in (("sparse_group", "SPARSE_GROUP"), ("sparse_delta_all", "SPARSE_DELTA_ALL"),
-                      ("sparse_delta_div", "SPARSE_DELTA_DIV"), ("fw_symmetric", "FW_SYMMETRIC"),
-                      ("sparse_wgs", "SPARSE_WGS_PER_CU"), ("h2d_codec", "H2D_CODEC"),
+    for flag, opt in (("sparse_delta_div", "SPARSE_DELTA_DIV"), ("fw_symmetric", "FW_SYMMETRIC"),
+                      ("h2d_codec", "H2D_CODEC"),
                       ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
                       ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT"),
                       ("fw_step", "FW_STEP"), ("fw_overlap", "FW_OVERLAP")):
@@ -288,8 +287,7 @@ def workload_key(args, V, seed, world):
     return (f"{args.graph}:{V}:{seed}:" + (f"x{args.lat_scale}:" if args.lat_scale != 1 else "")
             + ("lb:" if args.graph != "ba" else "")
             + f"packed2:tile{args.fw_tile or 128}:"
-            f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g{args.sparse_group or 8}:"
-            f"w{args.sparse_wgs or 2}"
+            f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g8:w2"
             + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
             + (f":n{world}" if world > 1 else "") + (f":sim{args.simulate_rank}" if args.simulate_rank else ""))
 
@@ -541,11 +539,8 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="N>1: independent full builds per rank (weak)")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: every rank ends with the whole table (RCCL row exchange; host entry: all rows D2H)")
-    ap.add_argument("--sparse-group", type=int, default=None, help="sparse: label rows in flight per wave (4/8)")
-    ap.add_argument("--sparse-wgs", type=int, default=None, help="sparse: resident batches per CU (1/2)")
     ap.add_argument("--sparse-delta-div", type=int, default=None,
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
-    ap.add_argument("--sparse-delta-all", type=int, default=None, help="sparse: 1 = bucket test over every dropped lane")
     ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
     ap.add_argument("--d2h-mode", type=int, default=None, help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync")
     ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")

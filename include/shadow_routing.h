@@ -144,12 +144,10 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_FW_TILE 7         /* dense u32 FW tile: 0 = auto (128), 64, 128 */
 /* 8 (SRG_OPT_FW_PACKED) and 18 (SRG_OPT_CHAIN_PRIO) were A/B switches, removed in round 4: the u32 FW
  * always runs the pair-packed tile and the chain kernels always raise their priority. */
-#define SRG_OPT_SPARSE_GROUP 10   /* sparse: label rows in flight per wave, 4 / 8 (default) / 16 (one workgroup per CU) */
-#define SRG_OPT_SPARSE_WGS_PER_CU 11 /* sparse: resident source batches (workgroups) per CU, 1 / 2 (default) */
+/* 10 (SPARSE_GROUP), 11 (SPARSE_WGS_PER_CU) and 13 (SPARSE_DELTA_ALL) were A/B switches of the sparse
+ * kernel, removed in round 4: 8 rows in flight, two workgroups per CU, any-lane bucket test. */
 #define SRG_OPT_SPARSE_DELTA_DIV 12  /* sparse: delta-stepping bucket width = max edge latency / value;
                                         0 = a single bucket (plain Bellman-Ford); default 1 */
-#define SRG_OPT_SPARSE_DELTA_ALL 13  /* sparse: 1 = a dropped vertex is pushed only when every dropped lane is
-                                        below the bucket bound, 0 (default) = when any is */
 #define SRG_OPT_SPARSE_GLOBAL_BITMAPS 14 /* sparse: 1 = keep the per-batch vertex bitmaps in global memory
                                         (automatic when 5V/8 bytes do not fit the LDS budget) */
 #define SRG_OPT_FW_SYMMETRIC 17     /* dense: 1 (default) = for an undirected graph, update only the FW tiles

@@ -36,10 +36,7 @@ SRG_OPT_ALGORITHM = 4
 SRG_OPT_SPARSE_LOCALITY = 5
 SRG_OPT_SIMULATE_RANK = 6
 SRG_OPT_FW_TILE = 7
-SRG_OPT_SPARSE_GROUP = 10
-SRG_OPT_SPARSE_WGS_PER_CU = 11
 SRG_OPT_SPARSE_DELTA_DIV = 12
-SRG_OPT_SPARSE_DELTA_ALL = 13
 SRG_OPT_SPARSE_GLOBAL_BITMAPS = 14
 SRG_OPT_FW_SYMMETRIC = 17
 SRG_OPT_D2H_MODE = 20

@@ -686,9 +686,6 @@ struct srg_ctx {
     bool gather_output = true;       // multi-rank: every rank ends with all n x n outputs
     int algorithm = SRG_ALGO_AUTO;   // dense FW / sparse batched Bellman-Ford
     bool sparse_locality = true;     // sparse: batch sources in BFS order
-    int sparse_group = 8;            // sparse: label rows in flight per wave (4, 8)
-    int sparse_wgs_per_cu = 2;       // sparse: resident batches (workgroups) per CU
-    bool sparse_delta_all = false;   // sparse: bucket test over every dropped lane (else any lane)
     int sparse_delta_div = 1;        // sparse: bucket width = max edge latency / this (0 = plain BF)
     bool sparse_global_bitmaps = false;  // sparse: force the vertex bitmaps into global memory
     int fw_tile = 0;                 // 0 = auto, 64 or 128
@@ -1861,6 +1858,10 @@ struct FwOverlap {
         bool good = exc != nullptr;
         for (size_t k = 0; good && k < nexc; ++k) {
             const uint32_t s = exc[3 * k + 1], d = exc[3 * k + 2];
+            // a self-loop whose next edge is an exception too opens no row (W ignores it): any
+            // position, e.g. a block of self-loops ahead of the rows
+            const bool next_exc = k + 1 < nexc ? exc[3 * (k + 1)] == exc[3 * k] + 1 : exc[3 * k] + 1 == e0 + ne;
+            if (s == d && next_exc) continue;
             good = s >= prev_src && s <= d;
             prev_src = s;
         }
@@ -2498,7 +2499,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
     // wide labels take the 128-VGPR budget: one workgroup per CU
-    const int wpc = wide ? 1 : c.sparse_wgs_per_cu;
+    const int wpc = wide ? 1 : 2;
     uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)wpc));
 
     // label slots (V x 64 x 8 B per resident batch, + 4 B loss words when wide) within about half
@@ -2517,24 +2518,18 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
-        auto kern = gbits ? (c.sparse_group == 4 ? k_sparse_bf<4, true> : k_sparse_bf<SP_G, true>)
-                          : (c.sparse_group == 4 ? k_sparse_bf<4, false> : k_sparse_bf<SP_G, false>);
-        if (c.sparse_wgs_per_cu == 1) {  // 128-VGPR budget (no spills)
-            kern = gbits ? (c.sparse_group == 16 ? k_sparse_bf<16, true, 4>
-                            : c.sparse_group == 4 ? k_sparse_bf<4, true, 4> : k_sparse_bf<SP_G, true, 4>)
-                         : (c.sparse_group == 16 ? k_sparse_bf<16, false, 4>
-                            : c.sparse_group == 4 ? k_sparse_bf<4, false, 4> : k_sparse_bf<SP_G, false, 4>);
-        }
+        // 8 rows in flight at two workgroups per CU: 4 rows tied, 16 rows / one workgroup per CU
+        // (128 VGPRs, no spills) ran 2.5x / 1.2x slower
+        auto kern = gbits ? k_sparse_bf<SP_G, true> : k_sparse_bf<SP_G, false>;
         if (wide) kern = gbits ? k_sparse_bf<SP_G, true, 4, LabelU64> : k_sparse_bf<SP_G, false, 4, LabelU64>;
         set_lds(kern, lds);
         uint32_t* slots_loss = wide ? (uint32_t*)c.b_WL.get((size_t)grid * V * 64 * 4) : nullptr;
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
-                     selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, 0u, gb, c.kout_key, c.kout_diag,
+                     selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, gb, c.kout_key, c.kout_diag,
                      slots_loss, in_w64};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
-        a.all_lanes = c.sparse_delta_all ? 1u : 0u;
         if (c.profiling) {
             while (c.prof_events.size() < 2) {
                 hipEvent_t e;
@@ -3591,20 +3586,9 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
         case SRG_OPT_SPARSE_LOCALITY:
             ctx->sparse_locality = value != 0.0;
             return SRG_OK;
-        case SRG_OPT_SPARSE_GROUP:
-            if (value != 4 && value != 8 && value != 16) return SRG_ERR_ARG;  // 16: one workgroup per CU only
-            ctx->sparse_group = (int)value;
-            return SRG_OK;
-        case SRG_OPT_SPARSE_WGS_PER_CU:
-            if (value != 1 && value != 2) return SRG_ERR_ARG;
-            ctx->sparse_wgs_per_cu = (int)value;
-            return SRG_OK;
         case SRG_OPT_SPARSE_DELTA_DIV:
             if (!(value >= 0.0 && value <= 1e6)) return SRG_ERR_ARG;
             ctx->sparse_delta_div = (int)value;
-            return SRG_OK;
-        case SRG_OPT_SPARSE_DELTA_ALL:
-            ctx->sparse_delta_all = value != 0.0;
             return SRG_OK;
         case SRG_OPT_SPARSE_GLOBAL_BITMAPS:
             ctx->sparse_global_bitmaps = value != 0.0;
@@ -3667,10 +3651,7 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_ALGORITHM: *value = ctx->algorithm; break;
         case SRG_OPT_SPARSE_LOCALITY: *value = ctx->sparse_locality; break;
         case SRG_OPT_FW_TILE: *value = ctx->fw_tile; break;
-        case SRG_OPT_SPARSE_GROUP: *value = ctx->sparse_group; break;
-        case SRG_OPT_SPARSE_WGS_PER_CU: *value = ctx->sparse_wgs_per_cu; break;
         case SRG_OPT_SPARSE_DELTA_DIV: *value = ctx->sparse_delta_div; break;
-        case SRG_OPT_SPARSE_DELTA_ALL: *value = ctx->sparse_delta_all; break;
         case SRG_OPT_SPARSE_GLOBAL_BITMAPS: *value = ctx->sparse_global_bitmaps; break;
         case SRG_OPT_FW_SYMMETRIC: *value = ctx->fw_symmetric; break;
         case SRG_OPT_D2H_MODE: *value = ctx->d2h_mode; break;

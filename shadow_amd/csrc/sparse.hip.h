@@ -34,7 +34,7 @@ constexpr unsigned long long LBL_INF = ~0ull;
 constexpr int SP_WAVES = 16;           // waves per workgroup (1024 threads)
 constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_CAP = 128;            // active-arc list entries per wave
-constexpr int SP_G = 8;                // label rows in flight per wave (default; SRG_OPT_SPARSE_GROUP)
+constexpr int SP_G = 8;                // label rows in flight per wave
 constexpr size_t sp_scratch_bytes() {
     return (size_t)SP_WAVES * (128 + 3 * SP_CAP) * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * (128 + 3 * SP_CAP) * 4
                                                                    : (size_t)64 * 65 * 8;
@@ -183,7 +183,6 @@ struct SparseArgs {
                                  // [5] some relaxation saturated the u32 latency key (a path >= 2^32-1 ns)
     uint64_t unit;               // latency unit in ns (outputs = key * unit)
     uint64_t delta;              // bucket width in latency units (~0 = one bucket: plain Bellman-Ford)
-    uint32_t all_lanes;          // 1 = push only when every lane that dropped is below the bound
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
     uint32_t* out_key;           // RoutingInfo key table (null: ns latencies into out_lat), diagonal 0xFFFFFFFF
     uint64_t* out_diag;          // with out_key: the raw self-loop latency per output row
@@ -191,11 +190,9 @@ struct SparseArgs {
     const uint64_t* in_w64;      // wide labels: u64 arc keys
 };
 
-// a vertex whose label dropped in some lanes is pushed now if some (all_lanes = 0) or every
-// (all_lanes = 1) dropped lane's new latency is below the bucket bound
-__device__ __forceinline__ bool bucket_ready(bool dropped, bool below, uint32_t all_lanes) {
-    return all_lanes ? __ballot(dropped && !below) == 0 : __ballot(dropped && below) != 0;
-}
+// a vertex whose label dropped in some lanes is pushed now if some dropped lane's new latency is
+// below the bucket bound (requiring every dropped lane below it was measured slower)
+__device__ __forceinline__ bool bucket_ready(bool dropped, bool below) { return __ballot(dropped && below) != 0; }
 
 // Vertex bitmaps (one bit per vertex): fprev = changed in the previous sweep (the arcs worth
 // pulling), fcur = changed in this sweep, mark/mnext = vertices to evaluate in this / the next
@@ -203,9 +200,9 @@ __device__ __forceinline__ bool bucket_ready(bool dropped, bool below, uint32_t 
 // only visits marked vertices, 64 per wave step (one bitmap word pair).  The five bitmaps take
 // 5 V / 8 bytes: in LDS up to V ~ 190k (GB = false), beyond that in a per-workgroup global
 // slice (GB = true; the same accesses, separated by the same barriers, L2-resident).
-// WPE = waves per SIMD the register budget is sized for: 8 (two 1024-thread workgroups per CU,
-// <= 64 VGPRs: the kernel spills ~90 B per lane to scratch) or 4 (one workgroup per CU, <= 128
-// VGPRs, no spills; SRG_OPT_SPARSE_WGS_PER_CU = 1).
+// WPE = waves per SIMD the register budget is sized for: 8 for the u32 labels (two 1024-thread
+// workgroups per CU, <= 64 VGPRs: the kernel spills ~48 B per lane to scratch; one workgroup per CU
+// without spills measured 1.2x slower), 4 for the wide labels (one workgroup per CU).
 // LB = label policy (LabelU32 / LabelU64 above).
 template <int G, bool GB, int WPE = 8, class LB = LabelU32>
 __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
@@ -333,7 +330,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                                     const bool dr = LB::lt(best, old);
                                     if (__ballot(dr)) {
                                         if (dr) lab.st((size_t)(w * 64 + cur) * 64 + lane, best);
-                                        if (bucket_ready(dr, LB::lat(best) < bound, a.all_lanes))
+                                        if (bucket_ready(dr, LB::lat(best) < bound))
                                             changed |= 1ull << cur;
                                         else
                                             deferred |= 1ull << cur;
@@ -354,7 +351,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                         const bool dr = LB::lt(best, old);
                         if (__ballot(dr)) {
                             if (dr) lab.st((size_t)(w * 64 + cur) * 64 + lane, best);
-                            if (bucket_ready(dr, LB::lat(best) < bound, a.all_lanes))
+                            if (bucket_ready(dr, LB::lat(best) < bound))
                                 changed |= 1ull << cur;
                             else
                                 deferred |= 1ull << cur;

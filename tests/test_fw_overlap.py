@@ -29,9 +29,19 @@ def same(a, b):
     return np.array_equal(a.latency_ns, b.latency_ns) and bits_equal(a.packet_loss, b.packet_loss)
 
 
-@pytest.mark.parametrize("V", [2100, 3000])
-def test_overlap_matches_after_h2d(V, monkeypatch, capfd):
+def gml_order(e):
+    """The GML writer's order: node i's self-loop, then its row (i, j > i)."""
+    key = np.minimum(e.src, e.dst).astype(np.int64) * (e.num_vertices + 1) + np.where(e.src == e.dst, 0, e.dst + 1)
+    p = np.argsort(key, kind="stable")
+    return Edges(e.num_vertices, e.src[p], e.dst[p], e.latency_ns[p], e.packet_loss[p], False)
+
+
+@pytest.mark.parametrize("V,order", [(2100, "selfloops_first"), (3000, "selfloops_first"), (3000, "gml")])
+def test_overlap_matches_after_h2d(V, order, monkeypatch, capfd):
+    """Self-loops as a block ahead of the rows (synth.atlas_like) or each ahead of its own row (GML)."""
     e = synth.atlas_like(V, seed=V + 1)
+    if order == "gml":
+        e = gml_order(e)
     nodes = list(range(V))
     monkeypatch.setenv("SRG_DEBUG_OVERLAP", "1")
     t1 = build(e, nodes, 1)

@@ -7,6 +7,8 @@ out=gpurun_out/${1:-r04d}
 mkdir -p $out
 timeout -k 10 600 python -u -m pytest -m gpu -x -v --timeout 250 --timeout-method thread tests/test_fw_overlap.py tests/test_routing_info_keys.py tests/test_fw_step.py > $out/pytest_new.log 2>&1 || { echo "new tests failed"; tail -60 $out/pytest_new.log; exit 1; }
 tail -4 $out/pytest_new.log
+timeout -k 10 400 python -u -m pytest -m gpu -x -v --timeout 250 --timeout-method thread tests/test_sparse_gpu.py tests/test_gpu_parity.py -k "wide or large_latency or unit" > $out/pytest_wide.log 2>&1 || { echo "wide tests failed"; tail -60 $out/pytest_wide.log; exit 1; }
+tail -4 $out/pytest_wide.log
 for ov in 1 0; do
   SRG_DEBUG_OVERLAP=1 timeout -k 10 300 python3 -u bench.py --steps 5 --no-cpu --no-verify --no-ri --fw-overlap $ov > $out/c3_ov$ov.json 2> $out/c3_ov$ov.err || { echo "c3 $ov failed"; tail -20 $out/c3_ov$ov.err; exit 1; }
   python3 -c "import json; d=json.load(open('$out/c3_ov$ov.json')); b=d['breakdown_ms']; print('c3 ov$ov', d['ms_per_step'], 'h2d', b['ms_h2d'], 'build', b['ms_build'], 'fw', b['ms_fw'], 'scan', b['ms_scan'], 'frac', d['roofline']['frac'] if d['roofline'] else None, 'dev', d['device_entry_ms'])"
