@@ -175,13 +175,15 @@ void srg_destroy(srg_ctx* ctx);
                                      * launches, 1 (whole 128-tiles) / 2 / 4; 0 (default) = by the bulk a
                                      * pivot leaves this rank: >= 2048 tiles 1, >= 1024 tiles 2, else 4
                                      * (C3: 1 on one rank, 2 on two, 4 on more; C1/C2: 4) */
-#define SRG_OPT_FW_STEP 32           /* symmetric FW schedule: 1 = one fused launch per pivot (the next pivot's
-                                     * chain on the launch's first workgroups, its line exchange between ranks
-                                     * inside the launch: stores into the peers' line buffers + arrival flags);
-                                     * 0 = the bulk and the chain on two streams, the exchange a collective;
-                                     * -1 (default) = fused for simulated ranks and for in-process ranks on
-                                     * distinct devices (ranks sharing a GPU set 1 only when each rank's launch
-                                     * has a hardware queue of its own) */
+#define SRG_OPT_FW_STEP 32           /* symmetric FW schedule.  -1 (default) = the bulk and the next pivot's chain
+                                     * on two streams; between ranks the chain exchanges its line segments
+                                     * device-side (stores into the peers' line buffers + arrival words) for
+                                     * simulated ranks and in-process ranks on distinct devices, else with
+                                     * the communicator's allgather.  0 = two streams, always the allgather.
+                                     * 2 = two streams, device-side exchange also for ranks sharing a GPU
+                                     * (each rank's chain stream needs a hardware queue of its own).
+                                     * 1 = one fused launch per pivot (chain on the launch's first
+                                     * workgroups, exchange inside it; measured slower) */
 #define SRG_OPT_FW_OVERLAP 33        /* host entry, one rank: 1 (default) = FW starts while the edge list is still
                                      * crossing PCIe (an undirected list ordered by source row with every edge
                                      * (s, d), s <= d -- a GML complete graph: each block-row of W is split and

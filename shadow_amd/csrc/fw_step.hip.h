@@ -333,4 +333,65 @@ __global__ void __launch_bounds__(256, SB == 1 ? 3 : 4) fw_step(StepArgs<K> a) {
     chain<K, T, SL>(a, w);
 }
 
+// ---- the two-stream chain's device-side exchange (routing.hip SymFw, xmode 1 / 2) ----------------
+// In place of the allgather of LB(k1) on the chain's stream: xmode 2 -- the workgroups copy this
+// rank's segment of LB(k1) (just written by the line launch before it) into every peer's LB(k1) with
+// write-through stores, drain, and the last one to arrive raises this rank's word at every peer, then
+// waits for every peer's word (their segments are in this rank's LB(k1) by then); xmode 1 -- a
+// simulated rank: one workgroup waits the modelled link time.  The next launch on the stream (the
+// pivot closure) starts after this one ends, so its loads see the peers' bytes.
+template <class K>
+struct XchgArgs {
+    const K* seg;                     // this rank's segment of LB(k1)
+    size_t off;                       // its element offset inside LB(k1)
+    size_t n8;                        // its size in 8-byte words
+    K* peer_lb[kMaxPeers];            // each peer's LB(k1) (null for this rank)
+    uint32_t* peer_flags[kMaxPeers];  // each peer's arrival words [pivot * G + from]
+    uint32_t* myflags;
+    uint32_t* cnt;                    // a zeroed word of this pivot: workgroups done copying
+    uint32_t* timeout;
+    int k1, G, g, sys, xmode;
+    uint32_t epoch;
+    uint32_t model_ns;
+};
+
+template <class K>
+__global__ void __launch_bounds__(256) k_line_xchg(XchgArgs<K> a) {
+    __builtin_amdgcn_s_setprio(3);
+    if (a.xmode == 1) {
+        if (threadIdx.x == 0) {
+            const unsigned long long t0 = wall_clock64(), ticks = a.model_ns / 10;  // 100 MHz
+            while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+        }
+        return;
+    }
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(a.seg);
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.n8; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t v = src[i];
+        for (int p = 0; p < a.G; ++p)
+            if (a.peer_lb[p]) st8_wt(reinterpret_cast<uint64_t*>(a.peer_lb[p] + a.off) + i, v, a.sys);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ uint32_t last;
+    if (threadIdx.x == 0) last = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    // every workgroup's stores have drained: publish, then wait for the peers
+    if (a.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int p = 0; p < a.G; ++p)
+        if (a.peer_flags[p]) {
+            uint32_t* f = a.peer_flags[p] + (size_t)a.k1 * a.G + a.g;
+            if (a.sys) __hip_atomic_store(f, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else __hip_atomic_store(f, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    const uint32_t ep = a.epoch;
+    for (int p = 0; p < a.G; ++p)
+        if (p != a.g && !poll_until(a.myflags + (size_t)a.k1 * a.G + p, a.sys, a.timeout, [ep](uint32_t v) { return v == ep; }))
+            break;
+    acquire_for(a.sys);
+}
+
 }  // namespace srg

@@ -1397,6 +1397,8 @@ inline void sym_tiles(srg_ctx& c, const Plan& pl, hipStream_t st, std::vector<in
 // the bulk of kb (tiles of block-rows <= maxI), end() mirrors or exchanges.  fw_line_sym runs it
 // straight through; the host entry's FW beside the H2D (FwOverlap) runs pivots as block-rows of the
 // edge list land, with every line kept (keep_lines) for the late tiles' catch-up.
+int chain_xmode(const srg_ctx& c);
+
 template <class K, int T>
 struct SymFw {
     static constexpr int KCS = 16;
@@ -1413,8 +1415,13 @@ struct SymFw {
     uint32_t* cflags = nullptr;
     const int* tiles = nullptr;
     std::vector<int> own_h, slot_h, first;
-    K* lbuf[2] = {nullptr, nullptr};
+    K* lbuf[3] = {nullptr, nullptr, nullptr};
     K* lball = nullptr;  // keep_lines: line p at lball + p * nb * TT
+    int xmode = 0;       // chain_xmode: how LB(k1) is exchanged
+    std::vector<void*> plb;       // xmode 2: every rank's line-buffer block, arrival words
+    std::vector<uint32_t*> pfl;
+    uint32_t* myflags = nullptr;
+    bool sys = false;
     uint64_t* prof_relax = nullptr;
     int* prof_n = nullptr;
 
@@ -1424,8 +1431,12 @@ struct SymFw {
         g = pl.g;
         multi = c.comm && c.comm->nranks > 1;
         lm = LineMap{nb, G};
+        xmode = chain_xmode(c);
     }
-    K* lb(int p) const { return keep_lines ? lball + (size_t)p * nb * TT : lbuf[p & 1]; }
+    // two line buffers round-robin; three with a device-side exchange (a peer may store LB(k1) while
+    // this rank's bulk of kb - 1 still reads LB(kb - 1), never earlier: the peer's chain of k1 ran
+    // after its exchange of kb, which waited for this rank's line kb, i.e. this rank's bulk of kb - 2)
+    K* lb(int p) const { return keep_lines ? lball + (size_t)p * nb * TT : lbuf[xmode ? p % 3 : p & 1]; }
     void line(const K* lbL, int L, K* lbK, int K1, int mode, int ntiles, hipStream_t s) const {
         if (!ntiles) return;
         if (split == 4)
@@ -1472,9 +1483,25 @@ struct SymFw {
             }
         }
         if (keep_lines) lball = (K*)c.b_xlb.get((size_t)nb * nb * TT * sizeof(K));
-        else {
+        else if (xmode) {  // one block of three (the peers' stores address it by offset)
+            K* x = (K*)c.b_xlb.get(3 * (size_t)nb * TT * sizeof(K));
+            for (int i = 0; i < 3; ++i) lbuf[i] = x + (size_t)i * nb * TT;
+        } else {
             lbuf[0] = (K*)c.b_L0.get(nb * TT * sizeof(K));
             lbuf[1] = (K*)c.b_L1.get(nb * TT * sizeof(K));
+        }
+        if (xmode == 2) {  // every rank's block and arrival words (a host rendezvous per build)
+            const size_t fb = (size_t)nb * G * 4;
+            if (c.b_xflags.bytes < fb) {
+                c.b_xflags.get(fb);
+                HIP_CHECK(hipMemsetAsync(c.b_xflags.p, 0, fb, st));
+            }
+            myflags = (uint32_t*)c.b_xflags.p;
+            HIP_CHECK(hipStreamSynchronize(st));  // zeroed words before any peer may raise one
+            plb.assign(G, nullptr);
+            pfl.assign(G, nullptr);
+            c.comm->share_ptrs(lbuf[0], myflags, plb.data(), pfl.data(), &sys);
+            if (++c.xepoch == 0) ++c.xepoch;
         }
         // closure barrier words: 16 per pivot (arrival counter, changed flag per step), then the
         // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
@@ -1499,7 +1526,9 @@ struct SymFw {
             K* lbn = lb(k1);
             stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
-            if (multi) {  // on the chain's own stream: no cross-queue hop around it
+            if (multi && xmode) {
+                exchange(lbn, k1, aux);
+            } else if (multi) {  // on the chain's own stream: no cross-queue hop around it
                 std::vector<size_t> offs(G), lens(G);
                 for (int r = 0; r < G; ++r) {
                     offs[r] = (size_t)lm.base(r, k1) * TT * sizeof(K);
@@ -1529,6 +1558,39 @@ struct SymFw {
             ++*prof_n;
         }
         if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
+    }
+    // device-side exchange of LB(k1) on the chain's stream (k_line_xchg)
+    void exchange(K* lbn, int k1, hipStream_t s) {
+        XchgArgs<K> a{};
+        a.k1 = k1;
+        a.G = G;
+        a.g = g;
+        a.sys = sys ? 1 : 0;
+        a.xmode = xmode;
+        a.epoch = c.xepoch;
+        a.timeout = c.fw_timeout;
+        a.myflags = myflags;
+        a.cnt = cflags + 16 * k1 + 13;  // a free word of the pivot's group (the closure uses 0..8)
+        a.off = (size_t)lm.base(g, k1) * TT;
+        a.seg = lbn + a.off;
+        a.n8 = (size_t)lm.count(g, k1) * TT * sizeof(K) / 8;
+        int grid = 1;
+        if (xmode == 1) {
+            size_t mx = 0;  // the largest segment a peer sends this rank
+            for (int r = 0; r < G; ++r)
+                if (r != g) mx = std::max(mx, (size_t)lm.count(r, k1) * TT * sizeof(K));
+            a.model_ns = (uint32_t)c.comm->model_xchg_ns(mx);
+        } else {
+            const size_t blk = (size_t)lbn - (size_t)lbuf[0];  // LB(k1)'s offset inside the block
+            for (int r = 0; r < G && r < kMaxPeers; ++r)
+                if (r != g) {
+                    a.peer_lb[r] = (K*)((unsigned char*)plb[r] + blk);
+                    a.peer_flags[r] = pfl[r];
+                }
+            grid = (int)std::max<size_t>(1, std::min<size_t>(64, (a.n8 + 255) / 256));
+        }
+        k_line_xchg<K><<<grid, 256, 0, s>>>(a);
+        HIP_CHECK(hipGetLastError());
     }
     void end(double& ms_xchg) {
         HIP_CHECK(hipGetLastError());
@@ -1771,23 +1833,32 @@ void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t
 
 // Which symmetric FW schedule runs: -1 = the two-stream schedule (fw_line_sym), else the fused
 // launch per pivot with that exchange mode (fw_line_fused): 0 one rank, 1 simulated rank, 2 peers.
-// SRG_OPT_FW_STEP: 1 = fused wherever possible, 0 = never, -1 (auto) = fused for a simulated rank
-// and for in-process ranks on distinct devices; one rank by the environment switch
-// SRG_FW_FUSED (A/B while the default is measured).  RCCL ranks keep the two-stream schedule (their
-// exchange is a collective on the chain's stream).
+// Fused only on request (SRG_OPT_FW_STEP = 1, or SRG_FW_FUSED=1 in the environment under auto): it
+// measured slower than the two-stream schedule at every rank count (sim 8:0 FW 9.1-11.0 vs 6.6 ms,
+// one rank C3 26.2 vs 22.2 ms): the resident bulk workgroups starve the chain's phases.
 int fw_step_mode(const srg_ctx& c) {
     const bool multi = c.comm && c.comm->nranks > 1;
-    if (c.fw_step == 0) return -1;
-    if (!multi) {
-        if (c.fw_step == 1) return 0;
-        const char* e = std::getenv("SRG_FW_FUSED");
-        return e && std::strcmp(e, "1") == 0 ? 0 : -1;
-    }
+    const char* e = std::getenv("SRG_FW_FUSED");
+    const bool env = e && std::strcmp(e, "1") == 0;
+    if (!(c.fw_step == 1 || (c.fw_step == -1 && env))) return -1;
+    if (!multi) return 0;
     if (c.comm->nranks > kMaxPeers) return -1;
     const int dx = c.comm->device_exchange();
+    return dx == 1 ? 1 : dx == 2 ? 2 : -1;
+}
+
+// The two-stream chain's exchange of LB(k1): 0 = the communicator's allgather on the chain's stream,
+// 1 = a simulated rank's modelled device-side exchange, 2 = stores into the peers' line buffers +
+// arrival words (k_line_xchg).  Auto (SRG_OPT_FW_STEP = -1): device-side for simulated ranks and for
+// in-process ranks on distinct devices; 2 forces it (ranks sharing a GPU: each rank's chain stream
+// needs a hardware queue of its own); 0 keeps the collective.
+int chain_xmode(const srg_ctx& c) {
+    const bool multi = c.comm && c.comm->nranks > 1;
+    if (!multi || c.fw_step == 0 || c.comm->nranks > kMaxPeers) return 0;
+    const int dx = c.comm->device_exchange();
     if (dx == 1) return 1;
-    if (dx == 2 && (c.fw_step == 1 || c.comm->distinct_devices())) return 2;
-    return -1;
+    if (dx == 2 && (c.fw_step == 2 || c.comm->distinct_devices())) return 2;
+    return 0;
 }
 
 // the symmetric FW over line buffers applies: undirected, u32 pair-packed 128-tiles or u64 64-tiles
@@ -3625,7 +3696,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_line_split = (int)value;
             return SRG_OK;
         case SRG_OPT_FW_STEP:
-            if (value != 0 && value != 1 && value != -1) return SRG_ERR_ARG;
+            if (value != 0 && value != 1 && value != 2 && value != -1) return SRG_ERR_ARG;
             ctx->fw_step = (int)value;
             return SRG_OK;
         case SRG_OPT_FW_OVERLAP:

@@ -1,6 +1,7 @@
-"""Child process of tests/test_fw_step.py: G in-process ranks on device 0 running the fused FW step
-with the DEVICE-SIDE line exchange (SRG_OPT_FW_STEP = 1: each rank stores its line segments into its
-peers' line buffers and raises arrival flags inside the launch).  Ranks sharing a GPU need a hardware
+"""Child process of tests/test_fw_step.py: G in-process ranks on device 0 running the symmetric FW with
+the DEVICE-SIDE line exchange: the fused step (SRG_OPT_FW_STEP = 1: each rank stores its line segments
+into its peers' line buffers and raises arrival flags inside the launch) and the two-stream chain's
+k_line_xchg (SRG_OPT_FW_STEP = 2: the same stores and flags in a launch on the chain's stream).  Ranks sharing a GPU need a hardware
 queue each for that (one rank's in-kernel wait must not sit in front of a peer's launch), so the
 parent starts this script with GPU_MAX_HW_QUEUES = 16.  Prints one JSON line: per case, whether every
 rank matched the single-GPU two-stream build and the oracle bit for bit."""
@@ -58,6 +59,10 @@ def main():
         dict(G=4, V=1100, seed=13, split=4),
         dict(G=2, V=400, seed=14, split=0, u64=True),
         dict(G=2, V=900, seed=15, split=2, env={"SRG_FW_SB": "1"}),
+        # the two-stream chain with the device-side exchange (k_line_xchg), forced on one GPU
+        dict(G=3, V=900, seed=17, split=2, step=2),
+        dict(G=4, V=1500, seed=18, split=0, step=2),
+        dict(G=2, V=400, seed=19, split=0, u64=True, step=2),
     ]
     if len(sys.argv) > 1 and sys.argv[1] == "diag":
         cases = [dict(G=2, V=900, seed=12, split=2), dict(G=3, V=1000, seed=15, split=2),

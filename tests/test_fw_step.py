@@ -69,8 +69,9 @@ def test_fused_atlas_line_splits(split):
 
 
 def test_fused_device_exchange_ranks():
-    """2-4 in-process ranks on one GPU, line segments exchanged inside the fused launch (peer stores +
-    arrival flags): every rank bit-exact vs the one-rank build and the oracle."""
+    """2-4 in-process ranks on one GPU, line segments exchanged device-side (peer stores + arrival
+    flags) inside the fused launch and by the two-stream chain's exchange launch: every rank bit-exact
+    vs the one-rank build and the oracle."""
     env = dict(os.environ)
     env["GPU_MAX_HW_QUEUES"] = "16"
     p = subprocess.run([sys.executable, "-u", os.path.join(HERE, "fw_step_ranks.py")], env=env, capture_output=True,
