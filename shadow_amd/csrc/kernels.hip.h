@@ -919,27 +919,93 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(K* __restrict__ D, size_t l
 
 // Late tiles (the host entry's FW beside the H2D, routing.hip FwOverlap; one rank, u32 keys): the
 // tiles (I, J >= I) of block-row I, whose edges landed after the bulks of pivots [0, P) ran without
-// them, catch up on pivot p = blockIdx.y:  D(I, J) = min(D(I, J), LB(p)[I] (x) LB(p)[J]), LB(p) the
-// FINAL line of p (kept for every pivot).  Blocked FW's bulk updates of a tile are independent of
-// one another once the lines are final, so this is exactly the skipped work, merged with atomicMin
-// (exact: min is associative; a read of D that already holds another pivot's contribution only
-// lowers this product's operand C, never below the true result).  I, J > p: both operands are
-// stored tiles (p, I), (p, J) read transposed / plain (acol, bcol as the bulk's).
+// them, catch up on pivots p in group blockIdx.y (pg pivots per group):
+//     D(I, J) = min(D(I, J), min over p of LB(p)[I] (x) LB(p)[J]),
+// LB(p) the FINAL line of p (kept for every pivot).  Blocked FW's bulk updates of a tile are
+// independent of one another once the lines are final, so this is exactly the skipped work: one
+// K = 128 pg product per workgroup, C in registers across its pivots, merged with atomicMin once
+// (exact: min is associative; a read of D that already holds another group's contribution only
+// lowers this product's operand C, never below the true result).  One atomicMin pass per pivot
+// (pg = 1) cost ~10 ms of catch-up at C3.  I, J > p: both operands are stored tiles (p, I),
+// (p, J), read in column form.
 template <int T>
 __global__ void __launch_bounds__(256, 3) fw_catchup(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lball,
-                                                     size_t lb_stride, int I, int nb) {
+                                                     size_t lb_stride, int I, int np, int pg) {
     constexpr int KC = 16;
     constexpr size_t TT = (size_t)T * T;
-    const int J = I + (int)blockIdx.x, p = (int)blockIdx.y;
-    const uint32_t* lb = lball + (size_t)p * lb_stride;  // line p: tile j at slot j (one rank)
+    using S = SymOp<T, KC>;
+    constexpr int M = T / 16;
+    constexpr int LDA = T + 2;
+    constexpr int BUF = KC * LDA;
+    constexpr int CPP = T / KC;  // chunks per pivot
+    const int J = I + (int)blockIdx.x, p0 = (int)blockIdx.y * pg, p1 = min(np, p0 + pg);
+    if (p0 >= p1) return;
     uint32_t* C = D + (size_t)I * T * ld + (size_t)J * T;
-    (void)nb;
-    fw_core_lb_e<T, T, KC, false>(C, ld, lb + (size_t)I * TT, true, lb + (size_t)J * TT, true, T,
-                                  [&](int r, int c, uint64_t bits) {
-                                      uint32_t* q = C + (size_t)r * ld + c;
-                                      atomicMin(q, (uint32_t)bits);
-                                      atomicMin(q + 1, (uint32_t)(bits >> 32));
-                                  });
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    u64p* lds = reinterpret_cast<u64p*>(smem_raw);
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    auto opA = [&](int p) { return lball + (size_t)p * lb_stride + (size_t)I * TT; };
+    auto opB = [&](int p) { return lball + (size_t)p * lb_stride + (size_t)J * TT; };
+    S sa, sb;
+    sym_load<T, KC>(sa, opA(p0), T, true, 0);
+    sym_load<T, KC>(sb, opB(p0), T, true, 0);
+    uint32_t c[M][M];
+#pragma unroll
+    for (int a = 0; a < M; ++a)
+#pragma unroll
+        for (int g = 0; g < M / 2; ++g) {
+            VecN<uint32_t, 2> v = ldv<uint32_t, 2>(C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx);
+            c[a][2 * g] = v.v[0];
+            c[a][2 * g + 1] = v.v[1];
+        }
+    sym_store<T, KC>(sa, lds, true);
+    sym_store<T, KC>(sb, lds + (KC / 2) * LDA, true);
+    __syncthreads();
+    const int nch = (p1 - p0) * CPP;
+#pragma unroll 1
+    for (int ch = 0; ch < nch; ++ch) {
+        const u64p* Ap = lds + (ch & 1) * BUF;
+        const u64p* Bp = Ap + (KC / 2) * LDA;
+        if (ch + 1 < nch) {  // issue early
+            const int pn = p0 + (ch + 1) / CPP, k0 = ((ch + 1) % CPP) * KC;
+            sym_load<T, KC>(sa, opA(pn), T, true, k0);
+            sym_load<T, KC>(sb, opB(pn), T, true, k0);
+        }
+#pragma unroll
+        for (int kp = 0; kp < KC / 2; ++kp) {
+            u64p ap[M], bp[M];
+#pragma unroll
+            for (int g = 0; g < M / 2; ++g) {
+                VecN<u64p, 2> va = ldv<u64p, 2>(Ap + kp * LDA + 32 * g + 2 * ty);
+                VecN<u64p, 2> vb = ldv<u64p, 2>(Bp + kp * LDA + 32 * g + 2 * tx);
+                ap[2 * g] = va.v[0];
+                ap[2 * g + 1] = va.v[1];
+                bp[2 * g] = vb.v[0];
+                bp[2 * g + 1] = vb.v[1];
+            }
+#pragma unroll
+            for (int a = 0; a < M; ++a)
+#pragma unroll
+                for (int b = 0; b < M; ++b) {
+                    const u64p s = add_pairs(ap[a], bp[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                }
+        }
+        if (ch + 1 < nch) {  // write late into the other buffer
+            u64p* An = lds + ((ch + 1) & 1) * BUF;
+            sym_store<T, KC>(sa, An, true);
+            sym_store<T, KC>(sb, An + (KC / 2) * LDA, true);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < M; ++a)
+#pragma unroll
+        for (int g = 0; g < M / 2; ++g) {
+            uint32_t* q = C + (size_t)pk_rc(ty, a) * ld + 32 * g + 2 * tx;
+            atomicMin(q, c[a][2 * g]);
+            atomicMin(q + 1, c[a][2 * g + 1]);
+        }
 }
 
 // Line launches of the FW critical chain, one (T/S) x (T/S) sub-tile of a line tile per

@@ -1953,9 +1953,13 @@ struct FwOverlap {
             const unsigned nb64 = (unsigned)(Vp / 64);
             k_w_split<false><<<dim3(nb64, 2), 256, 0, st>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
             if (next > 0) {
+                // pivot groups: enough workgroups for ~3 per CU, each a K = 128 pg product
+                const int tiles = nb - I;
+                const int groups = std::max(1, std::min(next, (768 + tiles - 1) / tiles));
+                const int pg = (next + groups - 1) / groups;
                 set_lds(fw_catchup<T>, lb_lds<uint32_t, T, 16>());
-                fw_catchup<T><<<dim3(nb - I, next), 256, lb_lds<uint32_t, T, 16>(), st>>>(D, Vp, fw->lball, (size_t)nb * TT,
-                                                                                          I, nb);
+                fw_catchup<T><<<dim3(tiles, (next + pg - 1) / pg), 256, lb_lds<uint32_t, T, 16>(), st>>>(
+                    D, Vp, fw->lball, (size_t)nb * TT, I, next, pg);
             }
             HIP_CHECK(hipGetLastError());
         }
