@@ -1103,6 +1103,25 @@ void advise_huge(void* p, size_t bytes) {
     if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
 }
 
+// Fault a fresh output range in from several threads before it is page-locked: hipHostRegister
+// faults the never-touched pages in one thread (49-58 ms for the 1.2 GB C3 table even in 2 MB
+// pages, exposed after FW on a fresh table); each thread writes one byte per page of its slice (the
+// table is an output: its contents are overwritten anyway).
+void prefault(void* p, size_t bytes, int nthreads) {
+    if (!p || bytes < ((size_t)64 << 20)) return;
+    const size_t pg = 4096, per = (bytes / nthreads + pg - 1) / pg * pg;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) {
+        const size_t a = (size_t)t * per, e = std::min(bytes, a + per);
+        if (a >= e) break;
+        th.emplace_back([=]() {
+            volatile unsigned char* b = (volatile unsigned char*)p;
+            for (size_t o = a; o < e; o += pg) b[o] = 0;
+        });
+    }
+    for (auto& x : th) x.join();
+}
+
 // Contexts per device in this process (srg_create / srg_destroy): the FW's cross-stream hops
 // use stream memory operations only when a context is alone on its device (stream_hop).
 std::mutex g_dev_mu;
@@ -1901,6 +1920,43 @@ struct FwOverlap {
     uint64_t prof_relax = 0;
     int prof_n = 0;
     double ms_xchg = 0;
+    // SRG_DEBUG_OVERLAP: timing events (H2D start, each chunk's keys landed, each pivot's bulk done)
+    bool dbg = false;
+    hipEvent_t e0 = nullptr;
+    std::vector<hipEvent_t> ce, pe;
+    std::vector<int> ca;  // block-rows complete after each chunk
+    hipEvent_t tev(hipStream_t s) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        HIP_CHECK(hipEventRecord(e, s));
+        return e;
+    }
+    // after the FW: when each chunk landed and how far the FW had got by then (debug only: syncs)
+    void report() {
+        if (!dbg || !e0) return;
+        HIP_CHECK(hipStreamSynchronize(st));
+        auto ms = [&](hipEvent_t e) {
+            float m = 0;
+            HIP_CHECK(hipEventElapsedTime(&m, e0, e));
+            return m;
+        };
+        std::vector<float> pt(pe.size());
+        for (size_t i = 0; i < pe.size(); ++i) pt[i] = ms(pe[i]);
+        for (size_t i = 0; i < ce.size(); ++i) {
+            const float t = ms(ce[i]);
+            int done = 0;
+            for (float x : pt) done += x <= t;
+            std::fprintf(stderr, "fw-overlap: chunk %2zu landed %6.2f ms, block-rows %3d, pivots done %3d\n", i, t, ca[i], done);
+        }
+        if (!pt.empty()) std::fprintf(stderr, "fw-overlap: last pivot done %.2f ms\n", pt.back());
+        for (hipEvent_t e : ce) HIP_CHECK(hipEventDestroy(e));
+        for (hipEvent_t e : pe) HIP_CHECK(hipEventDestroy(e));
+        HIP_CHECK(hipEventDestroy(e0));
+        ce.clear();
+        pe.clear();
+        ca.clear();
+        e0 = nullptr;
+    }
 
     void init(srg_ctx& cc, uint32_t V_, const std::vector<uint32_t>& nodes_h) {
         c = &cc;
@@ -1921,6 +1977,8 @@ struct FwOverlap {
         fw.reset(new SymFw<uint32_t, T>(cc, pl, D, Vp, st));
         fw->keep_lines = true;
         on = ok = true;
+        dbg = std::getenv("SRG_DEBUG_OVERLAP") != nullptr;
+        if (dbg) e0 = tev(hs);
     }
     // a chunk's edges [e0, e0 + ne) are on the device (in hs order); exc = its exceptions (global
     // index, src, dst) when sequential-pair, null otherwise
@@ -1946,6 +2004,10 @@ struct FwOverlap {
         HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
         // rows below the chunk's last source row are complete (all of them after the last chunk)
         const int newA = last ? nb - 1 : std::min(nb - 1, (int)(prev_src / T) - 1);
+        if (dbg) {
+            ce.push_back(tev(hs));
+            ca.push_back(newA + 1);
+        }
         advance(newA);
     }
     void advance(int newA) {
@@ -1971,6 +2033,7 @@ struct FwOverlap {
         }
         while (next < nb && (next + 1 < nb ? A >= next + 1 : A >= nb - 1)) {
             fw->pivot(next, A);
+            if (dbg) pe.push_back(tev(st));
             ++next;
         }
         if (next == nb && !ended) {
@@ -3214,6 +3277,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         void* view[2] = {nullptr, nullptr};  // device pointers of the mapped registrations
         size_t b[2] = {0, 0};
         hipStream_t wait = nullptr;
+        bool fault = true;
         bool join() {
             if (th.joinable()) th.join();
             return ok;
@@ -3228,6 +3292,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
     } reg;
     reg.device = c->device;
     reg.wait = c->d2h_stream;
+    if (const char* e = std::getenv("SRG_PREFAULT")) reg.fault = std::strcmp(e, "0") != 0;  // A/B
     const bool early = !direct && nn * 12 >= ((size_t)64 << 20);
     const bool ext = (bool)c->ext_reg;
     // a rank of a group that fills only its own rows [n r / N, n (r+1) / N) of a table the ranks
@@ -3249,6 +3314,10 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             if (!reg.b[0] || hipSetDevice(reg.device) != hipSuccess) return;
             advise_huge(reg.p[0], reg.b[0]);
             advise_huge(reg.p[1], reg.b[1]);
+            if (reg.fault) {
+                prefault(reg.p[0], reg.b[0], 8);
+                prefault(reg.p[1], reg.b[1], 8);
+            }
             if (hipHostRegister(reg.p[0], reg.b[0], hipHostRegisterMapped) != hipSuccess) return;
             if (hipHostRegister(reg.p[1], reg.b[1], hipHostRegisterMapped) != hipSuccess) {
                 (void)hipHostUnregister(reg.p[0]);
@@ -3308,8 +3377,10 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         if (ov.on && !coded) ov.ok = false;
         const int ov_early = ov.next;  // pivots enqueued while chunks were still crossing
         if (ov.on && ov.ok && !ov.ended) ov.advance(ov.nb - 1);
-        if (ov.on && std::getenv("SRG_DEBUG_OVERLAP"))
+        if (ov.on && std::getenv("SRG_DEBUG_OVERLAP")) {
             std::fprintf(stderr, "fw-overlap: ok=%d pivots_during_h2d=%d of %d\n", ov.ok ? 1 : 0, ov_early, ov.nb);
+            if (ov.ok) ov.report();
+        }
         LateLoss late;
         late.ls = c->loss_stream;
         if (coded && want_late) start_late_loss(*c, g, dg, hst, late, a0, a1);
