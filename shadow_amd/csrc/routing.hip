@@ -3270,7 +3270,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                float* out_loss, srg_stats* stats, char* errbuf, size_t errlen, bool direct,
                uint32_t* out_key = nullptr, uint64_t* out_diag = nullptr) {
     const bool keys = out_key != nullptr;
-    if (keys && (direct || (c && c->comm && c->comm->nranks > 1) || !out_diag)) {
+    if (keys && (direct || (c && c->comm && c->comm->nranks > 1) || (num_nodes && !out_diag))) {
         set_err(errbuf, errlen, "key table: one rank, shortest paths only");
         return SRG_ERR_ARG;
     }
