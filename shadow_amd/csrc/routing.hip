@@ -2656,11 +2656,10 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     const int wpc = wide ? 1 : 2;
     uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)wpc));
 
-    // label slots (V x 64 x 8 B per resident batch, + 4 B loss words when wide) within about half
-    // of the free HBM
+    // label slots (V x 64 x 8 B per resident batch, 16 B when wide) within about half of the free HBM
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t slot_bytes = (size_t)V * 64 * (wide ? 12 : 8);
+    const size_t slot_bytes = (size_t)V * 64 * (wide ? 16 : 8);
     grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
     const uint32_t nwv = (V + 63) / 64;
     const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
@@ -2668,7 +2667,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     const bool gbits = c.sparse_global_bitmaps || bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / wpc;
     const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
     if (nbatch) {
-        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * V * 64 * 8);
+        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * slot_bytes);
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
@@ -2677,10 +2676,9 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         auto kern = gbits ? k_sparse_bf<SP_G, true> : k_sparse_bf<SP_G, false>;
         if (wide) kern = gbits ? k_sparse_bf<SP_G, true, 4, LabelU64> : k_sparse_bf<SP_G, false, 4, LabelU64>;
         set_lds(kern, lds);
-        uint32_t* slots_loss = wide ? (uint32_t*)c.b_WL.get((size_t)grid * V * 64 * 4) : nullptr;
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
                      selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, gb, c.kout_key, c.kout_diag,
-                     slots_loss, in_w64};
+                     in_w64};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);

@@ -51,9 +51,12 @@ __device__ __forceinline__ unsigned long long lbl_relax(unsigned long long lu, u
 }
 
 // Label policies.  Narrow (u32 latency keys): one u64 per lane, (key << 32) | loss bits, lexmin =
-// u64 min.  Wide (u64 latency keys, for graphs whose used paths pass 2^32-1 units): the latency
-// u64 and the loss bits u32 in two arrays of the same [V][64] shape, lexmin compares both words;
-// the host only takes it when max_lat * V < 2^64, so sums never wrap (saturation is a guard).
+// u64 min.  Wide (u64 latency keys, for graphs whose used paths pass 2^32-1 units): one 16-byte
+// slot per lane {latency u64, loss bits}, read and written by single 16-B vector accesses so that
+// a wave pulling a row another wave is lowering sees either label whole (two separate arrays let a
+// reader pair a new latency with an old, smaller loss, and that candidate could stick: a 1050-vertex
+// case differed in loss); lexmin compares both words.  The host only takes it when
+// max_lat * V < 2^64, so sums never wrap (saturation is a guard).
 struct LabelU32 {
     using T = unsigned long long;
     static constexpr bool wide = false;
@@ -79,8 +82,8 @@ struct LabelU64 {
     };
     static constexpr bool wide = true;
     static constexpr uint64_t LAT_MAX = ~0ull;
-    unsigned long long* L;
-    uint32_t* S;
+    typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+    v2u64* L;  // [V][64] slots: x = latency key, y = loss bits
     __device__ static T inf() { return T{~0ull, 0xFFFFFFFFu}; }
     __device__ static T zero() { return T{0ull, 0u}; }
     __device__ static bool lt(T a, T b) { return a.l < b.l || (a.l == b.l && a.s < b.s); }
@@ -88,11 +91,14 @@ struct LabelU64 {
     __device__ static uint64_t lat(T a) { return a.l; }
     __device__ static uint32_t loss_bits(T a) { return a.s; }
     __device__ T ld(size_t i) const {
-        return T{__builtin_nontemporal_load(&L[i]), __builtin_nontemporal_load(&S[i])};
+        const v2u64 v = __builtin_nontemporal_load(&L[i]);
+        return T{v.x, (uint32_t)v.y};
     }
     __device__ void st(size_t i, T v) const {
-        L[i] = v.l;
-        S[i] = v.s;
+        v2u64 w;
+        w.x = v.l;
+        w.y = v.s;
+        L[i] = w;
     }
     // arc weight: the list holds the arc index, the u64 key is read per relaxation (wave-uniform)
     __device__ static T relax(T u, uint32_t wtag, float b, const uint64_t* in_w64) {
@@ -186,8 +192,7 @@ struct SparseArgs {
     unsigned long long* gbits;   // [gridDim.x][5][nw] vertex bitmaps when they do not fit in LDS (GB = true)
     uint32_t* out_key;           // RoutingInfo key table (null: ns latencies into out_lat), diagonal 0xFFFFFFFF
     uint64_t* out_diag;          // with out_key: the raw self-loop latency per output row
-    uint32_t* slots_loss;        // wide labels: [gridDim.x][V][64] loss bits beside the u64 latencies in `slots`
-    const uint64_t* in_w64;      // wide labels: u64 arc keys
+    const uint64_t* in_w64;      // wide labels: u64 arc keys (`slots` then holds 16-byte labels)
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some dropped lane's new latency is
@@ -228,8 +233,10 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
     uint32_t* w_b = w_w + SP_CAP;   // 1 - arc loss, or SP_OWN
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
     LB lab;
-    lab.L = a.slots + (size_t)blockIdx.x * V * 64;
-    if constexpr (LB::wide) lab.S = a.slots_loss + (size_t)blockIdx.x * V * 64;
+    if constexpr (LB::wide)
+        lab.L = reinterpret_cast<typename LabelU64::v2u64*>(a.slots) + (size_t)blockIdx.x * V * 64;
+    else
+        lab.L = a.slots + (size_t)blockIdx.x * V * 64;
     uint32_t max_sweeps = 0;
     unsigned long long evals = 0;
     uint32_t saturated = 0;  // a finite label + arc reached 2^32-1: INF may then mean "too long", not unreachable
@@ -516,10 +523,10 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                     unsigned long long v = 0;
                     if (j < a.ncols) {
                         const size_t idx = (size_t)a.cols[j] * 64 + lane;
-                        if constexpr (LB::wide)
-                            v = pass ? (unsigned long long)__builtin_nontemporal_load(&lab.S[idx])
-                                     : __builtin_nontemporal_load(&lab.L[idx]);
-                        else
+                        if constexpr (LB::wide) {
+                            const auto w = lab.ld(idx);
+                            v = pass ? (unsigned long long)w.s : w.l;
+                        } else
                             v = lab.ld(idx);
                     }
                     tile[i * 65 + lane] = v;
