@@ -745,7 +745,7 @@ struct srg_ctx {
                                         // two-stream schedule, -1 = auto (SRG_OPT_FW_STEP)
     DevBuf b_xlb, b_xflags;             // fused FW: three line buffers in one block, peers' arrival flags
     uint32_t xepoch = 0;                // fused FW with a device-side exchange: this build's flag value
-    hipEvent_t ev_ov = nullptr;         // FW beside the H2D: chunk landed
+    std::vector<hipEvent_t> ev_ov;      // FW beside the H2D: one "chunk landed" event per chunk
     uint32_t* kout_key = nullptr;       // this call's RoutingInfo key table on the device (key mode), and
     uint64_t* kout_diag = nullptr;      // its diagonal (raw self-loop latencies per position)
     DevBuf b_odiag;
@@ -764,8 +764,9 @@ struct srg_ctx {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         for (uint32_t* p : sig)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate, ev_ov})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_ov) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
             if (e) (void)hipEventDestroy(e);
         if (h_lring) (void)hipHostFree(h_lring);
@@ -1901,13 +1902,16 @@ bool sym_fw_for(const srg_ctx& c, const DevGraph& g) {
 // checks run after the H2D as before (a failed check or certification discards this FW).  Any chunk
 // that is not sequential-pair, or an edge (s, d) with s > d or a source row going backwards,
 // abandons the overlap (ok = false): the build then runs from the landed edge list as usual.
+// The FW's launches are issued by a thread of its own (enq): from the codec's submitting thread,
+// ~80 pivots x ~6 launches and waits delayed the chunk submissions, H2D 8-9 -> 11-13 ms at C3
+// (profiles/r04/c3_overlap_ab.txt).  The submitting thread records one event per landed chunk and
+// queues (rows complete, event); the FW thread waits on the event in its stream and enqueues.
 struct FwOverlap {
     static constexpr int T = 128;
     static constexpr size_t TT = (size_t)T * T;
     srg_ctx* c = nullptr;
     hipStream_t st = nullptr;   // FW (c.stream)
     hipStream_t hs = nullptr;   // H2D chunks (c.comm_stream)
-    hipEvent_t ev = nullptr;
     uint32_t V = 0;
     size_t Vp = 0;
     int nb = 0;
@@ -1915,8 +1919,17 @@ struct FwOverlap {
     std::unique_ptr<SymFw<uint32_t, T>> fw;
     uint32_t *W = nullptr, *WL = nullptr, *D = nullptr;
     unsigned long long* KW = nullptr;
-    int A = -1, next = 0;       // block-rows complete; pivots enqueued
-    bool on = false, ok = false, begun = false, ended = false;
+    int A = -1, next = 0;       // block-rows complete; pivots enqueued (FW thread)
+    std::atomic<bool> ok{false};
+    bool on = false, begun = false, ended = false;
+    // the FW thread and its queue of (block-rows complete, chunk event)
+    std::thread enq;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<int, hipEvent_t>> q;
+    bool closing = false;
+    std::exception_ptr err;
+    size_t nev = 0;  // chunk events used this call
     uint32_t prev_src = 0;
     uint64_t prof_relax = 0;
     int prof_n = 0;
@@ -1983,8 +1996,6 @@ struct FwOverlap {
         D = (uint32_t*)cc.b_D.get(VV * 4);
         KW = (unsigned long long*)cc.b_PRED.get(VV * 8);
         HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, hs));
-        if (!cc.ev_ov) HIP_CHECK(hipEventCreateWithFlags(&cc.ev_ov, hipEventDisableTiming));
-        ev = cc.ev_ov;
         fw.reset(new SymFw<uint32_t, T>(cc, pl, D, Vp, st));
         fw->keep_lines = true;
         // event waits for the chain's hops here: with the value hops (k_hop_set / k_hop_wait) a bulk
@@ -1992,9 +2003,54 @@ struct FwOverlap {
         // table in 5 of 6 runs of tests/test_fw_step.py's atlas case after test_events.py and
         // test_fw_overlap.py in one process, none with event waits (SRG_STREAM_HOPS=events: 3 of 3)
         fw->value_hops = false;
-        on = ok = true;
+        on = true;
+        ok = true;
         dbg = std::getenv("SRG_DEBUG_OVERLAP") != nullptr;
         if (dbg) e0 = tev(hs);
+        enq = std::thread([this]() { run(); });
+    }
+    void run() {  // the FW thread: wait on each landed chunk in the FW stream, enqueue what it completes
+        try {
+            HIP_CHECK(hipSetDevice(c->device));
+            for (;;) {
+                std::pair<int, hipEvent_t> it;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&]() { return closing || !q.empty(); });
+                    if (q.empty()) return;
+                    it = q.front();
+                    q.pop_front();
+                }
+                if (!ok) continue;
+                HIP_CHECK(hipStreamWaitEvent(st, it.second, 0));
+                advance(it.first);
+            }
+        } catch (...) {
+            err = std::current_exception();
+            ok = false;
+        }
+    }
+    // every queued chunk enqueued (or dropped); rethrows the FW thread's error
+    void finish() {
+        if (!enq.joinable()) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            closing = true;
+        }
+        cv.notify_one();
+        enq.join();
+        if (err) std::rethrow_exception(err);
+    }
+    ~FwOverlap() {
+        if (enq.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                closing = true;
+                ok = false;
+            }
+            cv.notify_one();
+            enq.join();
+        }
     }
     // a chunk's edges [e0, e0 + ne) are on the device (in hs order); exc = its exceptions (global
     // index, src, dst) when sequential-pair, null otherwise
@@ -2016,15 +2072,25 @@ struct FwOverlap {
         }
         k_w_key<<<grid_for(ne), kThreads, 0, hs>>>(ne, dg.src + e0, dg.dst + e0, dg.lat + e0, 1, nullptr, KW, Vp, V);
         HIP_CHECK(hipGetLastError());
+        // one event per chunk (the FW thread may not have waited on the previous one yet)
+        if (nev == c->ev_ov.size()) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->ev_ov.push_back(e);
+        }
+        hipEvent_t ev = c->ev_ov[nev++];
         HIP_CHECK(hipEventRecord(ev, hs));
-        HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
         // rows below the chunk's last source row are complete (all of them after the last chunk)
         const int newA = last ? nb - 1 : std::min(nb - 1, (int)(prev_src / T) - 1);
         if (dbg) {
             ce.push_back(tev(hs));
             ca.push_back(newA + 1);
         }
-        advance(newA);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.emplace_back(newA, ev);
+        }
+        cv.notify_one();
     }
     void advance(int newA) {
         for (int I = A + 1; I <= newA; ++I) {
@@ -3388,6 +3454,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // codec_in gives up on the first chunk that is neither)
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) &&
                            codec_in(*c, g, dg, hst, a0, a1, !want_late, all_narrow, all_seq, on_chunk);
+        if (ov.on) ov.finish();  // the FW thread has enqueued every landed chunk's work
         if (ov.on && !coded) ov.ok = false;
         const int ov_early = ov.next;  // pivots enqueued while chunks were still crossing
         if (ov.on && ov.ok && !ov.ended) ov.advance(ov.nb - 1);
