@@ -351,6 +351,9 @@ def verify_rows(edges, table_lat, table_loss, V, k=4, seed=4242):
     return {"rows": rows, "bit_exact": bool(ok)}
 
 
+COLD_BREAKDOWN = {}  # cold_call: srg_create vs the first call, and that call's own stage times
+
+
 def cold_call(make, args, edges, V):
     """srg_create (or srg_multi_create) + the first srg_compute_shortest_paths on freshly
     allocated, never-touched output arrays -- what Shadow's one call per simulation pays
@@ -359,11 +362,17 @@ def cold_call(make, args, edges, V):
     t0 = time.perf_counter()
     router = make()
     apply_options(router, args)
+    t1 = time.perf_counter()
     lat = np.empty((V, V), dtype=np.uint64)   # not pre-faulted
     loss = np.empty((V, V), dtype=np.float32)
-    router.compute_shortest_paths(edges, np.arange(V, dtype=np.uint32), lat, loss)
-    ms = (time.perf_counter() - t0) * 1e3
+    t = router.compute_shortest_paths(edges, np.arange(V, dtype=np.uint32), lat, loss)
+    t2 = time.perf_counter()
+    ms = (t2 - t0) * 1e3
     del lat, loss
+    st = t.stats
+    COLD_BREAKDOWN.update({"create_ms": round((t1 - t0) * 1e3, 1), "first_call_ms": round((t2 - t1) * 1e3, 1),
+                           **{k: round(st[k], 2) for k in ("ms_h2d", "ms_fw", "ms_scan", "ms_d2h", "ms_host_register")
+                              if k in st}})
     return router, ms
 
 
@@ -736,6 +745,8 @@ def main():
             extra_cfg["fallback"] = fallback
         if cold_ms is not None:
             extra_cfg["cold_call_ms"] = round(cold_ms, 1)
+            if COLD_BREAKDOWN:
+                extra_cfg["cold_call_breakdown_ms"] = dict(COLD_BREAKDOWN)
         emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg,
              {"device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None, "verified_rows": ver,
               "routing_info": ri_times})
