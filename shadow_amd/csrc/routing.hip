@@ -1419,17 +1419,6 @@ inline void sym_tiles(srg_ctx& c, const Plan& pl, hipStream_t st, std::vector<in
 // edge list land, with every line kept (keep_lines) for the late tiles' catch-up.
 int chain_xmode(const srg_ctx& c);
 
-template <class K, int T, int SB, int SL>
-void launch_step(const StepArgs<K>& a, int grid, hipStream_t st) {
-    constexpr size_t lds = step_lds<K, T, SB, SL>();
-    static bool attr = false;
-    if (!attr) {
-        set_lds(fw_step<K, T, SB, SL>, lds);
-        attr = true;
-    }
-    fw_step<K, T, SB, SL><<<grid, 256, lds, st>>>(a);
-}
-
 template <class K, int T>
 struct SymFw {
     static constexpr int KCS = 16;
@@ -1454,11 +1443,6 @@ struct SymFw {
     std::vector<uint32_t*> pfl;
     uint32_t* myflags = nullptr;
     bool sys = false;
-    // chain_one: the chain of k1 (line w.r.t. kb, exchange, closure, line w.r.t. k1) as ONE fw_step
-    // launch of chain workgroups only (ntile = 0) on the chain's stream, beside the bulk launch on
-    // the main stream (SRG_CHAIN_ONE=1; ranks with a device-side exchange, line split >= 2)
-    bool chain_one = false;
-    int chain_wgs = 256;
     uint64_t* prof_relax = nullptr;
     int* prof_n = nullptr;
 
@@ -1469,9 +1453,6 @@ struct SymFw {
         multi = c.comm && c.comm->nranks > 1;
         lm = LineMap{nb, G};
         xmode = chain_xmode(c);
-        const char* e1 = std::getenv("SRG_CHAIN_ONE");
-        chain_one = multi && xmode && e1 && std::strcmp(e1, "1") == 0;
-        if (const char* e2 = std::getenv("SRG_FW_CH")) chain_wgs = std::max(T / 16 * T / 16, std::atoi(e2));
     }
     // two line buffers round-robin; three with a device-side exchange (a peer may store LB(k1) while
     // this rank's bulk of kb - 1 still reads LB(kb - 1), never earlier: the peer's chain of k1 ran
@@ -1565,23 +1546,19 @@ struct SymFw {
         if (k1 < nb) {
             K* lbn = lb(k1);
             stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
-            if (chain_one && split >= 2) {
-                chain_launch(lbk, kb, lbn, k1, aux);
-            } else {
-                line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
-                if (multi && xmode) {
-                    exchange(lbn, k1, aux);
-                } else if (multi) {  // on the chain's own stream: no cross-queue hop around it
-                    std::vector<size_t> offs(G), lens(G);
-                    for (int r = 0; r < G; ++r) {
-                        offs[r] = (size_t)lm.base(r, k1) * TT * sizeof(K);
-                        lens[r] = (size_t)lm.count(r, k1) * TT * sizeof(K);
-                    }
-                    c.comm->allgatherv(lbn, offs.data(), lens.data(), aux);
+            line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
+            if (multi && xmode) {
+                exchange(lbn, k1, aux);
+            } else if (multi) {  // on the chain's own stream: no cross-queue hop around it
+                std::vector<size_t> offs(G), lens(G);
+                for (int r = 0; r < G; ++r) {
+                    offs[r] = (size_t)lm.base(r, k1) * TT * sizeof(K);
+                    lens[r] = (size_t)lm.count(r, k1) * TT * sizeof(K);
                 }
-                close_pivot(lbn, k1, aux);
-                line(lbn, k1, lbn, k1, 1, nb, aux);
+                c.comm->allgatherv(lbn, offs.data(), lens.data(), aux);
             }
+            close_pivot(lbn, k1, aux);
+            line(lbn, k1, lbn, k1, 1, nb, aux);
             HIP_CHECK(hipGetLastError());
         }
         // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
@@ -1602,42 +1579,6 @@ struct SymFw {
             ++*prof_n;
         }
         if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
-    }
-    // the whole chain of k1 as one launch of chain workgroups (fw_step.hip.h phases A, X, C, D)
-    void chain_launch(const K* lbk, int kb, K* lbn, int k1, hipStream_t s) {
-        StepArgs<K> a{};
-        a.D = D;
-        a.ld = Vp;
-        a.lbk = lbk;
-        a.lbn = lbn;
-        a.kb = kb;
-        a.k1 = k1;
-        a.lm = lm;
-        a.g = g;
-        a.tiles = tiles;
-        a.ntile = 0;
-        a.CH = std::max(T / 16 * T / 16, std::min(chain_wgs, nb * split * split));
-        a.sync = cflags + (size_t)16 * k1;
-        a.timeout = c.fw_timeout;
-        a.xmode = xmode;
-        a.sys = sys ? 1 : 0;
-        a.epoch = c.xepoch;
-        a.myflags = myflags;
-        if (xmode == 1) {
-            size_t mx = 0;
-            for (int r = 0; r < G; ++r)
-                if (r != g) mx = std::max(mx, (size_t)lm.count(r, k1) * TT * sizeof(K));
-            a.model_ns = (uint32_t)c.comm->model_xchg_ns(mx);
-        } else {
-            const size_t blk = (size_t)lbn - (size_t)lbuf[0];
-            for (int r = 0; r < G && r < kMaxPeers; ++r)
-                if (r != g) {
-                    a.peer_lbn[r] = (K*)((unsigned char*)plb[r] + blk);
-                    a.peer_flags[r] = pfl[r];
-                }
-        }
-        if (split == 2) launch_step<K, T, 1, 2>(a, a.CH, s);
-        else launch_step<K, T, 1, 4>(a, a.CH, s);
     }
     // device-side exchange of LB(k1) on the chain's stream (k_line_xchg)
     void exchange(K* lbn, int k1, hipStream_t s) {
@@ -1730,6 +1671,16 @@ void fw_sym_finish(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, 
 // per-pivot critical path has no cross-stream hop and no separate collective: peers exchange their
 // line segments inside the launch (xmode 2: stores into every peer's line buffer + arrival flags;
 // xmode 1: a simulated rank waits the modelled link time; 0: one rank).
+template <class K, int T, int SB, int SL>
+void launch_step(const StepArgs<K>& a, int grid, hipStream_t st) {
+    constexpr size_t lds = step_lds<K, T, SB, SL>();
+    static bool attr = false;
+    if (!attr) {
+        set_lds(fw_step<K, T, SB, SL>, lds);
+        attr = true;
+    }
+    fw_step<K, T, SB, SL><<<grid, 256, lds, st>>>(a);
+}
 
 template <class K, int T>
 void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax, int& prof_n,

@@ -63,10 +63,6 @@ def main():
         dict(G=3, V=900, seed=17, split=2, step=2),
         dict(G=4, V=1500, seed=18, split=0, step=2),
         dict(G=2, V=400, seed=19, split=0, u64=True, step=2),
-        # ... with the chain as one launch of chain workgroups beside the bulk (SRG_CHAIN_ONE)
-        dict(G=3, V=900, seed=21, split=2, step=2, env={"SRG_CHAIN_ONE": "1"}),
-        dict(G=4, V=1500, seed=22, split=4, step=2, env={"SRG_CHAIN_ONE": "1"}),
-        dict(G=2, V=400, seed=23, split=2, u64=True, step=2, env={"SRG_CHAIN_ONE": "1"}),
     ]
     if len(sys.argv) > 1 and sys.argv[1] == "diag":
         cases = [dict(G=2, V=900, seed=12, split=2), dict(G=3, V=1000, seed=15, split=2),

@@ -78,4 +78,5 @@ def test_fused_device_exchange_ranks():
                        text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     res = json.loads(p.stdout.strip().splitlines()[-1])
-    assert all(r["ok"] for r in res), res
+    bad = [(r["case"], r["errors"], [(d["lat_bad"], d["loss_bad"], d["rows"][:4]) for d in r["diag"]]) for r in res if not r["ok"]]
+    assert not bad, bad
