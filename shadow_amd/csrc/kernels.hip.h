@@ -380,18 +380,6 @@ __device__ __forceinline__ u64p add_pairs(u64p x, u64p y) {
     return r;
 }
 
-// Two relaxations of a packed pair: c = min(c, x_k + y_k, x_{k+1} + y_{k+1}).  The halves are
-// added as two 32-bit adds (full-rate v_add_u32; no carry can cross them, see above) rather than
-// one v_lshl_add_u64: the 64-bit op issues at about a quarter of the rate and every v_min3 reading
-// its result waited an s_nop (451 of them in the bulk tile's k loop), while two adds + v_min3
-// measured 0.334 against 0.187 wave-instructions per SIMD cycle
-// (profiles/r01_valu_rate_microbench.txt: 9 vs 10.7 cycles per two relaxations).
-__device__ __forceinline__ uint32_t pair_relax(uint32_t c, u64p x, u64p y) {
-    const uint32_t s0 = (uint32_t)x + (uint32_t)y;
-    const uint32_t s1 = (uint32_t)(x >> 32) + (uint32_t)(y >> 32);
-    return KeyOps<uint32_t>::min3(c, s0, s1);
-}
-
 __device__ __forceinline__ int pk_rc(int t, int e) { return 32 * (e >> 1) + 2 * t + (e & 1); }
 
 template <int T, int KC>
@@ -518,7 +506,8 @@ __device__ __forceinline__ void fw_tile_pk(uint32_t* __restrict__ D, size_t ld, 
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b) {
-                    c[a][b] = pair_relax(c[a][b], xa[a], xb[b]);
+                    const u64p s = add_pairs(xa[a], xb[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         };
         // one register set: the other resident waves hide the LDS latency
@@ -700,7 +689,8 @@ __device__ __forceinline__ void fw_core_lb_e(uint32_t* __restrict__ C, size_t ld
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b) {
-                    c[a][b] = pair_relax(c[a][b], ap[a], bp[b]);
+                    const u64p s = add_pairs(ap[a], bp[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         }
         if (ch + 1 < NCH) {  // write late into the other buffer
@@ -997,7 +987,8 @@ __global__ void __launch_bounds__(256, 3) fw_catchup(uint32_t* __restrict__ D, s
             for (int a = 0; a < M; ++a)
 #pragma unroll
                 for (int b = 0; b < M; ++b) {
-                    c[a][b] = pair_relax(c[a][b], ap[a], bp[b]);
+                    const u64p s = add_pairs(ap[a], bp[b]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
                 }
         }
         if (ch + 1 < nch) {  // write late into the other buffer
