@@ -1930,6 +1930,7 @@ struct FwOverlap {
     bool closing = false;
     std::exception_ptr err;
     size_t nev = 0;  // chunk events used this call
+    int catchup_wgs = 768;  // catch-up launch size target (SRG_CATCHUP_WGS: A/B)
     uint32_t prev_src = 0;
     uint64_t prof_relax = 0;
     int prof_n = 0;
@@ -2007,6 +2008,7 @@ struct FwOverlap {
         ok = true;
         dbg = std::getenv("SRG_DEBUG_OVERLAP") != nullptr;
         if (dbg) e0 = tev(hs);
+        if (const char* e = std::getenv("SRG_CATCHUP_WGS")) catchup_wgs = std::max(1, std::atoi(e));
         enq = std::thread([this]() { run(); });
     }
     void run() {  // the FW thread: wait on each landed chunk in the FW stream, enqueue what it completes
@@ -2099,7 +2101,7 @@ struct FwOverlap {
             if (next > 0) {
                 // pivot groups: enough workgroups for ~3 per CU, each a K = 128 pg product
                 const int tiles = nb - I;
-                const int groups = std::max(1, std::min(next, (768 + tiles - 1) / tiles));
+                const int groups = std::max(1, std::min(next, (catchup_wgs + tiles - 1) / tiles));
                 const int pg = (next + groups - 1) / groups;
                 set_lds(fw_catchup<T>, lb_lds<uint32_t, T, 16>());
                 fw_catchup<T><<<dim3(tiles, (next + pg - 1) / pg), 256, lb_lds<uint32_t, T, 16>(), st>>>(
