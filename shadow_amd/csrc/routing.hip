@@ -1920,6 +1920,7 @@ struct FwOverlap {
     uint32_t *W = nullptr, *WL = nullptr, *D = nullptr;
     unsigned long long* KW = nullptr;
     int A = -1, next = 0;       // block-rows complete; pivots enqueued (FW thread)
+    int splitA = -1;            // block-rows split from KW on the H2D stream (submitting thread)
     std::atomic<bool> ok{false};
     bool on = false, begun = false, ended = false;
     // the FW thread and its queue of (block-rows complete, chunk event)
@@ -2074,6 +2075,15 @@ struct FwOverlap {
         }
         k_w_key<<<grid_for(ne), kThreads, 0, hs>>>(ne, dg.src + e0, dg.dst + e0, dg.lat + e0, 1, nullptr, KW, Vp, V);
         HIP_CHECK(hipGetLastError());
+        // rows below the chunk's last source row are complete (all of them after the last chunk):
+        // their tiles are split from KW here, on the H2D stream (beside FW: k_w_split writes the
+        // upper tiles of its block-row, which FW does not touch before the row is complete, and
+        // lower-triangle entries FW never reads)
+        const int newA = last ? nb - 1 : std::min(nb - 1, (int)(prev_src / T) - 1);
+        for (int I = splitA + 1; I <= newA; ++I)
+            k_w_split<false><<<dim3((unsigned)(Vp / 64), 2), 256, 0, hs>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
+        splitA = std::max(splitA, newA);
+        HIP_CHECK(hipGetLastError());
         // one event per chunk (the FW thread may not have waited on the previous one yet)
         if (nev == c->ev_ov.size()) {
             hipEvent_t e;
@@ -2082,8 +2092,6 @@ struct FwOverlap {
         }
         hipEvent_t ev = c->ev_ov[nev++];
         HIP_CHECK(hipEventRecord(ev, hs));
-        // rows below the chunk's last source row are complete (all of them after the last chunk)
-        const int newA = last ? nb - 1 : std::min(nb - 1, (int)(prev_src / T) - 1);
         if (dbg) {
             ce.push_back(tev(hs));
             ca.push_back(newA + 1);
@@ -2096,8 +2104,8 @@ struct FwOverlap {
     }
     void advance(int newA) {
         for (int I = A + 1; I <= newA; ++I) {
-            const unsigned nb64 = (unsigned)(Vp / 64);
-            k_w_split<false><<<dim3(nb64, 2), 256, 0, st>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
+            if (I > splitA)  // (only after the H2D: the submitting thread splits every landed row)
+                k_w_split<false><<<dim3((unsigned)(Vp / 64), 2), 256, 0, st>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
             if (next > 0) {
                 // pivot groups: enough workgroups for ~3 per CU, each a K = 128 pg product
                 const int tiles = nb - I;
