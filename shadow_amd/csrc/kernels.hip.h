@@ -928,9 +928,10 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(K* __restrict__ D, size_t l
 // lowers this product's operand C, never below the true result).  One atomicMin pass per pivot
 // (pg = 1) cost ~10 ms of catch-up at C3.  I, J > p: both operands are stored tiles (p, I),
 // (p, J), read in column form.
+// (blockIdx.x enumerates the tiles (I, J >= I) of the block-rows I0, I0 + 1, ... row by row.)
 template <int T>
 __global__ void __launch_bounds__(256, 3) fw_catchup(uint32_t* __restrict__ D, size_t ld, const uint32_t* __restrict__ lball,
-                                                     size_t lb_stride, int I, int np, int pg) {
+                                                     size_t lb_stride, int I0, int nb, int np, int pg) {
     constexpr int KC = 16;
     constexpr size_t TT = (size_t)T * T;
     using S = SymOp<T, KC>;
@@ -938,7 +939,9 @@ __global__ void __launch_bounds__(256, 3) fw_catchup(uint32_t* __restrict__ D, s
     constexpr int LDA = T + 2;
     constexpr int BUF = KC * LDA;
     constexpr int CPP = T / KC;  // chunks per pivot
-    const int J = I + (int)blockIdx.x, p0 = (int)blockIdx.y * pg, p1 = min(np, p0 + pg);
+    int I = I0, t = (int)blockIdx.x;
+    while (t >= nb - I) t -= nb - I++;
+    const int J = I + t, p0 = (int)blockIdx.y * pg, p1 = min(np, p0 + pg);
     if (p0 >= p1) return;
     uint32_t* C = D + (size_t)I * T * ld + (size_t)J * T;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];

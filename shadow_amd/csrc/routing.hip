@@ -2103,20 +2103,21 @@ struct FwOverlap {
         cv.notify_one();
     }
     void advance(int newA) {
-        for (int I = A + 1; I <= newA; ++I) {
+        for (int I = A + 1; I <= newA; ++I)
             if (I > splitA)  // (only after the H2D: the submitting thread splits every landed row)
                 k_w_split<false><<<dim3((unsigned)(Vp / 64), 2), 256, 0, st>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
-            if (next > 0) {
-                // pivot groups: enough workgroups for ~3 per CU, each a K = 128 pg product
-                const int tiles = nb - I;
-                const int groups = std::max(1, std::min(next, (catchup_wgs + tiles - 1) / tiles));
-                const int pg = (next + groups - 1) / groups;
-                set_lds(fw_catchup<T>, lb_lds<uint32_t, T, 16>());
-                fw_catchup<T><<<dim3(tiles, (next + pg - 1) / pg), 256, lb_lds<uint32_t, T, 16>(), st>>>(
-                    D, Vp, fw->lball, (size_t)nb * TT, I, next, pg);
-            }
-            HIP_CHECK(hipGetLastError());
+        if (next > 0 && newA > A) {
+            // the newly complete block-rows (A, newA] catch up in ONE launch over all their tiles;
+            // pivot groups sized for ~3 workgroups per CU, each a K = 128 pg product
+            int tiles = 0;
+            for (int I = A + 1; I <= newA; ++I) tiles += nb - I;
+            const int groups = std::max(1, std::min(next, (catchup_wgs + tiles - 1) / tiles));
+            const int pg = (next + groups - 1) / groups;
+            set_lds(fw_catchup<T>, lb_lds<uint32_t, T, 16>());
+            fw_catchup<T><<<dim3(tiles, (next + pg - 1) / pg), 256, lb_lds<uint32_t, T, 16>(), st>>>(
+                D, Vp, fw->lball, (size_t)nb * TT, A + 1, nb, next, pg);
         }
+        HIP_CHECK(hipGetLastError());
         A = std::max(A, newA);
         if (A < 0) return;
         if (!begun) {
