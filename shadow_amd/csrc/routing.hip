@@ -2841,7 +2841,10 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
         if (n) fail(SRG_ERR_ARG, "nodes given for an empty graph");
         return;
     }
-    Prelude P = prelude(c, g, nodes, n, st, true);
+    // with the FW already queued beside the H2D the edge checks go on the (idle) H2D stream: on st
+    // they would wait behind the whole FW before the host could read them
+    const bool ov_fw = ov && ov->on && ov->ok && ov->begun;
+    Prelude P = prelude(c, g, nodes, n, ov_fw ? c.comm_stream : st, true);
     if (n == 0) return;
     // u64 keys hold path sums below INF = 2^62 (a sum of two keys never wraps); a graph whose
     // worst-case path could reach 2^62 still runs, and only a used pair left at INF is an error:
