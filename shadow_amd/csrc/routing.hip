@@ -636,8 +636,7 @@ struct HostPool {
 struct SdmaAgents {
     bool ok = false;
     hsa_agent_t gpu{}, cpu{};
-    uint32_t engine = 0;   // hsa_amd_sdma_engine_id_t bit of the engine used for D2H
-    uint32_t engine2 = 0;  // a second engine: each copy is split over both (0 = one engine)
+    uint32_t engine = 0;  // hsa_amd_sdma_engine_id_t bit of the engine used for D2H
     void init(int device) {
         if (hsa_init() != HSA_STATUS_SUCCESS) return;
         int bus = -1, dev = -1, dom = -1;
@@ -676,10 +675,6 @@ struct SdmaAgents {
         gpu = q.gpu;
         cpu = q.cpu;
         engine = mask & (~mask + 1);  // lowest available engine
-        const uint32_t rest = mask & ~engine;
-        engine2 = rest & (~rest + 1);
-        if (const char* e = std::getenv("SRG_SDMA_ENGINES"))  // A/B: 1 = one engine
-            if (std::atoi(e) == 1) engine2 = 0;
         ok = true;
     }
 };
@@ -1025,25 +1020,15 @@ struct HostSink {
                 err = "hipEventSynchronize failed before a D2H copy";
                 continue;
             }
-            // two engines when there are: the halves of the copy cross PCIe side by side
-            const size_t half = sdma->engine2 && j.bytes >= ((size_t)8 << 20) ? (j.bytes / 2) & ~(size_t)4095 : 0;
-            const size_t parts[2] = {j.bytes - half, half};
-            const uint32_t eng[2] = {sdma->engine, sdma->engine2};
-            size_t off = 0;
-            for (int q = 0; q < 2 && err.empty(); ++q) {
-                if (!parts[q]) continue;
-                hsa_signal_t sg;
-                if (hsa_signal_create(1, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
-                    err = "hsa_signal_create failed";
-                    break;
-                }
-                sigs.push_back(sg);
-                if (hsa_amd_memory_async_copy_on_engine((unsigned char*)j.dst + off, sdma->cpu, (const unsigned char*)j.src + off,
-                                                        sdma->gpu, parts[q], 0, nullptr, sg, (hsa_amd_sdma_engine_id_t)eng[q],
-                                                        true) != HSA_STATUS_SUCCESS)
-                    err = "hsa_amd_memory_async_copy_on_engine failed";
-                off += parts[q];
+            hsa_signal_t sg;
+            if (hsa_signal_create(1, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
+                err = "hsa_signal_create failed";
+                continue;
             }
+            sigs.push_back(sg);
+            if (hsa_amd_memory_async_copy_on_engine(j.dst, sdma->cpu, j.src, sdma->gpu, j.bytes, 0, nullptr, sg,
+                                                    (hsa_amd_sdma_engine_id_t)sdma->engine, true) != HSA_STATUS_SUCCESS)
+                err = "hsa_amd_memory_async_copy_on_engine failed";
         }
     }
     // rows [row0, row0 + rows) of a row-major n-column device array, after the work queued on st
