@@ -394,61 +394,4 @@ __global__ void __launch_bounds__(256) k_line_xchg(XchgArgs<K> a) {
     acquire_for(a.sys);
 }
 
-// ---- early closure (routing.hip SymFw, device-side exchange) ----------------------------------
-// The pivot closure needs only the pivot tile of LB(k1), not the whole line: line A stores its tiles
-// into every peer's LB(k1) itself (line_item mode 0 with peers, write-through), the workgroups of the
-// pivot tile raise an arrival word for it as soon as they are done, and the last workgroup of the
-// launch the word for the whole segment.  A rank's closure then waits only for the pivot tile
-// (k_wait_words), line D for every segment -- the rest of the line crosses while the pivot closes.
-// Words in `sync` (this pivot's 16): [9] line-A items done, [10] pivot-tile items done, [14..15] the
-// time line A ended (simulated ranks).  Arrival words in each rank's `myflags`: [k1 * G + from] a
-// segment, [nb * G + k1] the pivot tile (raised by its owner).
-template <class K, int T, int SL>
-__global__ void __launch_bounds__(256, 2) k_line_a_x(StepArgs<K> a) {
-    __builtin_amdgcn_s_setprio(3);
-    constexpr int SS = SL * SL;
-    const LineMap& lm = a.lm;
-    const int G = lm.G;
-    const int i = (int)blockIdx.x;
-    const int j = lm.j0(a.g, a.k1) + G * (i / SS);
-    line_item<K, T, SL>(a, 0, j, i % SS);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x != 0 || a.xmode != 2) return;
-    auto raise = [&](size_t idx) {
-        if (a.sys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        for (int p = 0; p < G; ++p)
-            if (a.peer_flags[p]) {
-                uint32_t* f = a.peer_flags[p] + idx;
-                if (a.sys) __hip_atomic_store(f, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                else __hip_atomic_store(f, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-    };
-    if (j == a.k1 && __hip_atomic_fetch_add(&a.sync[10], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == SS - 1)
-        raise((size_t)lm.nb * G + a.k1);
-    if (__hip_atomic_fetch_add(&a.sync[9], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
-        raise((size_t)a.k1 * G + a.g);
-}
-
-// One wave waits: xmode 2 -- for the words [w0, w0 + n) of myflags except `skip` to hold the epoch;
-// xmode 1 (simulated) -- until `ns` after the time in sync[14..15] (stamped there by the first wait of
-// the pivot, `stamp` = 1).  Bounded like every wait of the FW (the timeout word).
-template <class K>
-__global__ void k_wait_words(StepArgs<K> a, size_t w0, int n, int skip, uint32_t ns, int stamp) {
-    if (threadIdx.x != 0) return;
-    unsigned long long* t0p = reinterpret_cast<unsigned long long*>(a.sync + 14);
-    if (a.xmode == 1) {
-        const unsigned long long now = wall_clock64();
-        if (stamp) *t0p = now;
-        const unsigned long long t0 = stamp ? now : *t0p, ticks = ns / 10;  // 100 MHz
-        while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
-        return;
-    }
-    const uint32_t ep = a.epoch;
-    for (int p = 0; p < n; ++p)
-        if (p != skip && !poll_until(a.myflags + w0 + p, a.sys, a.timeout, [ep](uint32_t v) { return v == ep; })) break;
-    acquire_for(a.sys);
-}
-
 }  // namespace srg

@@ -1443,10 +1443,6 @@ struct SymFw {
     std::vector<uint32_t*> pfl;
     uint32_t* myflags = nullptr;
     bool sys = false;
-    // early closure (device-side exchange, line split >= 2): line A stores into the peers itself and
-    // the closure waits only for the pivot tile (fw_step.hip.h k_line_a_x / k_wait_words);
-    // SRG_EARLY_CLOSE=0 keeps line A -> whole exchange -> closure
-    bool early = true;
     uint64_t* prof_relax = nullptr;
     int* prof_n = nullptr;
 
@@ -1457,8 +1453,6 @@ struct SymFw {
         multi = c.comm && c.comm->nranks > 1;
         lm = LineMap{nb, G};
         xmode = chain_xmode(c);
-        const char* ec = std::getenv("SRG_EARLY_CLOSE");
-        early = !(ec && std::strcmp(ec, "0") == 0);
     }
     // two line buffers round-robin; three with a device-side exchange (a peer may store LB(k1) while
     // this rank's bulk of kb - 1 still reads LB(kb - 1), never earlier: the peer's chain of k1 ran
@@ -1518,7 +1512,7 @@ struct SymFw {
             lbuf[1] = (K*)c.b_L1.get(nb * TT * sizeof(K));
         }
         if (xmode == 2) {  // every rank's block and arrival words (a host rendezvous per build)
-            const size_t fb = ((size_t)nb * G + nb) * 4;  // segments [k1 * G + from], pivot tiles [nb * G + k1]
+            const size_t fb = (size_t)nb * G * 4;
             if (c.b_xflags.bytes < fb) {
                 c.b_xflags.get(fb);
                 HIP_CHECK(hipMemsetAsync(c.b_xflags.p, 0, fb, st));
@@ -1552,9 +1546,6 @@ struct SymFw {
         if (k1 < nb) {
             K* lbn = lb(k1);
             stream_hop(c, 0, st, aux, c.ev_a);  // st: bulk of kb - 1 done
-            if (multi && xmode && early && split >= 2) {
-                early_chain(lbk, kb, lbn, k1, aux);
-            } else {
             line(lbk, kb, lbn, k1, 0, lm.count(g, k1), aux);
             if (multi && xmode) {
                 exchange(lbn, k1, aux);
@@ -1568,7 +1559,6 @@ struct SymFw {
             }
             close_pivot(lbn, k1, aux);
             line(lbn, k1, lbn, k1, 1, nb, aux);
-            }
             HIP_CHECK(hipGetLastError());
         }
         // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
@@ -1589,57 +1579,6 @@ struct SymFw {
             ++*prof_n;
         }
         if (k1 < nb) stream_hop(c, 1, aux, st, c.ev_d);  // the chain of k1 (LB(k1) final) before the bulk of k1
-    }
-    // the chain of k1 with the early closure: line A (own tiles, into the peers too) -> the pivot
-    // tile's arrival -> closure -> every segment's arrival -> line w.r.t. k1
-    void early_chain(const K* lbk, int kb, K* lbn, int k1, hipStream_t s) {
-        StepArgs<K> a{};
-        a.D = D;
-        a.ld = Vp;
-        a.lbk = lbk;
-        a.lbn = lbn;
-        a.kb = kb;
-        a.k1 = k1;
-        a.lm = lm;
-        a.g = g;
-        a.sync = cflags + (size_t)16 * k1;
-        a.timeout = c.fw_timeout;
-        a.xmode = xmode;
-        a.sys = sys ? 1 : 0;
-        a.epoch = c.xepoch;
-        a.myflags = myflags;
-        uint32_t piv_ns = 0, seg_ns = 0;
-        if (xmode == 1) {
-            size_t mx = 0;
-            for (int r = 0; r < G; ++r)
-                if (r != g) mx = std::max(mx, (size_t)lm.count(r, k1) * TT * sizeof(K));
-            piv_ns = (uint32_t)c.comm->model_xchg_ns(TT * sizeof(K));
-            seg_ns = (uint32_t)c.comm->model_xchg_ns(mx);
-        } else {
-            const size_t blk = (size_t)lbn - (size_t)lbuf[0];
-            for (int r = 0; r < G && r < kMaxPeers; ++r)
-                if (r != g) {
-                    a.peer_lbn[r] = (K*)((unsigned char*)plb[r] + blk);
-                    a.peer_flags[r] = pfl[r];
-                }
-        }
-        const int nA = lm.count(g, k1) * split * split;
-        if (nA) {
-            if (split == 2)
-                k_line_a_x<K, T, 2><<<nA, 256, lb_lds<K, T / 2, line_kc<2>()>(), s>>>(a);
-            else
-                k_line_a_x<K, T, 4><<<nA, 256, lb_lds<K, T / 4, line_kc<4>()>(), s>>>(a);
-        }
-        if (xmode == 1)
-            k_wait_words<K><<<1, 64, 0, s>>>(a, 0, 0, -1, piv_ns, 1);
-        else if (lm.owner(k1, k1) != g)
-            k_wait_words<K><<<1, 64, 0, s>>>(a, (size_t)nb * G + k1, 1, -1, 0, 0);
-        close_pivot(lbn, k1, s);
-        if (xmode == 1)
-            k_wait_words<K><<<1, 64, 0, s>>>(a, 0, 0, -1, seg_ns, 0);
-        else
-            k_wait_words<K><<<1, 64, 0, s>>>(a, (size_t)k1 * G, G, g, 0, 0);
-        line(lbn, k1, lbn, k1, 1, nb, s);
     }
     // device-side exchange of LB(k1) on the chain's stream (k_line_xchg)
     void exchange(K* lbn, int k1, hipStream_t s) {
