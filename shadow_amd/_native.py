@@ -171,7 +171,8 @@ def lib():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python shadow_amd/build.py` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-    L = ctypes.CDLL(LIB_PATH)
+    # SRG_LIB_PATH: load another build of the library (A/B of two builds in one tree; diagnostics)
+    L = ctypes.CDLL(os.environ.get("SRG_LIB_PATH") or LIB_PATH)
     c = ctypes
     L.srg_create.restype = c.c_int
     L.srg_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.c_char_p, c.c_size_t]

@@ -673,7 +673,7 @@ __device__ __forceinline__ void fw_core_lb_e(uint32_t* __restrict__ C, size_t ld
             sym_load<TM, KC>(sa, Ab, ldab, acol, (ch + 1) * KC);
             sym_load<TM, KC>(sb, Bb, ldab, bcol, (ch + 1) * KC);
         }
-#pragma unroll
+#pragma unroll 2
         for (int kp = 0; kp < KC / 2; ++kp) {
             u64p ap[M], bp[M];
 #pragma unroll
@@ -688,9 +688,16 @@ __device__ __forceinline__ void fw_core_lb_e(uint32_t* __restrict__ C, size_t ld
 #pragma unroll
             for (int a = 0; a < M; ++a)
 #pragma unroll
-                for (int b = 0; b < M; ++b) {
-                    const u64p s = add_pairs(ap[a], bp[b]);
-                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                for (int b = 0; b < M; b += 2) {
+                    // two pair-adds, then their two v_min3: a v_min3 reading an add's result no
+                    // longer follows it directly, which cost a hazard wait (s_nop) per pair; with
+                    // the k-pair loop unrolled by 2 instead of fully (its hoisted LDS reads then fit
+                    // the 168-VGPR budget: 156, no spill) the bulk launch runs 2 % faster
+                    // (0.253-0.255 vs 0.258-0.262 ms, tools/gpu_r04v.sh)
+                    const u64p s0 = add_pairs(ap[a], bp[b]);
+                    const u64p s1 = add_pairs(ap[a], bp[b + 1]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s0, (uint32_t)(s0 >> 32));
+                    c[a][b + 1] = KeyOps<uint32_t>::min3(c[a][b + 1], (uint32_t)s1, (uint32_t)(s1 >> 32));
                 }
         }
         if (ch + 1 < NCH) {  // write late into the other buffer
@@ -989,9 +996,11 @@ __global__ void __launch_bounds__(256, 3) fw_catchup(uint32_t* __restrict__ D, s
 #pragma unroll
             for (int a = 0; a < M; ++a)
 #pragma unroll
-                for (int b = 0; b < M; ++b) {
-                    const u64p s = add_pairs(ap[a], bp[b]);
-                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s, (uint32_t)(s >> 32));
+                for (int b = 0; b < M; b += 2) {  // (interleaved as in fw_core_lb_e)
+                    const u64p s0 = add_pairs(ap[a], bp[b]);
+                    const u64p s1 = add_pairs(ap[a], bp[b + 1]);
+                    c[a][b] = KeyOps<uint32_t>::min3(c[a][b], (uint32_t)s0, (uint32_t)(s0 >> 32));
+                    c[a][b + 1] = KeyOps<uint32_t>::min3(c[a][b + 1], (uint32_t)s1, (uint32_t)(s1 >> 32));
                 }
         }
         if (ch + 1 < nch) {  // write late into the other buffer
