@@ -5,6 +5,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("%s: %s\n", #x, hipGetErrorString(e_)); std::exit(1); } } while (0)
 
@@ -14,7 +17,9 @@ static double ms(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-int main() {
+// usage: init_probe [par]   (par: the first four streams created by four threads at once)
+int main(int argc, char** argv) {
+    const bool par = argc > 1 && std::strcmp(argv[1], "par") == 0;
     auto T = std::chrono::steady_clock::now();
     auto t = T;
     int n = 0;
@@ -24,7 +29,18 @@ int main() {
     CK(hipSetDevice(0));
     std::printf("hipSetDevice                        %8.2f ms\n", ms(t));
     hipStream_t s[6];
-    for (int i = 0; i < 6; ++i) {
+    if (par) {
+        t = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (int i = 0; i < 4; ++i)
+            th.emplace_back([&s, i]() {
+                CK(hipSetDevice(0));
+                CK(hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking));
+            });
+        for (auto& x : th) x.join();
+        std::printf("4 x hipStreamCreate in 4 threads    %8.2f ms\n", ms(t));
+    }
+    for (int i = par ? 4 : 0; i < 6; ++i) {
         t = std::chrono::steady_clock::now();
         CK(hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking));
         std::printf("hipStreamCreate #%d                  %8.2f ms\n", i, ms(t));
