@@ -2477,11 +2477,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                 if (c1 == c0) continue;
                 const uint32_t nblk = (nbTT5 + 3) / 4 * ((c1 - c0 + 7) / 8);
-                static const int scan_pipe = [] {
-                    const char* e = std::getenv("SRG_SCAN_PIPE");
-                    return e ? std::atoi(e) : 0;
-                }();
-                (scan_pipe == 1 ? tight_v5<1> : scan_pipe == 2 ? tight_v5<2> : tight_v5<0>)<<<8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                tight_v5<<<8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
                     DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0, v5_goff,
                     (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
                 HIP_CHECK(hipGetLastError());

@@ -190,13 +190,7 @@ struct alignas(64) V5Grp {
 // rows by 4, and both come out of that XCD's L2 after the first read.  (With one source block per
 // XCD the rows were shared 64 ways, but every record stream came from the Infinity Cache, and the
 // scalar record loads are what each group waits for.)
-// PIPE (round 4): the next chunk's rows staged by LDS-DMA (no staging registers) and the pair loop
-// software-pipelined one group deep -- group p + 4's row reads are issued before group p's checks,
-// so each group's LDS round trip overlaps the previous group's arithmetic.
-// PIPE = 1 sized for 2 waves per SIMD (144 VGPRs, no spill, one workgroup per CU), 2 for 4 waves
-// per SIMD (128 VGPRs; one 8-B spill pair in the hit paths)
-template <int PIPE>
-__global__ void __launch_bounds__(512, PIPE == 1 ? 2 : 4) tight_v5(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
+__global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ DST, size_t npad, uint32_t dst_bytes,
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
@@ -242,90 +236,13 @@ __global__ void __launch_bounds__(512, PIPE == 1 ? 2 : 4) tight_v5(const uint32_
         for (uint32_t i = 0; i < 4; ++i)
             *reinterpret_cast<uint4*>(&rows[buf * (V5_UC * V5_SB) + (srow + 16 * i) * V5_SB + scol]) = sv[i];
     };
-    // LDS-DMA staging (PIPE): wave w's lanes carry rows 2w + 16i (lanes 0-31) and 2w + 16i + 1
-    // (lanes 32-63), 16 B each, landing lane-linear = the rows' 1-KB span; buffer loads, so rows
-    // past DST read 0 as in stage_load
-    auto stage_dma = [&](uint32_t k, uint32_t buf) {
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-            const uint32_t u = k * V5_UC + 2 * wave + 16 * i + (lane >> 5);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, &rows[buf * (V5_UC * V5_SB) + (2 * wave + 16 * i) * V5_SB], 16,
-                                                     (u * (uint32_t)npad + c * V5_SB + (lane & 31) * 4) * 4u, 0, 0, 0);
-        }
-    };
-    if constexpr (PIPE) {
-        stage_dma(0, 0);
-    } else {
-        stage_load(0);
-        stage_store(0);
-    }
+    stage_load(0);
+    stage_store(0);
     __syncthreads();
     const unsigned char* lds = reinterpret_cast<const unsigned char*>(rows);
     for (uint32_t k = 0; k < nK; ++k) {
-        if (k + 1 < nK) {
-            if constexpr (PIPE)
-                stage_dma(k + 1, (k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
-            else
-                stage_load(k + 1);  // issue early, write after the chunk
-        }
-        if (active && PIPE) {
-            const size_t q = ((size_t)b * nK + k) * V5_WAVES + wave;
-            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q]);
-            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q + 1]);
-            const uint32_t vb = (k & 1u) * (V5_UC * V5_SB * 4u) + lane * 8u;
-            // both slot offsets masked to whole rows of one buffer (0x7E00: 0 .. 63 x 512): groups
-            // read past p1 (the next slice's, or the uninitialised slack) stay inside the ring
-            auto rows_of = [&](const V5Grp& g, uint2* A) {
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) {
-                    A[2 * i] = *reinterpret_cast<const uint2*>(lds + vb + (g.v[4 * i] & 0x7E00u));
-                    A[2 * i + 1] = *reinterpret_cast<const uint2*>(lds + vb + (g.v[4 * i + 2] & 0x7E00u));
-                }
-            };
-            auto check = [&](const V5Grp& g, const uint2* A, uint32_t p) {
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) {
-                    const uint32_t tl = g.v[4 * i] >> 16;
-                    const uint32_t dl = ndl[tl], dh = ndh[tl];
-                    const uint32_t w0 = g.v[4 * i + 1], w1 = g.v[4 * i + 3];
-                    const uint32_t x0l = A[2 * i].x + w0 + dl, x0h = A[2 * i].y + w0 + dh;
-                    const uint32_t x1l = A[2 * i + 1].x + w1 + dl, x1h = A[2 * i + 1].y + w1 + dh;
-                    const uint32_t m = min(min(x0l, x0h), min(x1l, x1h));
-                    if (__builtin_expect(__ballot(m == 0) != 0, 0)) {
-                        const uint32_t e0 = 2 * (p + i);
-                        uint32_t sl = stl[tl], sh = sth[tl];
-                        if (x0l == 0) sl = (sl == PRED_NONE) ? e0 : PRED_MULTI;
-                        if (x1l == 0) sl = (sl == PRED_NONE) ? e0 + 1 : PRED_MULTI;
-                        if (x0h == 0) sh = (sh == PRED_NONE) ? e0 : PRED_MULTI;
-                        if (x1h == 0) sh = (sh == PRED_NONE) ? e0 + 1 : PRED_MULTI;
-                        stl[tl] = sl;
-                        sth[tl] = sh;
-                    }
-                }
-            };
-            if (p0 < p1) {
-                const V5Grp* G = reinterpret_cast<const V5Grp*>(rec);  // group p = G[p / 4]
-                V5Grp g0 = G[p0 / 4];
-                uint2 A[8], B[8];
-                rows_of(g0, A);
-                V5Grp g1 = G[p0 / 4 + 1];
-                for (uint32_t p = p0;;) {
-                    rows_of(g1, B);  // group p + 4's rows in flight during group p's checks
-                    const V5Grp g2 = G[p / 4 + 2];
-                    check(g0, A, p);
-                    p += 4;
-                    if (p >= p1) break;
-                    rows_of(g2, A);
-                    const V5Grp g3 = G[p / 4 + 2];
-                    check(g1, B, p);
-                    p += 4;
-                    if (p >= p1) break;
-                    g0 = g2;
-                    g1 = g3;
-                }
-            }
-        }
-        if (active && !PIPE) {
+        if (k + 1 < nK) stage_load(k + 1);  // issue early, write after the chunk
+        if (active) {
             const size_t q = ((size_t)b * nK + k) * V5_WAVES + wave;
             const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q]);
             const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q + 1]);
@@ -364,8 +281,8 @@ __global__ void __launch_bounds__(512, PIPE == 1 ? 2 : 4) tight_v5(const uint32_
             }
         }
         if (k + 1 < nK) {
-            if constexpr (!PIPE) stage_store((k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
-            __syncthreads();  // (PIPE: drains the chunk's LDS-DMA, vmcnt)
+            stage_store((k + 1) & 1u);  // the other buffer: its readers (chunk k - 1) passed the last barrier
+            __syncthreads();
         }
     }
     if (!active) return;
