@@ -1734,8 +1734,7 @@ void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, 
                                                                               kChainPrio);
     HIP_CHECK(hipGetLastError());
     constexpr int NC = (T / 16) * (T / 16);
-    int CH = std::max(NC, std::min(256, nb * SL * SL));
-    if (const char* e = std::getenv("SRG_FW_CH")) CH = std::max(NC, std::atoi(e));  // experiments
+    const int CH = std::max(NC, std::min(256, nb * SL * SL));
     const bool prof = c.profiling && nb > 2;
     if (prof) {
         while (c.prof_events.size() < (size_t)2 * nb) {
@@ -1931,7 +1930,7 @@ struct FwOverlap {
     bool closing = false;
     std::exception_ptr err;
     size_t nev = 0;  // chunk events used this call
-    int catchup_wgs = 768;  // catch-up launch size target (SRG_CATCHUP_WGS: A/B)
+    static constexpr int catchup_wgs = 768;  // catch-up launch size target (128 / 256 / 1536 measured slower)
     uint32_t prev_src = 0;
     uint64_t prof_relax = 0;
     int prof_n = 0;
@@ -2009,7 +2008,6 @@ struct FwOverlap {
         ok = true;
         dbg = std::getenv("SRG_DEBUG_OVERLAP") != nullptr;
         if (dbg) e0 = tev(hs);
-        if (const char* e = std::getenv("SRG_CATCHUP_WGS")) catchup_wgs = std::max(1, std::atoi(e));
         enq = std::thread([this]() { run(); });
     }
     void run() {  // the FW thread: wait on each landed chunk in the FW stream, enqueue what it completes
