@@ -189,6 +189,11 @@ void srg_destroy(srg_ctx* ctx);
                                      * (s, d), s <= d -- a GML complete graph: each block-row of W is split and
                                      * caught up on the pivots already run as soon as its edges have landed);
                                      * 0 = FW after the whole list (any list falls back to that by itself) */
+#define SRG_OPT_TEST_FAULT 34         /* TEST HOOK ONLY (never set in production): 1 = overwrite the closed FW matrix
+                                     * with zeros after FW (a lost synchronisation's result: the build must fail
+                                     * with SRG_ERR_INTERNAL, not return it); 2 = nonzero FW sync words and zero
+                                     * line buffers before each symmetric FW (a recycled allocation: the build
+                                     * must still be exact); 0 (default) = off */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

@@ -48,6 +48,7 @@ SRG_OPT_LATE_LOSS = 30
 SRG_OPT_FW_LINE_SPLIT = 31
 SRG_OPT_FW_STEP = 32
 SRG_OPT_FW_OVERLAP = 33
+SRG_OPT_TEST_FAULT = 34
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

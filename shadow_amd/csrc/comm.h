@@ -34,20 +34,19 @@ struct Comm {
     virtual void bcast(void* buf, size_t bytes, int root, hipStream_t s) = 0;
     virtual void allgatherv(void* buf, const size_t* offs, const size_t* lens, hipStream_t s) = 0;
     virtual void allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t s) = 0;
-    // Device-side exchange of the FW line buffers inside the fused per-pivot launch
-    // (fw_step.hip.h): 0 = not available (collectives only), 1 = modelled (a simulated rank: the
-    // launch waits model_xchg_ns), 2 = peer pointers (share_ptrs).
+    // Device-side exchange of the FW line buffers (xchg.hip.h k_line_xchg): 0 = not available
+    // (collectives only), 1 = modelled (a simulated rank: the exchange waits model_xchg_ns), 2 = peer
+    // pointers (share_ptrs).
     virtual int device_exchange() const { return 0; }
     virtual double model_xchg_ns(size_t) const { return 0.0; }
-    // every rank on its own device: the fused launches of different ranks never share a hardware
-    // queue, so one rank's in-kernel wait cannot block a peer's launch (the device-side exchange is
-    // the default then; ranks sharing a GPU opt in, SRG_OPT_FW_EXCHANGE)
+    // every rank on its own device
     virtual bool distinct_devices() const { return false; }
-    // collective: every rank publishes its line-buffer block and arrival-flag array; on return
-    // lbs[r] / flags[r] are rank r's (reachable from this rank's kernels), sys = some rank is on
-    // another device (system-scope fences and stores)
-    virtual void share_ptrs(void*, uint32_t*, void** lbs, uint32_t** flags, bool* sys) {
-        (void)lbs, (void)flags, (void)sys;
+    // collective: every rank publishes its line-buffer block and arrival-flag array and proposes the
+    // build's flag value; on return lbs[r] / flags[r] are rank r's (reachable from this rank's
+    // kernels), sys = some rank is on another device (system-scope fences and stores), *epoch = the
+    // largest value proposed (every rank raises and waits for the same value)
+    virtual void share_ptrs(void*, uint32_t*, void** lbs, uint32_t** flags, bool* sys, uint32_t* epoch) {
+        (void)lbs, (void)flags, (void)sys, (void)epoch;
         throw CommError("device-side exchange unsupported by this communicator");
     }
 };

@@ -159,8 +159,9 @@ struct LocalGroup {
         int device = 0;
         hipEvent_t ev_arrive = nullptr, ev_done = nullptr;
         std::vector<uint32_t> host;  // allreduce staging
-        void* xlb = nullptr;         // share_ptrs: line-buffer block, arrival flags
+        void* xlb = nullptr;         // share_ptrs: line-buffer block, arrival flags, proposed flag value
         uint32_t* xflags = nullptr;
+        uint32_t xepoch = 0;
     };
     std::vector<Slot> slots;
     bool aborted = false;  // a rank failed outside the collective protocol: release the others
@@ -319,17 +320,21 @@ struct LocalComm final : Comm {
                 if (g->slots[p].device == g->slots[q].device) return false;
         return true;
     }
-    void share_ptrs(void* lb, uint32_t* flags, void** lbs, uint32_t** fl, bool* sys) override {
+    void share_ptrs(void* lb, uint32_t* flags, void** lbs, uint32_t** fl, bool* sys, uint32_t* epoch) override {
         g->slots[rank].xlb = lb;
         g->slots[rank].xflags = flags;
+        g->slots[rank].xepoch = *epoch;
         g->barrier();
         bool other = false;
+        uint32_t ep = 0;
         for (int p = 0; p < nranks; ++p) {
             lbs[p] = g->slots[p].xlb;
             fl[p] = g->slots[p].xflags;
             other |= g->slots[p].device != device;
+            ep = std::max(ep, g->slots[p].xepoch);
         }
         *sys = other;
+        *epoch = ep;
         g->barrier();  // every rank has read every slot
     }
     void allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t s) override {

@@ -1121,8 +1121,8 @@ __device__ __forceinline__ void st_wt(K* p, K v) {
 // the launch).  Keys <= INF = 2^31 - 1: no sum wraps.  P is read and written write-through
 // (grid_sync); the previous kernel's plain stores are visible at the launch boundary.  K = u64:
 // keys <= INF = 2^62, the same.
-// The closure's body for output block (by, bx) of nwg participating workgroups (the fused FW
-// step runs it on its first chain workgroups, fw_step.hip.h); A, B, sh: LDS scratch.
+// The closure's body for output block (by, bx) of nwg participating workgroups; A, B, sh: LDS
+// scratch.
 template <class K, int T>
 __device__ __forceinline__ void close_body(K* __restrict__ P, uint32_t* __restrict__ sync, uint32_t* __restrict__ timeout,
                                            int by, int bx, uint32_t nwg, K (*A)[T + 1], K (*B)[17], uint32_t* sh) {

@@ -36,12 +36,13 @@
 #include "../../include/shadow_routing.h"
 #include "internal.h"
 #include "kernels.hip.h"
+#include "guards.h"
 #include "edge_codec.h"
 #include "tight_sparse.hip.h"
 #include "comm.h"
 #include "sparse.hip.h"
 #include "events.hip.h"
-#include "fw_step.hip.h"
+#include "xchg.hip.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -95,6 +96,7 @@ struct EdgeStats {
     unsigned long long unit;      // gcd of the non-self-loop latencies (0: none, or all zero)
     uint32_t bad_endpoint;        // an endpoint >= V
     uint32_t lat_overflow;        // a non-self-loop latency == UINT64_MAX (ns conversion overflow)
+    unsigned long long min_lat_inv;  // ~(min latency over non-self-loop edges) (0: no such edge)
 };
 
 struct Flags {
@@ -105,6 +107,7 @@ struct Flags {
     unsigned long long first_bad;  // direct paths: first (i*n+j) with edge count != 1
     uint32_t wrap;                 // k_wrap_edges: a relaxation the reference would run wraps u64
     uint32_t wrap_inf;             // k_wrap_edges: a relaxation from a vertex left at INF (unknown distance)
+    uint32_t impossible;           // k_certify: a used off-diagonal key below the smallest edge key (guards.h)
 };
 
 constexpr int kThreads = 256;
@@ -151,7 +154,7 @@ __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const 
                             const uint64_t* __restrict__ lat, const float* __restrict__ loss, uint32_t V,
                             uint32_t* __restrict__ selfcnt, uint64_t* __restrict__ self_lat,
                             float* __restrict__ self_loss, EdgeStats* st) {
-    unsigned long long mx = 0;
+    unsigned long long mx = 0, mn = 0;  // mn = ~min: a max reduction like mx (0 = no edge yet)
     uint32_t bad = 0, ovf = 0;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < E; e += (size_t)gridDim.x * blockDim.x) {
         const uint32_t s = src[e], t = dst[e];
@@ -166,6 +169,7 @@ __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const 
             if (loss) self_loss[s] = loss[e];  // null: the loss arrives later (k_self_loss)
         } else {
             mx = l > mx ? l : mx;
+            mn = ~l > mn ? ~l : mn;
             ovf |= (l == UINT64_MAX);
         }
     }
@@ -173,8 +177,11 @@ __global__ void k_edge_scan(uint64_t E, const uint32_t* __restrict__ src, const 
     for (int off = 32; off > 0; off >>= 1) {
         unsigned long long o = __shfl_down(mx, off, 64);
         mx = o > mx ? o : mx;
+        o = __shfl_down(mn, off, 64);
+        mn = o > mn ? o : mn;
     }
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_lat, mx);
+    if ((threadIdx.x & 63) == 0 && mn) atomicMax(&st->min_lat_inv, mn);
     if (bad) atomicOr(&st->bad_endpoint, 1u);
     if (ovf) atomicOr(&st->lat_overflow, 1u);
 }
@@ -341,12 +348,15 @@ __global__ void k_init_d(const K* __restrict__ W, K* __restrict__ D, size_t ld) 
 // Row kernels over (used row x used column) arrays: one workgroup per row (grid = rows), the
 // threads striding over the columns -- no 64-bit division per element (the grid-stride form with
 // i / ncols ran 10x below HBM rate: 0.6 ms per C3 pass).
+// Also the impossible-result guard (guards.h): a used off-diagonal key below the smallest edge key
+// (0 included) cannot be a path length -- a fault inside the builder, never returned as OK.
 template <class K>
 __global__ void __launch_bounds__(256) k_certify(const K* __restrict__ D, size_t ld, const uint32_t* __restrict__ rows,
                                                  uint32_t nrows, const uint32_t* __restrict__ cols, uint32_t ncols,
-                                                 Flags* flags) {
-    const K* Dr = D + (size_t)rows[blockIdx.x] * ld;
-    uint32_t hit = 0;
+                                                 K min_key, Flags* flags) {
+    const uint32_t s = rows[blockIdx.x];
+    const K* Dr = D + (size_t)s * ld;
+    uint32_t hit = 0, bad = 0;
     constexpr uint32_t U = 8;  // independent loads in flight per thread (the gather is latency-bound)
     for (uint32_t j0 = threadIdx.x; j0 < ncols; j0 += blockDim.x * U) {
         uint32_t cc[U];
@@ -359,9 +369,14 @@ __global__ void __launch_bounds__(256) k_certify(const K* __restrict__ D, size_t
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) d[u] = Dr[cc[u]];
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) hit |= (j0 + u * blockDim.x < ncols) & (d[u] == KeyOps<K>::INF);
+        for (uint32_t u = 0; u < U; ++u) {
+            const bool in = j0 + u * blockDim.x < ncols;
+            hit |= in & (d[u] == KeyOps<K>::INF);
+            bad |= in & impossible_key<K>(d[u], min_key, cc[u] == s);
+        }
     }
     if (__ballot(hit) && (threadIdx.x & 63) == 0) atomicOr(&flags->inf_in_used_row, 1u);
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags->impossible, 1u);
 }
 
 template <class K>
@@ -740,16 +755,18 @@ struct srg_ctx {
     uint32_t* sig[2] = {nullptr, nullptr};  // stream_hop signals (HSA signal memory), their last values
     uint32_t sig_val[2] = {0, 0};
     bool hop_values = false;            // this build's hops use the signals (stream_hop)
+    unsigned long long hop_bound_ticks = 200000000ull;  // a value hop's wait bound (100 MHz ticks; SymFw::begin)
+    hipEvent_t ev_fwreset = nullptr;    // SymFw::begin: the chain stream after the reset of the FW sync words
     int fw_line_split = 0;              // symmetric FW: line sub-tiles per dimension (0 = auto) (SRG_OPT_FW_LINE_SPLIT)
-    int fw_step = -1;                   // symmetric FW: 1 = one fused launch per pivot (fw_step.hip.h), 0 = the
-                                        // two-stream schedule, -1 = auto (SRG_OPT_FW_STEP)
-    DevBuf b_xlb, b_xflags;             // fused FW: three line buffers in one block, peers' arrival flags
-    uint32_t xepoch = 0;                // fused FW with a device-side exchange: this build's flag value
+    int fw_step = -1;                   // symmetric FW's line exchange between ranks (SRG_OPT_FW_STEP, chain_xmode)
+    DevBuf b_xlb, b_xflags;             // line buffers (kept lines / the exchange's three), peers' arrival flags
+    uint32_t xepoch = 0;                // device-side exchange: this build's flag value (agreed in share_ptrs)
     std::vector<hipEvent_t> ev_ov;      // FW beside the H2D: one "chunk landed" event per chunk
     uint32_t* kout_key = nullptr;       // this call's RoutingInfo key table on the device (key mode), and
     uint64_t* kout_diag = nullptr;      // its diagonal (raw self-loop latencies per position)
     DevBuf b_odiag;
     int fw_overlap = 1;                 // host entry: FW starts while the edge list arrives (SRG_OPT_FW_OVERLAP)
+    int test_fault = 0;                 // TEST HOOK (SRG_OPT_TEST_FAULT): 1 = zero D after FW, 2 = stale FW sync words
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -764,7 +781,7 @@ struct srg_ctx {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         for (uint32_t* p : sig)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate, ev_fwreset})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_ov) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
@@ -1132,24 +1149,36 @@ std::map<int, int> g_dev_ctx;
 // HSA signal memory cost 5 us per hop against 11 us for hipEventRecord + hipStreamWaitEvent
 // (tools/xq_probe.hip; 1-3 ms of FW at N = 2..8).  The wait is a polling kernel the
 // runtime knows nothing about, so it is safe only while every wait is queued behind the write it
-// waits for: true for one context (its host thread enqueues each write before the wait, and
-// streams sharing a hardware queue keep that order), not for several contexts on one device
-// (in-process rank groups: two waits could each block the queue holding the other's write), nor
-// under a profiler that serialises dispatches (rocprofv3 --pmc hung on it): those use events
-// (and SRG_STREAM_HOPS=events forces them).
+// waits for: true for one context -- ONE host thread enqueues both halves of every hop, the write
+// first (fw_line_sym: the calling thread; FwOverlap: its FW thread, which issues every launch on
+// the FW and chain streams, the submitting thread only the H2D stream), and streams sharing a
+// hardware queue keep that order -- not for several contexts on one device (in-process rank
+// groups: two waits could each block the queue holding the other's write), nor under a profiler
+// that serialises dispatches (rocprofv3 --pmc hung on it): those use events (and
+// SRG_STREAM_HOPS=events forces them).
 // The value form is a pair of one-wave kernels of our own instead of hipStreamWriteValue32 /
 // hipStreamWaitValue32 (the same mechanism: the runtime's wait is a polling blit kernel too), so
-// that the wait is bounded: past ~2 s it raises the FW timeout word and returns, and the host
+// that the wait is bounded: past its bound it raises the FW timeout word and returns, and the host
 // reports SRG_ERR_HIP after FW instead of hanging on a mis-ordered enqueue.
+// The wait also returns as soon as the timeout word is set (a closure barrier gave up: nothing
+// after it is valid).  That word and the closure barrier words are reset per build on the FW
+// stream; SymFw::begin orders the chain stream after that reset with an EVENT.  Without it (rounds
+// 3-4) a chain-stream wait could run before the reset, read the previous occupant's value of the
+// word (a recycled allocation: nonzero), return at once, and the reset then erased the evidence:
+// the chain ran ahead of line 0 and the build returned an all-zero table with rc = 0, or a closure
+// counted arrivals into words the reset then zeroed (the barrier timeouts) -- DESIGN.md §5.
 __global__ void k_hop_set(uint32_t* sig, uint32_t v) {
     if (threadIdx.x == 0) __hip_atomic_store(sig, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ void k_hop_wait(const uint32_t* sig, uint32_t v, uint32_t* timeout) {
+__global__ void k_hop_wait(const uint32_t* sig, uint32_t v, uint32_t* timeout, unsigned long long bound_ticks) {
     if (threadIdx.x != 0) return;
     const unsigned long long t0 = wall_clock64();  // 100 MHz
     while (__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - v > 0x7FFFFFFFu) {  // sig < v (mod 2^32)
-        if (wall_clock64() - t0 > 200000000ull || __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            __hip_atomic_store(timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // keep the raiser's code
+        if (wall_clock64() - t0 > bound_ticks) {
+            uint32_t zero = 0;  // 2 = a hop timed out, unless something else was first
+            __hip_atomic_compare_exchange_strong(timeout, &zero, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1160,7 +1189,7 @@ void stream_hop(srg_ctx& c, int i, hipStream_t from, hipStream_t to, hipEvent_t 
     if (c.hop_values && c.sig[i] && c.fw_timeout) {
         const uint32_t v = ++c.sig_val[i];
         k_hop_set<<<1, 64, 0, from>>>(c.sig[i], v);
-        k_hop_wait<<<1, 64, 0, to>>>(c.sig[i], v, c.fw_timeout);
+        k_hop_wait<<<1, 64, 0, to>>>(c.sig[i], v, c.fw_timeout, c.hop_bound_ticks);
         HIP_CHECK(hipGetLastError());
         return;
     }
@@ -1430,7 +1459,6 @@ struct SymFw {
     hipStream_t st;
     int nb, G, g, split = 1, ntile = 0, prio = kChainPrio;
     bool multi = false, prof = false, keep_lines = false;
-    bool value_hops = true;  // false: the chain's stream hops are event waits (FwOverlap)
     LineMap lm{1, 1};
     size_t lds_bulk = 0;
     uint32_t* cflags = nullptr;
@@ -1477,7 +1505,7 @@ struct SymFw {
         {
             const char* hv = std::getenv("SRG_STREAM_HOPS");
             std::lock_guard<std::mutex> lk(g_dev_mu);
-            c.hop_values = value_hops && g_dev_ctx[c.device] == 1 && !(hv && std::strcmp(hv, "events") == 0);
+            c.hop_values = g_dev_ctx[c.device] == 1 && !(hv && std::strcmp(hv, "events") == 0);
         }
         lds_bulk = lb_lds<K, T, KCS>();
         set_lds(fw_bulk_lb<K, T, KCS>, lds_bulk);
@@ -1521,14 +1549,37 @@ struct SymFw {
             HIP_CHECK(hipStreamSynchronize(st));  // zeroed words before any peer may raise one
             plb.assign(G, nullptr);
             pfl.assign(G, nullptr);
-            c.comm->share_ptrs(lbuf[0], myflags, plb.data(), pfl.data(), &sys);
-            if (++c.xepoch == 0) ++c.xepoch;
+            // the flag value of this build: every rank proposes its next one and all take the largest,
+            // so a rank that skipped or repeated a build cannot leave the others waiting for a stale
+            // value
+            uint32_t ep = c.xepoch + 1 ? c.xepoch + 1 : 1;
+            c.comm->share_ptrs(lbuf[0], myflags, plb.data(), pfl.data(), &sys, &ep);
+            c.xepoch = ep;
         }
         // closure barrier words: 16 per pivot (arrival counter, changed flag per step), then the
         // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
         cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
         c.fw_timeout = cflags + (size_t)nb * 16;
+        if (c.test_fault == 2) {
+            // TEST HOOK: the state of a recycled allocation -- nonzero sync words, zero line buffers --
+            // in place before this build's reset (the value-hop race of rounds 3-4, stream_hop)
+            HIP_CHECK(hipMemsetAsync(cflags, 0xA5, ((size_t)nb * 16 + 4) * 4, c.aux_stream));
+            if (keep_lines) HIP_CHECK(hipMemsetAsync(lball, 0, (size_t)nb * nb * TT * sizeof(K), c.aux_stream));
+            HIP_CHECK(hipStreamSynchronize(c.aux_stream));
+        }
         HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
+        // the chain stream's kernels (hop waits, closures, the exchange) read and count in these
+        // words: the chain stream waits for their reset by an EVENT (a value hop's wait kernel would
+        // read the very word being reset; see stream_hop)
+        HIP_CHECK(hipEventRecord(c.ev_fwreset, st));
+        HIP_CHECK(hipStreamWaitEvent(c.aux_stream, c.ev_fwreset, 0));
+        // a value hop's wait bound: 2 s, or 20 x an estimate of the longest legitimate wait (one
+        // bulk launch of this rank at ~30 T relaxations/s) when that is longer
+        {
+            const double relax = (double)nb * (nb + 1) / 2 / G * (double)T * T * T;
+            const double ticks = 20.0 * relax / 30e12 * 1e8;
+            c.hop_bound_ticks = std::max<unsigned long long>(200000000ull, (unsigned long long)std::min(ticks, 1e12));
+        }
         sym_tiles(c, pl, st, own_h, slot_h, first);
         ntile = (int)own_h.size();
         tiles = (const int*)c.b_tiles.p;
@@ -1666,171 +1717,6 @@ void fw_sym_finish(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, 
     ms_xchg += ms_since(t0x);
 }
 
-// The symmetric FW as one fused launch per pivot (fw_step.hip.h): pivot kb's bulk and the chain of
-// k1 = kb + 1 (line w.r.t. kb, exchange, closure, line w.r.t. k1) in one launch on `st`, so the
-// per-pivot critical path has no cross-stream hop and no separate collective: peers exchange their
-// line segments inside the launch (xmode 2: stores into every peer's line buffer + arrival flags;
-// xmode 1: a simulated rank waits the modelled link time; 0: one rank).
-template <class K, int T, int SB, int SL>
-void launch_step(const StepArgs<K>& a, int grid, hipStream_t st) {
-    constexpr size_t lds = step_lds<K, T, SB, SL>();
-    static bool attr = false;
-    if (!attr) {
-        set_lds(fw_step<K, T, SB, SL>, lds);
-        attr = true;
-    }
-    fw_step<K, T, SB, SL><<<grid, 256, lds, st>>>(a);
-}
-
-template <class K, int T>
-void fw_line_fused(srg_ctx& c, const Plan& pl, K* D, size_t Vp, hipStream_t st, uint64_t& prof_relax, int& prof_n,
-                   double& ms_xchg, int xmode) {
-    const int nb = pl.nb, G = pl.G, g = pl.g;
-    constexpr size_t TT = (size_t)T * T;
-    const LineMap lm{nb, G};
-    const size_t lbb = (size_t)nb * TT * sizeof(K);
-    K* xlb = (K*)c.b_xlb.get(3 * lbb);
-    K* LB[3] = {xlb, xlb + (size_t)nb * TT, xlb + 2 * (size_t)nb * TT};
-    // sync words: 16 per pivot (fw_step StepSync; pivot 0's closure uses words 0..8), then the
-    // timeout word
-    uint32_t* cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
-    c.fw_timeout = cflags + (size_t)nb * 16;
-    HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
-    std::vector<int> own_h, slot_h, first;
-    sym_tiles(c, pl, st, own_h, slot_h, first);
-    const int ntile = (int)own_h.size();
-    const int* tiles = (const int*)c.b_tiles.p;
-    // device-side exchange: every rank's line-buffer block and arrival words (re-shared per build:
-    // a host rendezvous of the group; buffers may have moved)
-    std::vector<void*> plb(G, nullptr);
-    std::vector<uint32_t*> pfl(G, nullptr);
-    bool sys = false;
-    uint32_t* myflags = nullptr;
-    if (xmode == 2) {
-        const size_t fb = (size_t)nb * G * 4;
-        if (c.b_xflags.bytes < fb) {
-            myflags = (uint32_t*)c.b_xflags.get(fb);
-            HIP_CHECK(hipMemsetAsync(myflags, 0, fb, st));
-        }
-        myflags = (uint32_t*)c.b_xflags.p;
-        HIP_CHECK(hipStreamSynchronize(st));  // zeroed flags before any peer may raise one
-        c.comm->share_ptrs(xlb, myflags, plb.data(), pfl.data(), &sys);
-        ++c.xepoch;
-        if (c.xepoch == 0) ++c.xepoch;
-    }
-    // line 0: every rank holds the same initial D (no exchange)
-    const int bulk_tiles = nb * (nb + 1) / 2 / G;
-    int SL = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
-    int SB = bulk_tiles >= 768 ? 1 : 2;
-    if (const char* e = std::getenv("SRG_FW_SB")) SB = std::atoi(e) == 2 ? 2 : 1;  // experiments
-    // quadrant lines at least: a whole-tile line core beside the bulk's in one kernel spilled 110
-    // VGPRs (the 168-VGPR budget of three waves per SIMD)
-    if (SL == 1) SL = 2;
-    k_pack_line<K, T><<<nb, 256, 0, st>>>(D, Vp, LB[0], 0, lm);
-    fw_close_sq<K, T><<<dim3(T / 16, T / 16), 256, 0, st>>>(LB[0] + (size_t)lm.slot(0, 0) * TT, cflags, c.fw_timeout,
-                                                           kChainPrio);
-    set_lds(fw_line_lb<K, T, 1>, lb_lds<K, T, line_kc<1>()>());
-    fw_line_lb<K, T, 1><<<dim3(nb, 1), 256, lb_lds<K, T, line_kc<1>()>(), st>>>(D, Vp, LB[0], 0, LB[0], 0, 1, lm, g,
-                                                                              kChainPrio);
-    HIP_CHECK(hipGetLastError());
-    constexpr int NC = (T / 16) * (T / 16);
-    const int CH = std::max(NC, std::min(256, nb * SL * SL));
-    const bool prof = c.profiling && nb > 2;
-    if (prof) {
-        while (c.prof_events.size() < (size_t)2 * nb) {
-            hipEvent_t e;
-            HIP_CHECK(hipEventCreate(&e));
-            c.prof_events.push_back(e);
-        }
-    }
-    // SRG_FW_TRACE=1: per-launch wall-clock stamps of the chain phases (fw_step TraceAt), printed to
-    // stderr after FW (a diagnostic, tools/README.md)
-    unsigned long long* trace = nullptr;
-    if (std::getenv("SRG_FW_TRACE")) {
-        trace = (unsigned long long*)c.b_scantmp.get((size_t)nb * 8 * 8);
-        std::vector<unsigned long long> init((size_t)nb * 8, 0);
-        for (int k = 0; k < nb; ++k) init[(size_t)k * 8 + TR_START] = ~0ull;
-        HIP_CHECK(hipMemcpyAsync(trace, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
-    }
-    for (int kb = 0; kb < nb; ++kb) {
-        const int k1 = kb + 1 < nb ? kb + 1 : -1;
-        StepArgs<K> a{};
-        a.trace = trace ? trace + (size_t)kb * 8 : nullptr;
-        a.D = D;
-        a.ld = Vp;
-        a.lbk = LB[kb % 3];
-        a.lbn = k1 >= 0 ? LB[k1 % 3] : nullptr;
-        a.kb = kb;
-        a.k1 = k1;
-        a.lm = lm;
-        a.g = g;
-        a.tiles = tiles;
-        a.ntile = ntile;
-        a.CH = k1 >= 0 ? CH : 0;
-        a.sync = cflags + (size_t)16 * (k1 >= 0 ? k1 : 0);
-        a.timeout = c.fw_timeout;
-        a.xmode = G > 1 ? xmode : 0;
-        a.sys = sys ? 1 : 0;
-        a.epoch = c.xepoch;
-        a.myflags = myflags;
-        if (xmode == 1 && k1 >= 0) {
-            size_t mx = 0;  // the largest segment a peer sends this rank
-            for (int r = 0; r < G; ++r)
-                if (r != g) mx = std::max(mx, (size_t)lm.count(r, k1) * TT * sizeof(K));
-            a.model_ns = (uint32_t)c.comm->model_xchg_ns(mx);
-        }
-        if (xmode == 2 && k1 >= 0)
-            for (int r = 0; r < G && r < kMaxPeers; ++r)
-                if (r != g) {
-                    a.peer_lbn[r] = (K*)plb[r] + (size_t)(k1 % 3) * nb * TT;
-                    a.peer_flags[r] = pfl[r];
-                }
-        const int grid = a.CH + ntile * SB * SB;
-        const bool timed = prof && ntile > 0 && k1 >= 0;
-        if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n], st));
-        if (grid > 0) {
-            if (SB == 1 && SL == 2) launch_step<K, T, 1, 2>(a, grid, st);
-            else if (SB == 1) launch_step<K, T, 1, 4>(a, grid, st);
-            else if (SL == 2) launch_step<K, T, 2, 2>(a, grid, st);
-            else launch_step<K, T, 2, 4>(a, grid, st);
-        }
-        HIP_CHECK(hipGetLastError());
-        if (timed) {
-            int64_t m = 0;  // bulk relaxations of this launch: own tiles off lines kb and k1
-            for (int t : own_h) {
-                int I, J;
-                tri_tile_h(nb, t, I, J);
-                if (I != kb && I != k1 && J != kb && J != k1) ++m;
-            }
-            HIP_CHECK(hipEventRecord(c.prof_events[2 * prof_n + 1], st));
-            prof_relax += (uint64_t)m * T * T * T;
-            ++prof_n;
-        }
-    }
-    if (trace) {
-        std::vector<unsigned long long> t((size_t)nb * 8);
-        HIP_CHECK(hipMemcpyAsync(t.data(), trace, t.size() * 8, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        double sum[6] = {0, 0, 0, 0, 0, 0}, gap = 0;
-        int cnt = 0;
-        for (int k = 0; k + 1 < nb; ++k) {
-            const unsigned long long* r = &t[(size_t)k * 8];
-            const double us[6] = {0, (r[1] - r[0]) * 0.01, (r[2] - r[0]) * 0.01, (r[3] - r[0]) * 0.01,
-                                  (r[4] - r[0]) * 0.01, (r[5] > r[0] ? r[5] - r[0] : 0) * 0.01};
-            const double g2 = k + 2 < nb ? (t[(size_t)(k + 1) * 8] - std::max(r[4], r[5])) * 0.01 : 0;
-            std::fprintf(stderr, "fw_step %d: arrived %.1f go %.1f cdone %.1f chain_end %.1f bulk_end %.1f gap %.1f us\n", k,
-                         us[1], us[2], us[3], us[4], us[5], g2);
-            for (int q = 1; q < 6; ++q) sum[q] += us[q];
-            gap += g2;
-            ++cnt;
-        }
-        if (cnt)
-            std::fprintf(stderr, "fw_step mean (G=%d SB=%d SL=%d CH=%d): arrived %.1f go %.1f cdone %.1f chain_end %.1f bulk_end %.1f gap %.1f us\n",
-                         G, SB, SL, CH, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt, gap / cnt);
-    }
-    fw_sym_finish<K, T>(c, pl, D, Vp, st, own_h, slot_h, first, ms_xchg);
-}
-
 // General FW, several ranks: every rank ends with the whole D (row blocks all-gathered)
 template <class K>
 void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t st, double& ms_xchg) {
@@ -1851,33 +1737,18 @@ void gather_rows(srg_ctx& c, const Plan& pl, K* D, size_t Vp, int T, hipStream_t
     ms_xchg += ms_since(t0x);
 }
 
-// Which symmetric FW schedule runs: -1 = the two-stream schedule (fw_line_sym), else the fused
-// launch per pivot with that exchange mode (fw_line_fused): 0 one rank, 1 simulated rank, 2 peers.
-// Fused only on request (SRG_OPT_FW_STEP = 1, or SRG_FW_FUSED=1 in the environment under auto): it
-// measured slower than the two-stream schedule at every rank count (sim 8:0 FW 9.1-11.0 vs 6.6 ms,
-// one rank C3 26.2 vs 22.2 ms): the resident bulk workgroups starve the chain's phases.
-int fw_step_mode(const srg_ctx& c) {
-    const bool multi = c.comm && c.comm->nranks > 1;
-    const char* e = std::getenv("SRG_FW_FUSED");
-    const bool env = e && std::strcmp(e, "1") == 0;
-    if (!(c.fw_step == 1 || (c.fw_step == -1 && env))) return -1;
-    if (!multi) return 0;
-    if (c.comm->nranks > kMaxPeers) return -1;
-    const int dx = c.comm->device_exchange();
-    return dx == 1 ? 1 : dx == 2 ? 2 : -1;
-}
-
-// The two-stream chain's exchange of LB(k1): 0 = the communicator's allgather on the chain's stream,
-// 1 = a simulated rank's modelled device-side exchange, 2 = stores into the peers' line buffers +
-// arrival words (k_line_xchg).  Auto (SRG_OPT_FW_STEP = -1): device-side for simulated ranks and for
-// in-process ranks on distinct devices; 2 forces it (ranks sharing a GPU: each rank's chain stream
-// needs a hardware queue of its own); 0 keeps the collective.
+// The chain's exchange of LB(k1) (xchg.hip.h): 0 = the communicator's allgather on the chain's
+// stream, 1 = a simulated rank's modelled device-side exchange, 2 = stores into the peers' line
+// buffers + arrival words (k_line_xchg).  Auto (SRG_OPT_FW_STEP = -1): the modelled exchange for
+// simulated ranks, else the collective; 2 asks for the stores between in-process ranks.  The stores
+// stay opt-in until they have run between distinct devices (only ranks sharing one GPU
+// have exercised them; such ranks then need a hardware queue each for their chain streams).
 int chain_xmode(const srg_ctx& c) {
     const bool multi = c.comm && c.comm->nranks > 1;
     if (!multi || c.fw_step == 0 || c.comm->nranks > kMaxPeers) return 0;
     const int dx = c.comm->device_exchange();
     if (dx == 1) return 1;
-    if (dx == 2 && (c.fw_step == 2 || c.comm->distinct_devices())) return 2;
+    if (dx == 2 && c.fw_step == 2) return 2;
     return 0;
 }
 
@@ -1999,11 +1870,6 @@ struct FwOverlap {
         HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, hs));
         fw.reset(new SymFw<uint32_t, T>(cc, pl, D, Vp, st));
         fw->keep_lines = true;
-        // event waits for the chain's hops here: with the value hops (k_hop_set / k_hop_wait) a bulk
-        // launch of this schedule read a line buffer before its chain had written it -- an all-zero
-        // table in 5 of 6 runs of tests/test_fw_step.py's atlas case after test_events.py and
-        // test_fw_overlap.py in one process, none with event waits (SRG_STREAM_HOPS=events: 3 of 3)
-        fw->value_hops = false;
         on = true;
         ok = true;
         dbg = std::getenv("SRG_DEBUG_OVERLAP") != nullptr;
@@ -2196,11 +2062,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         prof_relax = ov->prof_relax;
         prof_n = ov->prof_n;
     } else if (sym_fw_for<K, T>(c, g)) {
-        if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64)) {
-            const int xm = fw_step_mode(c);
-            if (xm >= 0) fw_line_fused<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx, xm);
-            else fw_line_sym<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx);
-        }
+        if constexpr ((sizeof(K) == 4 && T == 128) || (sizeof(K) == 8 && T == 64))
+            fw_line_sym<K, T>(c, pl, D, Vp, st, prof_relax, prof_n, ms_dx);
     } else {
         // u32 keys: the pair-packed tile (two relaxations per 64-bit add + v_min3); the add + min3
         // tile (PK = 0) ran the same C3 launch in 0.304 instead of 0.242 ms (profiles/r02c/fw_fold.txt)
@@ -2214,8 +2077,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     const double ms_fw = tm.lap();
     if (sym_fw_for<K, T>(c, g) && rb_get<uint32_t>(c, MS_TIMEOUT))
         fail(SRG_ERR_HIP, rb_get<uint32_t>(c, MS_TIMEOUT) == 2
-                              ? "FW chain: a cross-stream hop waited more than 2 s (mis-ordered enqueue)"
+                              ? "FW chain: a cross-stream hop waited past its bound (mis-ordered enqueue)"
                               : "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
+    if (c.test_fault == 1)  // TEST HOOK (SRG_OPT_TEST_FAULT): a lost synchronisation's result, for the guard
+        HIP_CHECK(hipMemsetAsync(D, 0, VV * sizeof(K), st));
     if (wl_late) {
         // WL = min loss among the min-latency parallel edges (what k_w_split gives), from the
         // losses that crossed PCIe during FW.  Built here, after FW, rather than beside it: on a
@@ -2289,7 +2154,13 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
 
     // u32 certification: no saturated key in any used row (every rank must agree)
     HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
-    if (nloc) k_certify<K><<<nloc, kThreads, 0, st>>>(D, Vp, lnodes, nloc, nodes, n, P.flags);
+    HIP_CHECK(hipMemsetAsync(&P.flags->impossible, 0, 4, st));
+    if (nloc)
+        k_certify<K><<<nloc, kThreads, 0, st>>>(D, Vp, lnodes, nloc, nodes, n, (K)min_edge_key(P.es.min_lat_inv, P.unit),
+                                                P.flags);
+    if (reduce_flag(&P.flags->impossible))
+        fail(SRG_ERR_INTERNAL, "FW produced an impossible table: a used pair's latency is below the smallest edge "
+                               "latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
     const uint32_t inf_any = reduce_flag(&P.flags->inf_in_used_row);
     if (sizeof(K) == 4 && inf_any) {
         // a used pair at INF: unreachable -- unless some path could reach 2^31-1 ns, in which case
@@ -2753,7 +2624,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
                      selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, gb, c.kout_key, c.kout_diag,
-                     in_w64};
+                     in_w64, min_edge_key(P.es.min_lat_inv, P.unit)};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
@@ -2772,11 +2643,14 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     // every rank agrees on the outcome before any exchange
     if (multi) {
         c.comm->allreduce_max_u32(fl, 2, st);
-        c.comm->allreduce_max_u32(fl + 5, 1, st);
+        c.comm->allreduce_max_u32(fl + 5, 2, st);
     }
     uint32_t hfl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_CHECK(hipMemcpyAsync(hfl, fl, 32, hipMemcpyDeviceToHost, st));
     const double ms_sssp = tm.lap();
+    if (hfl[6])
+        fail(SRG_ERR_INTERNAL, "the sparse build produced an impossible table: a used pair's latency is below the "
+                               "smallest edge latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
     if (std::getenv("SRG_DEBUG_SPARSE")) {
         const unsigned long long ev = (unsigned long long)hfl[2] | (unsigned long long)hfl[3] << 32;
         std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu\n", nbatch, grid,
@@ -3451,7 +3325,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             DevGraph probe{g->num_vertices, (int)g->directed, E};
             const bool ov_want = c->fw_overlap && !direct && nr == 1 && want_late && c->h2d_codec && E >= ((size_t)1 << 20) &&
                                  !g->directed && c->fw_symmetric && (c->fw_tile == 0 || c->fw_tile == 128) &&
-                                 g->num_vertices >= 256 && n > 0 && !choose_sparse(*c, probe) && fw_step_mode(*c) < 0;
+                                 g->num_vertices >= 256 && n > 0 && !choose_sparse(*c, probe);
             if (ov_want) {
                 HIP_CHECK(hipStreamSynchronize(c->aux_stream));  // nothing of an aborted call still runs
                 ov.init(*c, g->num_vertices, std::vector<uint32_t>(nodes, nodes + n));
@@ -3770,7 +3644,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
         // serialise the W build and FW behind the loss DMAs (measured: build 1.0 -> 3.6 ms)
         c->loss_stream = c->d2h_stream;
-        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate})
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate, &c->ev_fwreset})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         int wv = 0;
         if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv) {
@@ -3864,12 +3738,17 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_line_split = (int)value;
             return SRG_OK;
         case SRG_OPT_FW_STEP:
-            if (value != 0 && value != 1 && value != 2 && value != -1) return SRG_ERR_ARG;
+            // (1, the fused one-launch-per-pivot FW, was removed in round 5: DESIGN.md §7)
+            if (value != 0 && value != 2 && value != -1) return SRG_ERR_ARG;
             ctx->fw_step = (int)value;
             return SRG_OK;
         case SRG_OPT_FW_OVERLAP:
             if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->fw_overlap = (int)value;
+            return SRG_OK;
+        case SRG_OPT_TEST_FAULT:
+            if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
+            ctx->test_fault = (int)value;
             return SRG_OK;
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
@@ -3902,6 +3781,7 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_FW_LINE_SPLIT: *value = ctx->fw_line_split; break;
         case SRG_OPT_FW_STEP: *value = ctx->fw_step; break;
         case SRG_OPT_FW_OVERLAP: *value = ctx->fw_overlap; break;
+        case SRG_OPT_TEST_FAULT: *value = ctx->test_fault; break;
         default: return SRG_ERR_ARG;
     }
     return SRG_OK;

@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include "kernels.hip.h"
+#include "guards.h"
 
 namespace srg {
 
@@ -193,6 +194,8 @@ struct SparseArgs {
     uint32_t* out_key;           // RoutingInfo key table (null: ns latencies into out_lat), diagonal 0xFFFFFFFF
     uint64_t* out_diag;          // with out_key: the raw self-loop latency per output row
     const uint64_t* in_w64;      // wide labels: u64 arc keys (`slots` then holds 16-byte labels)
+    uint64_t min_key;            // smallest arc key: a used off-diagonal latency below it is impossible
+                                 // (guards.h) -> flags[6]
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some dropped lane's new latency is
@@ -515,7 +518,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
         // ---- output rows: 64 targets x 64 sources tiles transposed through LDS ----
         // narrow labels: one pass (the tile holds the packed label); wide: pass 0 the latencies,
         // pass 1 the loss bits
-        uint32_t bad = 0;
+        uint32_t bad = 0, imp = 0;
         for (uint32_t j0 = 0; j0 < a.ncols; j0 += 64) {
             for (int pass = 0; pass < (LB::wide ? 2 : 1); ++pass) {
                 for (uint32_t i = wave; i < 64; i += SP_WAVES) {
@@ -546,6 +549,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
                         } else {
                             const uint64_t lat = LB::wide ? l : l >> 32;
                             bad |= lat == LB::LAT_MAX;
+                            imp |= impossible_key<uint64_t>(lat, a.min_key, false);
                             ol = lat * a.unit;
                         }
                         if (a.out_key) {  // narrow only (the host never asks wide labels for keys)
@@ -562,6 +566,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
             }
         }
         if (bad) atomicOr(&a.flags[0], 1u);
+        if (imp) atomicOr(&a.flags[6], 1u);
     }
     if (threadIdx.x == 0) atomicMax(&a.flags[1], max_sweeps);
     if (__ballot(saturated) && lane == 0) atomicOr(&a.flags[5], 1u);

@@ -1,10 +1,9 @@
-"""Child process of tests/test_fw_step.py: G in-process ranks on device 0 running the symmetric FW with
-the DEVICE-SIDE line exchange: the fused step (SRG_OPT_FW_STEP = 1: each rank stores its line segments
-into its peers' line buffers and raises arrival flags inside the launch) and the two-stream chain's
-k_line_xchg (SRG_OPT_FW_STEP = 2: the same stores and flags in a launch on the chain's stream).  Ranks sharing a GPU need a hardware
-queue each for that (one rank's in-kernel wait must not sit in front of a peer's launch), so the
-parent starts this script with GPU_MAX_HW_QUEUES = 16.  Prints one JSON line: per case, whether every
-rank matched the single-GPU two-stream build and the oracle bit for bit."""
+"""Child process of tests/test_fw_exchange.py: G in-process ranks on device 0 running the symmetric FW
+with the DEVICE-SIDE line exchange (SRG_OPT_FW_STEP = 2: the chain's k_line_xchg stores each rank's
+line segments into its peers' line buffers and raises arrival words, xchg.hip.h).  Ranks sharing a GPU
+need a hardware queue each for that (one rank's in-kernel wait must not sit in front of a peer's
+launch), so the parent starts this script with GPU_MAX_HW_QUEUES = 16.  Prints one JSON line: per
+case, whether every rank matched the single-GPU build and the oracle bit for bit."""
 import json
 import os
 import sys
@@ -25,7 +24,7 @@ def bits_equal(a, b):
     return np.array_equal(np.asarray(a, dtype=np.float32).view(np.uint32), np.asarray(b, dtype=np.float32).view(np.uint32))
 
 
-def run(G, e, nodes, split, step=1):
+def run(G, e, nodes, split, step=2):
     group = LocalGroup(G)
     routers = [Router(0) for _ in range(G)]
     for r, rt in enumerate(routers):
@@ -55,18 +54,11 @@ def run(G, e, nodes, split, step=1):
 def main():
     cases = [
         dict(G=2, V=700, seed=11, split=0),
-        dict(G=3, V=900, seed=12, split=2),
+        dict(G=3, V=900, seed=17, split=2),
+        dict(G=4, V=1500, seed=18, split=0),
         dict(G=4, V=1100, seed=13, split=4),
-        dict(G=2, V=400, seed=14, split=0, u64=True),
-        dict(G=2, V=900, seed=15, split=2, env={"SRG_FW_SB": "1"}),
-        # the two-stream chain with the device-side exchange (k_line_xchg), forced on one GPU
-        dict(G=3, V=900, seed=17, split=2, step=2),
-        dict(G=4, V=1500, seed=18, split=0, step=2),
-        dict(G=2, V=400, seed=19, split=0, u64=True, step=2),
+        dict(G=2, V=400, seed=19, split=0, u64=True),
     ]
-    if len(sys.argv) > 1 and sys.argv[1] == "diag":
-        cases = [dict(G=2, V=900, seed=12, split=2), dict(G=3, V=1000, seed=15, split=2),
-                 dict(G=2, V=900, seed=12, split=2, env={"SRG_FW_SB": "1"}), dict(G=5, V=1300, seed=16, split=0)]
     res = []
     for c in cases:
         kw = dict(lat_lo=2 ** 31, lat_hi=2 ** 33) if c.get("u64") else {}
@@ -77,11 +69,7 @@ def main():
         t0 = ref.compute_shortest_paths(e, nodes)
         ref.close()
         lat, loss = oracle.compute_shortest_paths(e.as_tuple(), nodes)
-        for k, v in c.get("env", {}).items():
-            os.environ[k] = v
-        out, errs = run(c["G"], e, nodes, c["split"], c.get("step", 1))
-        for k in c.get("env", {}):
-            del os.environ[k]
+        out, errs = run(c["G"], e, nodes, c["split"])
         ok = all(x is None for x in errs) and all(
             np.array_equal(t.latency_ns, t0.latency_ns) and bits_equal(t.packet_loss, t0.packet_loss)
             and np.array_equal(t.latency_ns, lat) and bits_equal(t.packet_loss, loss) for t in out if t is not None)
