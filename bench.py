@@ -563,8 +563,8 @@ def main():
     ap.add_argument("--fw-line-split", type=int, default=None,
                     help="symmetric FW: sub-tiles per dimension of the chain's line launches (1/2/4; 0 = auto)")
     ap.add_argument("--fw-step", type=int, default=None,
-                    help="symmetric FW: 1 = one fused launch per pivot (chain + bulk, in-launch line exchange), "
-                         "0 = two-stream schedule, -1 = auto")
+                    help="symmetric FW line exchange between ranks: 2 = device-side stores (in-process ranks), "
+                         "0 = the collective, -1 = auto")
     ap.add_argument("--fw-overlap", type=int, default=None,
                     help="host entry, one rank: 1 = FW starts while the edge list arrives (default), 0 = after it")
     ap.add_argument("--no-locality", action="store_true", help="sparse: batch sources in node order")

@@ -106,6 +106,10 @@ typedef struct srg_stats {
     uint64_t latency_unit_ns;   /* shortest paths: the gcd of the non-self-loop edge latencies; the
                                    kernels count latency in these units (exact: every path sum is a
                                    multiple), outputs are back in ns.  1 = nanosecond keys        */
+    int32_t fw_overlap_pivots;  /* host entry: FW pivots enqueued while the edge list was still crossing
+                                   PCIe (SRG_OPT_FW_OVERLAP; 0 = none)                              */
+    int32_t fw_overlap_kept;    /* host entry: 1 = the FW that ran beside the H2D produced the table
+                                   (its certification passed), 0 = the build ran FW after the H2D   */
 } srg_stats;
 
 #define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */
@@ -209,7 +213,8 @@ int srg_compute_shortest_paths(srg_ctx* ctx, const srg_edge_list* graph,
 /* Same computation with every array already resident in device memory (HBM):
  * graph->src/dst/latency_ns/packet_loss/node_ids, nodes and out_* are device pointers;
  * `hip_stream` is a hipStream_t (NULL = default stream).  Returns after the stream work
- * is complete.  This is the entry the benchmark times (inputs resident in HBM).        */
+ * is complete.  (The benchmark's headline times the HOST entry above, as Shadow calls it;
+ * this entry is reported beside it as the inputs-resident-in-HBM figure.)              */
 int srg_compute_shortest_paths_device(srg_ctx* ctx, const srg_edge_list* graph_dev,
                                       const uint32_t* nodes_dev, uint32_t num_nodes,
                                       uint64_t* out_latency_ns_dev, float* out_packet_loss_dev,
@@ -283,10 +288,13 @@ uint32_t srg_graph_parse_chunks(const srg_graph* g);
 
 /* ---- multi-GPU: one process (or thread) per GPU, SPMD -------------------------------
  * After srg_comm_init*, every rank calls srg_compute_shortest_paths[_device] with the SAME
- * graph and nodes.  FW row blocks are split across ranks with a per-pivot-block broadcast of
- * the pivot row panel; each rank routes the used sources whose rows it owns; output rows are
- * exchanged point to point (SRG_OPT_GATHER_OUTPUT).  The reference has no multi-process path
- * (rayon threads only, mod.rs:190-208): this is new, MI355X-side design.    */
+ * graph and nodes.  Undirected graphs: the symmetric FW's stored tiles (I, J), I <= J, are dealt
+ * to rank (I + J) mod G and each pivot's line buffer (the pivot's row panel = its column panel)
+ * is exchanged once per pivot (allgather; SRG_OPT_FW_STEP = 2: device-side stores); directed
+ * graphs: row blocks with a per-pivot broadcast of the row panel.  Each rank routes the used
+ * sources at positions [n r / G, n (r+1) / G) of `nodes`; output rows are exchanged
+ * (SRG_OPT_GATHER_OUTPUT).  The reference has no multi-process path (rayon threads only,
+ * mod.rs:190-208): this is new, MI355X-side design.                         */
 #define SRG_UNIQUE_ID_BYTES 128
 /* RCCL (over xGMI): rank 0 creates the id, the caller shares it (e.g. torch.distributed). */
 int srg_comm_unique_id(unsigned char id[SRG_UNIQUE_ID_BYTES], char* errbuf, size_t errlen);

@@ -132,6 +132,8 @@ class Stats(ctypes.Structure):
         ("d2h_overlapped_bytes", ctypes.c_uint64),
         ("min_latency_ns", ctypes.c_uint64),
         ("latency_unit_ns", ctypes.c_uint64),
+        ("fw_overlap_pivots", ctypes.c_int32),
+        ("fw_overlap_kept", ctypes.c_int32),
     ]
 
     def as_dict(self):

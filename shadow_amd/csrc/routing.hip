@@ -2725,7 +2725,8 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
     // sum; keys count units (a ms-granular graph fits u32 keys up to 2^31-1 ms of path), outputs
     // are key * unit -- exact.  SRG_LATENCY_UNIT=1 keeps nanosecond keys (tests, A/B).
     const char* lu = std::getenv("SRG_LATENCY_UNIT");
-    P.unit = (P.es.unit > 1 && !(lu && std::strcmp(lu, "1") == 0)) ? P.es.unit : 1;
+    const uint64_t unit = (P.es.unit > 1 && !(lu && std::strcmp(lu, "1") == 0)) ? P.es.unit : 1;
+    P.unit = unit;
     // the FW that ran beside the H2D counted nanoseconds (exact for any unit; its certification
     // decides as usual, a failure reruns on the u64 keys)
     const bool pre = ov && ov->on && ov->ok && ov->ended && P.es.max_lat < 0xFFFFFFFFull;
@@ -2747,8 +2748,18 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
         return;
     }
     if (pre) {
-        if (run_dense<uint32_t, FwOverlap::T>(c, g, ov->pl, nodes, n, out_lat, out_loss, st, P, stats, sink, ov)) return;
-    } else if (P.max_key < 0xFFFFFFFFull) {
+        if (run_dense<uint32_t, FwOverlap::T>(c, g, ov->pl, nodes, n, out_lat, out_loss, st, P, stats, sink, ov)) {
+            if (stats) stats->fw_overlap_kept = 1;
+            return;
+        }
+        // the overlapped FW counted nanoseconds and failed its certification: the latencies' gcd unit
+        // may still fit u32 keys -- the normal u32 build before the u64 one
+        P.unit = unit;
+        P.max_key = P.es.max_lat / P.unit;
+        if (stats) stats->latency_unit_ns = P.unit;
+        P.range_risk = (unsigned __int128)P.max_key * (g.V > 1 ? g.V - 1 : 1) >= ((unsigned __int128)1 << 62);
+    }
+    if ((!pre || P.unit > 1) && P.max_key < 0xFFFFFFFFull) {
         // FW tile: 128 (more work per launch) on one GPU; the multi-rank schedule is bound by
         // the per-pivot chain (close pivot -> panels), whose latency scales with T^3
         const int tile = c.fw_tile ? c.fw_tile : 128;
@@ -3343,6 +3354,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         if (ov.on) ov.finish();  // the FW thread has enqueued every landed chunk's work
         if (ov.on && !coded) ov.ok = false;
         const int ov_early = ov.next;  // pivots enqueued while chunks were still crossing
+        if (stats && ov.on && ov.ok) stats->fw_overlap_pivots = ov_early;
         if (ov.on && ov.ok && !ov.ended) ov.advance(ov.nb - 1);
         if (ov.on && std::getenv("SRG_DEBUG_OVERLAP")) {
             std::fprintf(stderr, "fw-overlap: ok=%d pivots_during_h2d=%d of %d\n", ov.ok ? 1 : 0, ov_early, ov.nb);

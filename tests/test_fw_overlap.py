@@ -125,6 +125,9 @@ def test_overlap_u32_range_rerun():
     t1 = build(e, nodes, 1)
     t0 = build(e, nodes, 0)
     assert same(t1, t0)
+    # after the failed nanosecond-key FW the build takes the u32 keys in units of the gcd,
+    # not the u64 keys
+    assert t1.stats["path_kind"] == N.SRG_PATH_DENSE_U32 and t1.stats["latency_unit_ns"] == t0.stats["latency_unit_ns"] > 1
 
 
 def _build_opts(e, nodes, opts):

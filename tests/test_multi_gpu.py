@@ -234,13 +234,64 @@ def test_rccl_single_rank():
 
 @pytest.fixture(scope="module")
 def c3_single():
-    """Config C3 (atlas_like(10000, seed=10000)) built by one rank: the reference table."""
+    """Config C3 (atlas_like(10000, seed=10000)) built by one rank through the host entry exactly as
+    the bench times it (edge list in host memory, FW beside the H2D, 1.2 GB table back): the
+    reference table of the multi-rank tests, pinned to the oracle by test_c3_host_entry_oracle_rows."""
     e = synth.atlas_like(10000, seed=10000)
     r = Router(0)
     t = r.compute_shortest_paths(e, list(range(10000)))
     r.close()
     assert t.stats["path_kind"] == N.SRG_PATH_DENSE_U32
     return e, t
+
+
+C3_ROWS = 512  # SURVEY §8(d): >= 512 seeded sources checked against the oracle at C3
+
+
+@pytest.fixture(scope="module")
+def c3_oracle_rows(c3_single):
+    e, _ = c3_single
+    rows = np.random.default_rng(10001).choice(10000, C3_ROWS, replace=False).tolist()
+    lat, loss = oracle.compute_shortest_paths(e.as_tuple(), list(range(10000)), rows=rows, mode=2, nthreads=16)
+    return rows, lat, loss
+
+
+@pytest.mark.slow
+def test_c3_host_entry_oracle_rows(c3_single, c3_oracle_rows):
+    """The headline path itself at full size: the host entry with the FW beside the
+    H2D -- what bench.py times and what Shadow's call site runs -- against C3_ROWS seeded oracle rows
+    (mode 2, pinned to the heap Dijkstra in test_oracle.py), bit-exact, plus whole-table properties."""
+    e, t = c3_single
+    assert t.stats["fw_overlap_kept"] == 1 and t.stats["fw_overlap_pivots"] > 0, t.stats
+    rows, lat, loss = c3_oracle_rows
+    assert np.array_equal(t.latency_ns[rows], lat)
+    assert bits_equal(t.packet_loss[rows], loss)
+    V = 10000
+    assert np.array_equal(np.diag(t.latency_ns), e.latency_ns[:V])
+    off = ~np.eye(V, dtype=bool)
+    assert np.array_equal(t.latency_ns[off], t.latency_ns.T[off])
+    assert int(t.latency_ns[off].min()) >= int(e.latency_ns[V:].min())
+
+
+@pytest.mark.slow
+def test_c3_routing_info_full_size(c3_single, c3_oracle_rows):
+    """Shadow's actual call at full C3 size: srg_routing_info_build (generate_routing_info +
+    RoutingInfo, sim_config.rs:425-462) keeps the build's certified u32 latency keys; its tables equal
+    the host-entry table everywhere and the oracle's rows, and path() / get_smallest_latency_ns()
+    agree with them."""
+    e, t = c3_single
+    V = 10000
+    ids = list(range(V))
+    ri = generate_routing_info(e, ids)
+    lt, ls, gid = ri.tables()
+    assert np.array_equal(lt, t.latency_ns) and bits_equal(ls, t.packet_loss)
+    rows, lat, loss = c3_oracle_rows
+    assert np.array_equal(lt[rows], lat) and bits_equal(ls[rows], loss)
+    rng = np.random.default_rng(3)
+    for s, d in rng.integers(0, V, size=(64, 2)):
+        p = ri.path(int(s), int(d))
+        assert p.latency_ns == int(t.latency_ns[s, d]) and np.float32(p.packet_loss) == t.packet_loss[s, d]
+    assert ri.get_smallest_latency_ns() == int(t.latency_ns.min())
 
 
 @pytest.mark.slow
