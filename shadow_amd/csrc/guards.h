@@ -19,7 +19,9 @@
 
 namespace srg {
 
-// d: a used pair's latency key; min_key: the smallest non-self-loop edge key; diagonal: the pair
+// d: a used pair's latency key; min_key: the smallest non-self-loop edge key, clamped by the caller
+// to the key type's INF (an edge of >= INF keys counts as absent, so INF itself stays legal: it is
+// the unreachable / out-of-range marker the other checks decide on); diagonal: the pair
 // is (s, s) (its output is the raw self-loop weight, mod.rs:211-217, not a path)
 template <class K>
 SRG_GUARD_HD inline bool impossible_key(K d, K min_key, bool diagonal) {

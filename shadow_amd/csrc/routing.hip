@@ -2156,8 +2156,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
     HIP_CHECK(hipMemsetAsync(&P.flags->impossible, 0, 4, st));
     if (nloc)
-        k_certify<K><<<nloc, kThreads, 0, st>>>(D, Vp, lnodes, nloc, nodes, n, (K)min_edge_key(P.es.min_lat_inv, P.unit),
-                                                P.flags);
+        k_certify<K><<<nloc, kThreads, 0, st>>>(
+            D, Vp, lnodes, nloc, nodes, n,
+            // (an edge of >= INF keys counts as absent: the bound is never above INF, which stays legal)
+            (K)std::min<uint64_t>(min_edge_key(P.es.min_lat_inv, P.unit), (uint64_t)KeyOps<K>::INF), P.flags);
     if (reduce_flag(&P.flags->impossible))
         fail(SRG_ERR_INTERNAL, "FW produced an impossible table: a used pair's latency is below the smallest edge "
                                "latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
