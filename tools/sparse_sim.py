@@ -58,7 +58,7 @@ def main():
         src.tofile(f)
         w.tofile(f)
     exe = "/tmp/ssim/sim"
-    subprocess.check_call(["g++", "-O3", "-march=native", "-o", exe, os.path.join(ROOT, "tools/sparse_sim.cpp")])
+    subprocess.check_call(["g++", "-O3", "-march=native", "-std=c++17", "-o", exe, os.path.join(ROOT, "tools/sparse_sim.cpp")])
     deg = np.diff(off)
     orders = {
         "identity": np.arange(V, dtype=np.uint32),
@@ -75,7 +75,7 @@ def main():
         o.tofile("/tmp/ssim/order.bin")
         for div in divs:
             r = subprocess.run([exe, "/tmp/ssim/csr.bin", "/tmp/ssim/order.bin", str(maxw // div), str(nb), "61", os.environ.get("PER_LANE", "0"),
-                                os.environ.get("GS_ACT", "0"), os.environ.get("LANES", "64")],
+                                os.environ.get("GS_ACT", "0"), os.environ.get("LANES", "64"), os.environ.get("HUBS", "0")],
                                capture_output=True, text=True)
             print(name, "delta=max/%d" % div, r.stdout.strip(), flush=True)
 
