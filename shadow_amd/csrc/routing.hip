@@ -41,7 +41,6 @@
 #include "tight_sparse.hip.h"
 #include "comm.h"
 #include "sparse.hip.h"
-#include "sparse_xcd.hip.h"
 #include "events.hip.h"
 #include "xchg.hip.h"
 
@@ -770,14 +769,13 @@ struct srg_ctx {
     int test_fault = 0;                 // TEST HOOK (SRG_OPT_TEST_FAULT): 1 = zero D after FW, 2 = stale FW sync words
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
-    DevBuf b_sxctl;                     // sparse XCD kernel: group blocks, batch queue, abort word
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
                           &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc, &b_odiag,
-                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered, &b_sxctl})
+                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
@@ -2546,14 +2544,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     c.own_row0 = p0;  // this rank's rows: positions [p0, p1) of `nodes`
     c.own_row1 = p1;
     const uint32_t nloc = p1 - p0;
-    // u32 labels: the XCD-cooperative kernel (sparse_xcd.hip.h; batches of SX_B sources, one per
-    // XCD, labels in that XCD's L2) when its LDS fits; the wide labels and graphs past that keep
-    // k_sparse_bf (64-source batches, one per workgroup).  SRG_SPARSE_KERNEL=bf forces the latter (A/B).
-    const uint32_t nwv = (V + 63) / 64;
-    const char* skenv = std::getenv("SRG_SPARSE_KERNEL");
-    const bool xcd = !wide && sx_lds_bytes<SX_B>(nwv) <= (size_t)160 * 1024 && !(skenv && std::strcmp(skenv, "bf") == 0);
-    const uint32_t BS = xcd ? (uint32_t)SX_B : 64u;
-    const uint32_t nbatch = (nloc + BS - 1) / BS;
+    const uint32_t nbatch = (nloc + 63) / 64;
     std::vector<uint32_t> h_off(V + 1), h_src(arcs);
     HIP_CHECK(hipMemcpyAsync(h_off.data(), off, ((size_t)V + 1) * 4, hipMemcpyDeviceToHost, st));
     if (arcs) HIP_CHECK(hipMemcpyAsync(h_src.data(), in_src, (size_t)arcs * 4, hipMemcpyDeviceToHost, st));
@@ -2592,7 +2583,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     if (c.sparse_locality)
         std::stable_sort(loc.begin(), loc.end(),
                          [&](uint32_t x, uint32_t y) { return order[P.nodes_h[x]] < order[P.nodes_h[y]]; });
-    std::vector<uint32_t> bsrc((size_t)std::max<uint32_t>(nbatch, 1) * BS), brow(bsrc.size());
+    std::vector<uint32_t> bsrc((size_t)std::max<uint32_t>(nbatch, 1) * 64), brow(bsrc.size());
     for (uint32_t i = 0; i < (uint32_t)bsrc.size(); ++i) {
         const bool real = i < nloc;
         bsrc[i] = P.nodes_h[real ? loc[i] : (nloc ? loc[0] : 0)];
@@ -2609,79 +2600,21 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
 
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
-    if (c.profiling) {
-        while (c.prof_events.size() < 2) {
-            hipEvent_t e;
-            HIP_CHECK(hipEventCreate(&e));
-            c.prof_events.push_back(e);
-        }
-    }
-    uint32_t hfl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t grid = 0;
-    if (nbatch && xcd) {
-        // one 1024-thread workgroup per CU; each finds its XCD's group at run time
-        grid = (uint32_t)dev_cus;
-        const size_t ctl_bytes = (size_t)SX_MAXG * sizeof(SxGroup) + 256;
-        unsigned char* ctl = (unsigned char*)c.b_sxctl.get(ctl_bytes);
-        HIP_CHECK(hipMemsetAsync(ctl, 0, ctl_bytes, st));
-        unsigned long long* lab = (unsigned long long*)c.b_D.get((size_t)SX_MAXG * V * SX_B * 8);
-        unsigned long long* sxb = (unsigned long long*)c.b_W.get((size_t)SX_MAXG * sx_bits_words(nwv) * 8);
-        SxArgs sa{};
-        sa.in_off = off;
-        sa.in_src = in_src;
-        sa.in_w = in_w;
-        sa.in_b = in_b;
-        sa.out_off = out_off;
-        sa.out_dst = out_dst;
-        sa.V = V;
-        sa.batch_src = d_bsrc;
-        sa.batch_row = d_brow;
-        sa.nbatch = nbatch;
-        sa.groups = reinterpret_cast<SxGroup*>(ctl);
-        sa.labels = lab;
-        sa.bits = sxb;
-        sa.queue = reinterpret_cast<uint32_t*>(ctl + (size_t)SX_MAXG * sizeof(SxGroup));
-        sa.abort = sa.queue + 1;
-        sa.cols = cols;
-        sa.ncols = n;
-        sa.self_lat = selflat;
-        sa.self_loss = selfloss;
-        sa.out_lat = out_lat;
-        sa.out_loss = out_loss;
-        sa.flags = fl;
-        sa.unit = P.unit;
-        sa.delta = c.sparse_delta_div > 0 ? std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div)
-                                          : ~0ull;
-        sa.out_key = c.kout_key;
-        sa.out_diag = c.kout_diag;
-        sa.min_key = min_edge_key(P.es.min_lat_inv, P.unit);
-        sa.reg_ticks = 2000;  // 20 us: every workgroup of the grid starts within ~1 us on an idle device
-        const size_t sx_lds = sx_lds_bytes<SX_B>(nwv);
-        set_lds(k_sparse_xcd<SX_B>, sx_lds);
-        if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[0], st));
-        k_sparse_xcd<SX_B><<<grid, SX_THREADS, sx_lds, st>>>(sa);
-        HIP_CHECK(hipGetLastError());
-        if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
-        uint32_t aborted = 0;
-        HIP_CHECK(hipMemcpyAsync(&aborted, sa.abort, 4, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        // a group's bounded wait gave up: every participant left (no hang), the table is incomplete
-        if (aborted) fail(SRG_ERR_INTERNAL, "sparse XCD kernel: a group wait timed out");
-    }
     // wide labels take the 128-VGPR budget: one workgroup per CU
     const int wpc = wide ? 1 : 2;
-    if (!xcd) grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)wpc));
+    uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)wpc));
 
     // label slots (V x 64 x 8 B per resident batch, 16 B when wide) within about half of the free HBM
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const size_t slot_bytes = (size_t)V * 64 * (wide ? 16 : 8);
     grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
+    const uint32_t nwv = (V + 63) / 64;
     const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
     // bitmaps in LDS while a CU still fits the requested workgroups, else in global memory
     const bool gbits = c.sparse_global_bitmaps || bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / wpc;
     const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
-    if (nbatch && !xcd) {
+    if (nbatch) {
         unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * slot_bytes);
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
@@ -2697,7 +2630,14 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
-        if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[0], st));
+        if (c.profiling) {
+            while (c.prof_events.size() < 2) {
+                hipEvent_t e;
+                HIP_CHECK(hipEventCreate(&e));
+                c.prof_events.push_back(e);
+            }
+            HIP_CHECK(hipEventRecord(c.prof_events[0], st));
+        }
         kern<<<grid, SP_THREADS, lds, st>>>(a);
         HIP_CHECK(hipGetLastError());
         if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
@@ -2707,24 +2647,16 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         c.comm->allreduce_max_u32(fl, 2, st);
         c.comm->allreduce_max_u32(fl + 5, 2, st);
     }
-    uint32_t hfl16[16] = {};
-    HIP_CHECK(hipMemcpyAsync(hfl16, fl, 64, hipMemcpyDeviceToHost, st));
+    uint32_t hfl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(hfl, fl, 32, hipMemcpyDeviceToHost, st));
     const double ms_sssp = tm.lap();
-    std::memcpy(hfl, hfl16, sizeof(hfl));
     if (hfl[6])
         fail(SRG_ERR_INTERNAL, "the sparse build produced an impossible table: a used pair's latency is below the "
                                "smallest edge latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
     if (std::getenv("SRG_DEBUG_SPARSE")) {
         const unsigned long long ev = (unsigned long long)hfl[2] | (unsigned long long)hfl[3] << 32;
-        std::fprintf(stderr, "sparse: %s kernel, %u batches of %u, grid %u, max sweeps %u, evaluations %llu, groups %u\n",
-                     xcd ? "xcd" : "bf", nbatch, BS, grid, hfl[1], ev, hfl[7]);
-        if (xcd) {
-            unsigned long long tw, tt;
-            std::memcpy(&tw, &hfl16[8], 8);
-            std::memcpy(&tt, &hfl16[10], 8);
-            std::fprintf(stderr, "sparse: xcd barrier wait %.1f%% of workgroup time, %u barriers per workgroup, %.2f us per barrier interval\n",
-                         tt ? 100.0 * tw / tt : 0.0, grid ? hfl16[12] / grid : 0, hfl16[12] ? tt / 100.0 / hfl16[12] : 0.0);
-        }
+        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu\n", nbatch, grid,
+                     hfl[1], ev);
     }
     if (hfl[0]) {
         // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
@@ -2760,8 +2692,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         stats->ms_exchange += ms_exchange;
         stats->path_kind = wide ? SRG_PATH_SPARSE_U64 : SRG_PATH_SPARSE_U32;
         stats->loss_rounds = (int)hfl[1];
-        // (k_sparse_bf counts list entries per wave, 64 lanes each; the XCD kernel counts lane relaxations)
-        stats->relaxations = (((uint64_t)hfl[3] << 32) | hfl[2]) * (xcd ? 1 : 64);
+        stats->relaxations = (((uint64_t)hfl[3] << 32) | hfl[2]) * 64;
         stats->nranks = G;
         stats->rank = rk;
         stats->local_sources = nloc;
