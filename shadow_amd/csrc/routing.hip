@@ -1014,6 +1014,82 @@ struct HostSink {
     std::string err;
     std::vector<hsa_signal_t> sigs;
     std::vector<hipEvent_t> evs;
+    // latency rows as the build's u32 keys (widen = true: host entry, dense u32 build, one rank):
+    // half the bytes of u64 ns over PCIe; a helper thread ships them through the context's pinned
+    // ring (3 slots) on the SDMA engine and the host pool widens each slot (key x unit) into the u64
+    // table while the next slots cross
+    bool widen = false;
+    HostPool* pool = nullptr;
+    unsigned char* ring = nullptr;
+    size_t ring_slot = 0;
+    std::thread kthread;
+    std::string kerr;
+    double ms_widen = 0;
+    uint64_t key_unit = 1;  // the keys' latency unit (set by the build that wrote them)
+    void send_keys(hipStream_t st, const uint32_t* dkey, size_t row0, size_t rows, uint64_t unit) {
+        if (!rows || !n) return;
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.push_back(e);
+        HIP_CHECK(hipEventRecord(e, st));
+        kthread = std::thread([this, e, dkey, row0, rows, unit]() { key_worker(e, dkey, row0, rows, unit); });
+        early_bytes += rows * n * 4;
+    }
+    void key_worker(hipEvent_t ev, const uint32_t* dkey, size_t row0, size_t rows, uint64_t unit) {
+        (void)hipSetDevice(device);
+        if (hipEventSynchronize(ev) != hipSuccess) {
+            kerr = "hipEventSynchronize failed before the key D2H";
+            return;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        constexpr int NS = 3;
+        const size_t rpc = std::max<size_t>(1, ring_slot / (n * 4));  // rows per chunk
+        const size_t nch = (rows + rpc - 1) / rpc;
+        hsa_signal_t sg[NS];
+        int made = 0;
+        for (; made < NS; ++made)
+            if (hsa_signal_create(0, 0, nullptr, &sg[made]) != HSA_STATUS_SUCCESS) break;
+        if (made < NS) {
+            for (int i = 0; i < made; ++i) hsa_signal_destroy(sg[i]);
+            kerr = "hsa_signal_create failed";
+            return;
+        }
+        auto issue = [&](size_t ci) {
+            const size_t r = ci * rpc, cnt = std::min(rpc, rows - r);
+            hsa_signal_store_relaxed(sg[ci % NS], 1);
+            if (hsa_amd_memory_async_copy_on_engine(ring + (ci % NS) * ring_slot, sdma->cpu, dkey + (row0 + r) * n, sdma->gpu,
+                                                    cnt * n * 4, 0, nullptr, sg[ci % NS],
+                                                    (hsa_amd_sdma_engine_id_t)sdma->engine, true) != HSA_STATUS_SUCCESS) {
+                kerr = "hsa_amd_memory_async_copy_on_engine failed (keys)";
+                hsa_signal_store_relaxed(sg[ci % NS], 0);
+                return false;
+            }
+            return true;
+        };
+        bool ok = true;
+        for (size_t ci = 0; ci < std::min<size_t>(NS, nch) && ok; ++ci) ok = issue(ci);
+        for (size_t ci = 0; ci < nch && ok; ++ci) {
+            hsa_signal_wait_scacquire(sg[ci % NS], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            const size_t r = ci * rpc, cnt = std::min(rpc, rows - r);
+            const uint32_t* kb = reinterpret_cast<const uint32_t*>(ring + (ci % NS) * ring_slot);
+            uint64_t* ob = lat + (row0 + r) * n;
+            const size_t tot = cnt * n;
+            pool->run([&](int w, int nw) {  // (the diagonal's 0xFFFFFFFF is patched by the caller)
+                const size_t a = tot * w / nw, z = tot * (w + 1) / nw;
+                if (unit == 1)
+                    for (size_t i = a; i < z; ++i) ob[i] = kb[i];
+                else
+                    for (size_t i = a; i < z; ++i) ob[i] = (uint64_t)kb[i] * unit;
+            });
+            if (ci + NS < nch) ok = issue(ci + NS);
+        }
+        // drain: no copy may still target the ring when the call returns
+        for (int i = 0; i < NS; ++i) {
+            hsa_signal_wait_scacquire(sg[i], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            hsa_signal_destroy(sg[i]);
+        }
+        ms_widen = ms_since(t0);
+    }
     bool ok() {
         if (!checked) {
             registered = ready && ready();
@@ -1075,6 +1151,8 @@ struct HostSink {
     }
     // wait for every copy; throws on a failed one
     void finish() {
+        if (kthread.joinable()) kthread.join();
+        if (!kerr.empty()) fail(SRG_ERR_HIP, "key D2H: " + kerr);
         if (worker.joinable()) {
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -1094,6 +1172,7 @@ struct HostSink {
         if (!err.empty()) fail(SRG_ERR_HIP, "D2H copy: " + err);
     }
     ~HostSink() {  // an exception unwound past finish(): drain before the buffers go away
+        if (kthread.joinable()) kthread.join();
         if (worker.joinable()) {
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -2007,8 +2086,13 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                FwOverlap* ov = nullptr) {
     // the FW already ran beside the H2D (FwOverlap): W, D and the closed D are in place
     const bool pre = ov && ov->on && ov->ok && ov->ended && sizeof(K) == 4 && T == FwOverlap::T;
-    if (sizeof(K) == 8 && c.kout_key)  // a key table needs the u32 keys
-        fail(SRG_INTERNAL_NEED_U64, "the build needs u64 latency keys: no u32 key table");
+    if (sizeof(K) == 8 && c.kout_key) {  // a key table needs the u32 keys
+        // (the host entry's internal key shipping just falls back to the u64 latency rows)
+        if (!(sink && sink->widen)) fail(SRG_INTERNAL_NEED_U64, "the build needs u64 latency keys: no u32 key table");
+        sink->widen = false;
+        c.kout_key = nullptr;
+        c.kout_diag = nullptr;
+    }
     const uint32_t V = g.V;
     const size_t Vp = ((size_t)V + T - 1) / T * T;
     const size_t VV = Vp * Vp;
@@ -2224,8 +2308,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // host entry, own rows only (one rank, or several without the exchange): the latency rows are
     // final -- they leave during the scan / loss pass
     const bool sink_rows = sink && !exchange && nloc && sink->ok();
+    if (sink && c.kout_key) sink->key_unit = P.unit;
     if (sink_rows) {
-        if (c.kout_key) sink->send_rows(st, c.kout_key, sink->lat, pl.p0, nloc, 4);  // (sink->lat: the host key table)
+        if (c.kout_key && sink->widen) sink->send_keys(st, c.kout_key, pl.p0, nloc, P.unit);  // (widened on the host)
+        else if (c.kout_key) sink->send_rows(st, c.kout_key, sink->lat, pl.p0, nloc, 4);  // (sink->lat: the host key table)
         else sink->send_rows(st, out_lat, sink->lat, pl.p0, nloc, 8);
         sink->lat_sent = true;
     }
@@ -3516,10 +3602,20 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
                                               q0 * n * 4);
         HIP_CHECK(hipStreamSynchronize(hst));  // (beside FW when it started early: st still runs it)
         const double ms_h2d = ms_since(t0);
+        // u64 output of a dense u32 build on one rank: the latency rows cross PCIe as the build's u32
+        // keys and are widened on the host (HostSink::send_keys; 0.6 GB less D2H at C3); a build that
+        // turns out to need u64 keys ships the u64 rows instead (run_dense clears sink.widen)
+        bool ikeys = !keys && !direct && early && nr == 1 && c->sdma.ok && c->d2h_mode == 1 && c->h_ring &&
+                     c->pool && (size_t)n * 4 <= c->h_ring_bytes / 3 && !std::getenv("SRG_NO_KEY_D2H");
+        {
+            DevGraph probe{g->num_vertices, (int)g->directed, E};
+            ikeys = ikeys && !choose_sparse(*c, probe);
+        }
+        bool kmode = keys || ikeys;
         // key mode: the device key table in the latency buffer's room, the diagonal beside it; the
         // kernels see them through the context for this call
-        uint32_t* dkey = keys ? reinterpret_cast<uint32_t*>(dol) : nullptr;
-        uint64_t* ddiag = keys ? (uint64_t*)c->b_odiag.get(std::max<size_t>(n, 1) * 8) : nullptr;
+        uint32_t* dkey = kmode ? reinterpret_cast<uint32_t*>(dol) : nullptr;
+        uint64_t* ddiag = kmode ? (uint64_t*)c->b_odiag.get(std::max<size_t>(n, 1) * 8) : nullptr;
         struct KeyScope {
             srg_ctx* c;
             ~KeyScope() { c->kout_key = nullptr, c->kout_diag = nullptr; }
@@ -3528,6 +3624,10 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         c->kout_diag = ddiag;
         HostSink sink;
         sink.lat = keys ? reinterpret_cast<uint64_t*>(out_key) : out_lat;  // (a host table pointer either way)
+        sink.widen = ikeys;
+        sink.pool = c->pool;
+        sink.ring = (unsigned char*)c->h_ring;
+        sink.ring_slot = c->h_ring_bytes / 3;
         sink.loss = out_loss;
         sink.n = n;
         sink.cs = c->d2h_stream;
@@ -3556,8 +3656,17 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         }
         c->own_row0 = 0;
         c->own_row1 = ~(size_t)0;
-        if (direct) direct_device(*c, dg, dn, num_nodes, dol, dos, st);
-        else compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr, ov.on ? &ov : nullptr);
+        if (direct) {
+            direct_device(*c, dg, dn, num_nodes, dol, dos, st);
+        } else {
+            compute_device(*c, dg, dn, num_nodes, dol, dos, st, stats, early ? &sink : nullptr, ov.on ? &ov : nullptr);
+            if (ikeys && !sink.widen) {  // the build took u64 keys (run_dense dropped the key table)
+                ikeys = false;
+                kmode = keys;
+                dkey = nullptr;
+                ddiag = nullptr;
+            }
+        }
         if (dg.late) {  // a path that never read the losses (error-free early return): drain
             dg.late->join();
             HIP_CHECK(hipStreamSynchronize(c->loss_stream));
@@ -3573,7 +3682,7 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         if (rows_nn && stats) {  // smallest latency over the table (feeds the runahead, manager.rs:238-243)
             unsigned long long* dmin = (unsigned long long*)c->b_multi.get(16);
             HIP_CHECK(hipMemsetAsync(dmin, 0xFF, 16, st));
-            if (keys) {  // smallest key (x unit below) and smallest diagonal latency
+            if (kmode) {  // smallest key (x unit below) and smallest diagonal latency
                 k_min_u32<<<grid_for(rows_nn, 1024), kThreads, 0, st>>>(dkey + rows_off, rows_nn, dmin);
                 k_min_u64<<<grid_for(n, 1024), kThreads, 0, st>>>(ddiag, n, dmin + 1);
             } else {
@@ -3584,22 +3693,31 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         if (rows_nn && !sink.lat_sent) {
             if (keys)
                 HIP_CHECK(hipMemcpyAsync(out_key + rows_off, dkey + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
-            else
+            else if (!ikeys)
                 HIP_CHECK(hipMemcpyAsync(out_lat + rows_off, dol + rows_off, rows_nn * 8, hipMemcpyDeviceToHost, st));
         }
         if (keys && n) HIP_CHECK(hipMemcpyAsync(out_diag, ddiag, n * 8, hipMemcpyDeviceToHost, st));
+        std::vector<uint64_t> hdiag(ikeys ? n : 0);  // the diagonal the widened rows are patched with
+        if (ikeys && n) HIP_CHECK(hipMemcpyAsync(hdiag.data(), ddiag, n * 8, hipMemcpyDeviceToHost, st));
         if (rows_nn && !sink.loss_sent)
             HIP_CHECK(hipMemcpyAsync(out_loss + rows_off, dos + rows_off, rows_nn * 4, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         if (rows_nn && stats) {
             hmin = rb_get<unsigned long long>(*c, MS_MIN);
-            if (keys) {
+            if (kmode) {
                 const unsigned long long dmin = *reinterpret_cast<const unsigned long long*>(c->hbox + 64 * MS_MIN + 8);
                 const uint64_t unit = stats->latency_unit_ns ? stats->latency_unit_ns : 1;
                 hmin = std::min<unsigned long long>(hmin == ~0ull ? ~0ull : hmin * unit, dmin);
             }
         }
+        if (ikeys && rows_nn && !sink.lat_sent) {
+            // the rows were not shipped early (the caller's tables could not be page-locked): keys now
+            sink.send_keys(st, dkey, r0, r1 - r0, sink.key_unit);
+            sink.lat_sent = true;
+        }
         sink.finish();
+        if (ikeys)
+            for (size_t r = r0; r < r1; ++r) out_lat[r * n + r] = hdiag[r];  // raw self-loop weights (mod.rs:211-217)
         if (stats) {
             stats->ms_h2d = ms_h2d;
             stats->ms_d2h = ms_since(t1);  // the D2H not hidden behind kernels
