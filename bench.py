@@ -359,6 +359,7 @@ def cold_call(make, args, edges, V):
     allocated, never-touched output arrays -- what Shadow's one call per simulation pays
     (sim_config.rs:137-141; the Rust binding's vec![0u64; n*n] is lazily zeroed memory)."""
     import numpy as np
+    from shadow_amd import _native as N
     t0 = time.perf_counter()
     router = make()
     apply_options(router, args)
@@ -370,6 +371,9 @@ def cold_call(make, args, edges, V):
     ms = (t2 - t0) * 1e3
     del lat, loss
     st = t.stats
+    if hasattr(router, "get_option"):  # srg_create: the HIP runtime's part vs the library's own
+        COLD_BREAKDOWN.update({"create_hip_runtime_ms": round(router.get_option(N.SRG_OPT_CREATE_MS_RUNTIME), 1),
+                               "create_library_ms": round(router.get_option(N.SRG_OPT_CREATE_MS_LIBRARY), 1)})
     COLD_BREAKDOWN.update({"create_ms": round((t1 - t0) * 1e3, 1), "first_call_ms": round((t2 - t1) * 1e3, 1),
                            **{k: round(st[k], 2) for k in ("ms_h2d", "ms_fw", "ms_scan", "ms_d2h", "ms_host_register")
                               if k in st}})
@@ -379,10 +383,12 @@ def cold_call(make, args, edges, V):
 def routing_info_times(edges, V, args, steps=3):
     """What Shadow's call site runs (sim_config.rs:425-462 -> RoutingInfo, mod.rs:428-477): one
     srg_routing_info_build per simulation.  cold = srg_create + the first build (fresh context, fresh
-    host tables); steady = further builds on the same context, each into fresh tables (a RoutingInfo
-    owns its tables).  One rank: the table keeps the build's u32 keys (stats.table_keys)."""
+    host tables); steady = further builds on the same context (a RoutingInfo owns its tables, from the
+    context's pinned-table pool: a freed RoutingInfo's tables are recycled still page-locked).  One
+    rank: the table keeps the build's u32 keys (stats.table_keys)."""
     import numpy as np
     from shadow_amd import Router, generate_routing_info
+    from shadow_amd import _native as N
     ids = list(range(V))
     t0 = time.perf_counter()
     r = Router(0)
@@ -390,6 +396,9 @@ def routing_info_times(edges, V, args, steps=3):
     ri = generate_routing_info(edges, ids, True, r)
     cold = (time.perf_counter() - t0) * 1e3
     keys = ri.stats.get("table_keys")
+    cold_reg = ri.stats.get("ms_host_register")
+    create = {"create_hip_runtime_ms": round(r.get_option(N.SRG_OPT_CREATE_MS_RUNTIME), 1),
+              "create_library_ms": round(r.get_option(N.SRG_OPT_CREATE_MS_LIBRARY), 1)}
     ri.close()
     ts = []
     for _ in range(steps):
@@ -401,7 +410,8 @@ def routing_info_times(edges, V, args, steps=3):
     r.close()
     return {"cold_ms": round(cold, 1), "steady_ms": round(float(np.median(ts)), 2),
             "steady_ms_all": [round(x, 2) for x in ts], "table_keys": keys,
-            "h2d_ms": round(st["ms_h2d"], 2), "d2h_tail_ms": round(st["ms_d2h"], 2)}
+            "h2d_ms": round(st["ms_h2d"], 2), "d2h_tail_ms": round(st["ms_d2h"], 2),
+            "host_register_ms": {"cold": round(cold_reg, 2), "steady": round(st["ms_host_register"], 2)}, **create}
 
 
 def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg, extra):

@@ -110,6 +110,11 @@ typedef struct srg_stats {
                                    PCIe (SRG_OPT_FW_OVERLAP; 0 = none)                              */
     int32_t fw_overlap_kept;    /* host entry: 1 = the FW that ran beside the H2D produced the table
                                    (its certification passed), 0 = the build ran FW after the H2D   */
+    int32_t d2h_key_rows;       /* host entry, u64 output: 1 = the latency rows crossed PCIe as the build's
+                                   u32 keys (4 B instead of 8 per pair) and were widened on the host  */
+    int32_t reserved0;
+    double ms_key_widen;        /* its widening + key-copy wall time on the helper thread (overlapped
+                                   with the loss pass; the part after the kernels is in ms_d2h)     */
 } srg_stats;
 
 #define SRG_PATH_DENSE_U32 0    /* dense FW, u32 saturating latency keys (exact, certified) */
@@ -198,6 +203,14 @@ void srg_destroy(srg_ctx* ctx);
                                      * with SRG_ERR_INTERNAL, not return it); 2 = nonzero FW sync words and zero
                                      * line buffers before each symmetric FW (a recycled allocation: the build
                                      * must still be exact); 0 (default) = off */
+#define SRG_OPT_TABLE_POOL_BYTES 35  /* RoutingInfo tables (srg_routing_info_build, one rank) come from a pool of
+                                     * page-locked host tables on the context; freeing a RoutingInfo returns
+                                     * them, so the next build skips the prefault + page-locking.  Bytes of idle
+                                     * tables the pool keeps (default 8 GiB; 0 = free them at once) */
+#define SRG_OPT_TABLE_POOL_IDLE_BYTES 36  /* read-only: bytes of idle tables the pool holds now */
+#define SRG_OPT_CREATE_MS_RUNTIME 37  /* read-only: srg_create's HIP-runtime part (device count, device context;
+                                      * the first context of a process pays the runtime's initialisation) */
+#define SRG_OPT_CREATE_MS_LIBRARY 38  /* read-only: srg_create's own part (streams, mailbox, SDMA agents, events) */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

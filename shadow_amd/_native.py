@@ -49,6 +49,10 @@ SRG_OPT_FW_LINE_SPLIT = 31
 SRG_OPT_FW_STEP = 32
 SRG_OPT_FW_OVERLAP = 33
 SRG_OPT_TEST_FAULT = 34
+SRG_OPT_TABLE_POOL_BYTES = 35
+SRG_OPT_TABLE_POOL_IDLE_BYTES = 36
+SRG_OPT_CREATE_MS_RUNTIME = 37
+SRG_OPT_CREATE_MS_LIBRARY = 38
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2
@@ -134,6 +138,9 @@ class Stats(ctypes.Structure):
         ("latency_unit_ns", ctypes.c_uint64),
         ("fw_overlap_pivots", ctypes.c_int32),
         ("fw_overlap_kept", ctypes.c_int32),
+        ("d2h_key_rows", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("ms_key_widen", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -473,7 +474,7 @@ __global__ void __launch_bounds__(256) k_extract(const K* __restrict__ D, const 
                                                  uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, Flags* flags,
                                                  int mode, uint64_t unit, uint32_t* __restrict__ out_key = nullptr,
                                                  uint64_t* __restrict__ out_diag = nullptr) {
-    // out_key (RoutingInfo's key table, srg_internal_compute_keys): latencies as u32 keys instead of
+    // out_key (RoutingInfo's key table, srg_internal_compute_table): latencies as u32 keys instead of
     // ns (0xFFFFFFFF on the diagonal, whose raw self-loop latency goes to out_diag)
     // mode bit 0: latency (+ unreachable check), bit 1: loss from L; one workgroup per local row a,
     // U columns per thread in flight (the gathers are latency-bound)
@@ -694,6 +695,48 @@ struct SdmaAgents {
     }
 };
 
+// Pinned-table pool (srg_internal_table_get / _put): the host tables a RoutingInfo owns
+// (routing_info.cpp) come from their context's pool and go back to it when the RoutingInfo is
+// freed, still page-locked.  The first build into a table pays the prefault + hipHostRegister
+// (on the host entry's helper thread, beside the H2D and FW, as for any caller's table); a later
+// build into a recycled table pays neither (the 1.2 GB C3 pair: ~12 ms cold, measured r04).
+// A table can outlive its context: it holds the pool by reference count, and a closed pool frees
+// what comes back.
+struct TablePool;
+struct srg_table {
+    std::shared_ptr<TablePool> pool;
+    void* p = nullptr;         // 2 MB aligned (transparent huge pages)
+    size_t cap = 0;            // its bytes (a multiple of 2 MB)
+    void* view = nullptr;      // its device view once registered
+    bool registered = false;
+};
+struct TablePool {
+    std::mutex mu;
+    std::vector<srg_table*> idle;
+    size_t idle_bytes = 0;
+    size_t limit = (size_t)8 << 30;  // idle bytes kept (SRG_OPT_TABLE_POOL_BYTES)
+    bool open = true;
+    static void destroy(srg_table* t);
+    void trim_locked(size_t keep) {  // the oldest idle tables first
+        while (idle_bytes > keep && !idle.empty()) {
+            srg_table* t = idle.front();
+            idle.erase(idle.begin());
+            idle_bytes -= t->cap;
+            destroy(t);
+        }
+    }
+    void close() {
+        std::lock_guard<std::mutex> lk(mu);
+        open = false;
+        trim_locked(0);
+    }
+};
+void TablePool::destroy(srg_table* t) {
+    if (t->registered) (void)hipHostUnregister(t->p);
+    if (t->p) munmap(t->p, t->cap);
+    delete t;
+}
+
 struct srg_ctx {
     int device = 0;
     double sparse_threshold = 0.35;  // essential-edge density above which the dense scan is used
@@ -767,6 +810,8 @@ struct srg_ctx {
     DevBuf b_odiag;
     int fw_overlap = 1;                 // host entry: FW starts while the edge list arrives (SRG_OPT_FW_OVERLAP)
     int test_fault = 0;                 // TEST HOOK (SRG_OPT_TEST_FAULT): 1 = zero D after FW, 2 = stale FW sync words
+    std::shared_ptr<TablePool> tpool = std::make_shared<TablePool>();  // RoutingInfo's pinned tables
+    double ms_create_runtime = 0, ms_create_lib = 0;  // srg_create: HIP runtime / device init vs the library's own
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
@@ -796,6 +841,7 @@ struct srg_ctx {
         if (h_ring) (void)hipHostFree(h_ring);
         for (DevBuf* b : {&b_n16s, &b_n16d, &b_n32l, &b_DST2, &b_exc})
             b->release();
+        tpool->close();
     }
 };
 
@@ -3313,11 +3359,11 @@ int guard(char* errbuf, size_t errlen, const std::function<void()>& body) {
     }
 }
 
-// out_key / out_diag (srg_internal_compute_keys, RoutingInfo's key table): non-null = the latencies
+// out_key / out_diag (srg_internal_compute_table, RoutingInfo's key table): non-null = the latencies
 // leave as the build's u32 keys plus the diagonal's raw self-loop latencies; out_lat is unused then
 int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32_t num_nodes, uint64_t* out_lat,
                float* out_loss, srg_stats* stats, char* errbuf, size_t errlen, bool direct,
-               uint32_t* out_key = nullptr, uint64_t* out_diag = nullptr) {
+               uint32_t* out_key = nullptr, uint64_t* out_diag = nullptr, srg_table* const* tabs = nullptr) {
     const bool keys = out_key != nullptr;
     if (keys && (direct || (c && c->comm && c->comm->nranks > 1) || (num_nodes && !out_diag))) {
         set_err(errbuf, errlen, "key table: one rank, shortest paths only");
@@ -3343,15 +3389,37 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         size_t b[2] = {0, 0};
         hipStream_t wait = nullptr;
         bool fault = true;
+        srg_table* tab[2] = {nullptr, nullptr};  // pooled tables (RoutingInfo): stay registered after the call
         bool join() {
             if (th.joinable()) th.join();
             return ok;
+        }
+        void run() {
+            const auto t0 = std::chrono::steady_clock::now();
+            if (!b[0] || hipSetDevice(device) != hipSuccess) return;
+            for (int i = 0; i < 2; ++i) {
+                if (tab[i] && tab[i]->registered) {  // a recycled pooled table: nothing to do
+                    view[i] = tab[i]->view;
+                    continue;
+                }
+                advise_huge(p[i], b[i]);
+                if (fault) prefault(p[i], b[i], 8);
+                if (hipHostRegister(p[i], b[i], hipHostRegisterMapped) != hipSuccess) {
+                    if (i == 1 && !tab[0]) (void)hipHostUnregister(p[0]);
+                    return;
+                }
+                if (hipHostGetDevicePointer(&view[i], p[i], 0) != hipSuccess) view[i] = nullptr;
+                if (tab[i]) tab[i]->registered = true, tab[i]->view = view[i];
+            }
+            ms = ms_since(t0);
+            ok = true;
         }
         ~Registration() {
             if (th.joinable()) th.join();
             if (ok) {
                 (void)hipStreamSynchronize(wait);  // no copy into the buffers may be in flight
-                for (int i = 0; i < 2; ++i) (void)hipHostUnregister(p[i]);
+                for (int i = 0; i < 2; ++i)
+                    if (!tab[i]) (void)hipHostUnregister(p[i]);
             }
         }
     } reg;
@@ -3369,30 +3437,17 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
     const size_t reg_r1 = rows_part ? (size_t)num_nodes * (c->comm->rank + 1) / c->comm->nranks : num_nodes;
     const size_t lat_elem = keys ? 4 : 8;
     unsigned char* out_lat_b = keys ? (unsigned char*)out_key : (unsigned char*)out_lat;  // the latency table
+    // pooled tables (srg_internal_compute_table): the whole mapping is registered once and kept
+    const bool pooled = early && !ext && !rows_part && tabs && tabs[0] && tabs[1] && tabs[0]->p == out_lat_b &&
+                        tabs[1]->p == (void*)out_loss && tabs[0]->cap >= nn * lat_elem && tabs[1]->cap >= nn * 4;
     if (early && !ext) {
         reg.p[0] = out_lat_b + reg_r0 * num_nodes * lat_elem;
         reg.b[0] = (reg_r1 - reg_r0) * num_nodes * lat_elem;
         reg.p[1] = out_loss + reg_r0 * num_nodes;
         reg.b[1] = (reg_r1 - reg_r0) * num_nodes * 4;
-        reg.th = std::thread([&reg]() {
-            const auto t0 = std::chrono::steady_clock::now();
-            if (!reg.b[0] || hipSetDevice(reg.device) != hipSuccess) return;
-            advise_huge(reg.p[0], reg.b[0]);
-            advise_huge(reg.p[1], reg.b[1]);
-            if (reg.fault) {
-                prefault(reg.p[0], reg.b[0], 8);
-                prefault(reg.p[1], reg.b[1], 8);
-            }
-            if (hipHostRegister(reg.p[0], reg.b[0], hipHostRegisterMapped) != hipSuccess) return;
-            if (hipHostRegister(reg.p[1], reg.b[1], hipHostRegisterMapped) != hipSuccess) {
-                (void)hipHostUnregister(reg.p[0]);
-                return;
-            }
-            for (int i = 0; i < 2; ++i)
-                if (hipHostGetDevicePointer(&reg.view[i], reg.p[i], 0) != hipSuccess) reg.view[i] = nullptr;
-            reg.ms = ms_since(t0);
-            reg.ok = true;
-        });
+        if (pooled)
+            for (int i = 0; i < 2; ++i) reg.tab[i] = tabs[i], reg.b[i] = tabs[i]->cap;
+        reg.th = std::thread([&reg]() { reg.run(); });
     }
     return guard(errbuf, errlen, [&]() {
         auto t0 = std::chrono::steady_clock::now();
@@ -3724,6 +3779,8 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             stats->ms_total = ms_since(t0);
             stats->ms_host_register = ext ? (sink.registered ? reg.ms : -1.0) : reg.join() ? reg.ms : -1.0;
             stats->d2h_overlapped_bytes = sink.early_bytes;
+            stats->d2h_key_rows = ikeys ? 1 : 0;
+            stats->ms_key_widen = sink.ms_widen;
             stats->min_latency_ns = hmin;
             if (direct) stats->path_kind = SRG_PATH_DIRECT;
         }
@@ -3748,6 +3805,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
             if (dbg) std::fprintf(stderr, "srg_create: %-28s %7.2f ms\n", what, ms_since(tc));
             tc = std::chrono::steady_clock::now();
         };
+        const auto tcreate = std::chrono::steady_clock::now();
         int count = 0;
         hipError_t e = hipGetDeviceCount(&count);
         lap("hipGetDeviceCount");
@@ -3758,7 +3816,10 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         c = new srg_ctx();
         c->device = device;
         HIP_CHECK(hipSetDevice(device));
+        HIP_CHECK(hipFree(nullptr));  // (the device's runtime context, if this process has none yet)
         lap("hipSetDevice");
+        c->ms_create_runtime = ms_since(tcreate);
+        const auto tlib = std::chrono::steady_clock::now();
         HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         // the FW lookahead chain (pivot close, row/col panels) is latency-critical: its workgroups
         // should be dispatched ahead of the bulk phase-3 tiles
@@ -3786,6 +3847,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
             HIP_CHECK(hipStreamSynchronize(c->stream));
         }
         lap("events, signals");
+        c->ms_create_lib = ms_since(tlib);
         std::lock_guard<std::mutex> lk(g_dev_mu);
         ++g_dev_ctx[device];
     });
@@ -3882,6 +3944,13 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
             ctx->test_fault = (int)value;
             return SRG_OK;
+        case SRG_OPT_TABLE_POOL_BYTES: {
+            if (!(value >= 0.0 && value <= 1e15)) return SRG_ERR_ARG;
+            std::lock_guard<std::mutex> pl(ctx->tpool->mu);
+            ctx->tpool->limit = (size_t)value;
+            ctx->tpool->trim_locked(ctx->tpool->limit);
+            return SRG_OK;
+        }
         case SRG_OPT_ALGORITHM:
             if (value != SRG_ALGO_AUTO && value != SRG_ALGO_DENSE && value != SRG_ALGO_SPARSE) return SRG_ERR_ARG;
             ctx->algorithm = (int)value;
@@ -3914,6 +3983,18 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         case SRG_OPT_FW_STEP: *value = ctx->fw_step; break;
         case SRG_OPT_FW_OVERLAP: *value = ctx->fw_overlap; break;
         case SRG_OPT_TEST_FAULT: *value = ctx->test_fault; break;
+        case SRG_OPT_TABLE_POOL_BYTES: {
+            std::lock_guard<std::mutex> pl(ctx->tpool->mu);
+            *value = (double)ctx->tpool->limit;
+            break;
+        }
+        case SRG_OPT_TABLE_POOL_IDLE_BYTES: {
+            std::lock_guard<std::mutex> pl(ctx->tpool->mu);
+            *value = (double)ctx->tpool->idle_bytes;
+            break;
+        }
+        case SRG_OPT_CREATE_MS_RUNTIME: *value = ctx->ms_create_runtime; break;
+        case SRG_OPT_CREATE_MS_LIBRARY: *value = ctx->ms_create_lib; break;
         default: return SRG_ERR_ARG;
     }
     return SRG_OK;
@@ -3929,14 +4010,69 @@ void srg_destroy(srg_ctx* ctx) {
     delete ctx;
 }
 
-int srg_internal_compute_keys(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
-                              uint32_t* out_key, uint64_t* out_diag, float* out_loss, uint64_t* unit_ns,
-                              srg_stats* stats, char* errbuf, size_t errlen) {
+int srg_internal_compute_table(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,
+                               int shortest, uint64_t* out_lat, uint32_t* out_key, uint64_t* out_diag, float* out_loss,
+                               uint64_t* unit_ns, srg_table* tab_lat, srg_table* tab_loss, srg_stats* stats,
+                               char* errbuf, size_t errlen) {
     srg_stats local{};
     srg_stats* st = stats ? stats : &local;
-    const int rc = host_entry(ctx, graph, nodes, num_nodes, nullptr, out_loss, st, errbuf, errlen, false, out_key, out_diag);
-    if (unit_ns) *unit_ns = st->latency_unit_ns ? st->latency_unit_ns : 1;
+    srg_table* tabs[2] = {tab_lat, tab_loss};
+    const int rc = host_entry(ctx, graph, nodes, num_nodes, out_key ? nullptr : out_lat, out_loss, st, errbuf, errlen,
+                              !shortest, out_key, out_diag, tabs);
+    if (unit_ns) *unit_ns = out_key && st->latency_unit_ns ? st->latency_unit_ns : 1;
     return rc;
+}
+
+srg_table* srg_internal_table_get(srg_ctx* ctx, size_t bytes, void** host) {
+    if (!ctx || !host) return nullptr;
+    *host = nullptr;
+    constexpr size_t HP = (size_t)2 << 20;
+    const size_t cap = (std::max<size_t>(bytes, 1) + HP - 1) / HP * HP;
+    TablePool& P = *ctx->tpool;
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        size_t best = SIZE_MAX;
+        for (size_t i = 0; i < P.idle.size(); ++i)  // the smallest idle table that holds it (and < 2x)
+            if (P.idle[i]->cap >= cap && P.idle[i]->cap <= 2 * cap && (best == SIZE_MAX || P.idle[i]->cap < P.idle[best]->cap))
+                best = i;
+        if (best != SIZE_MAX) {
+            srg_table* t = P.idle[best];
+            P.idle.erase(P.idle.begin() + best);
+            P.idle_bytes -= t->cap;
+            *host = t->p;
+            return t;
+        }
+    }
+    // a fresh mapping, 2 MB aligned; its pages are faulted in and locked by the first build into
+    // it (host_entry's registration thread, beside the H2D and FW)
+    void* m = mmap(nullptr, cap + HP, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) return nullptr;
+    const uintptr_t a = ((uintptr_t)m + HP - 1) / HP * HP;
+    if (a > (uintptr_t)m) munmap(m, a - (uintptr_t)m);
+    if ((uintptr_t)m + cap + HP > a + cap) munmap((void*)(a + cap), (uintptr_t)m + cap + HP - (a + cap));
+    srg_table* t = new (std::nothrow) srg_table();
+    if (!t) {
+        munmap((void*)a, cap);
+        return nullptr;
+    }
+    t->pool = ctx->tpool;
+    t->p = (void*)a;
+    t->cap = cap;
+    *host = t->p;
+    return t;
+}
+
+void srg_internal_table_put(srg_table* t) {
+    if (!t) return;
+    std::shared_ptr<TablePool> P = t->pool;  // (keeps the pool alive past this table)
+    std::lock_guard<std::mutex> lk(P->mu);
+    if (P->open && t->cap <= P->limit) {
+        P->idle.push_back(t);
+        P->idle_bytes += t->cap;
+        P->trim_locked(P->limit);
+    } else {
+        TablePool::destroy(t);
+    }
 }
 
 int srg_compute_shortest_paths(srg_ctx* ctx, const srg_edge_list* graph, const uint32_t* nodes, uint32_t num_nodes,

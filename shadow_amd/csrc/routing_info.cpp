@@ -8,7 +8,10 @@
 // The reference materialises two HashMaps of n^2 entries (mod.rs:190-208 and sim_config.rs:448-450:
 // 2 x 10^8 inserts at C3).  Here the table stays the dense n x n SoA the GPU wrote (row-major by
 // position of the id in the caller's list) plus a GML-id -> position index, so the build is the
-// host entry (H2D + kernels + overlapped D2H) and nothing else.  Host-only C++: no HIP calls here.
+// host entry (H2D + kernels + overlapped D2H) and nothing else.  A single-context RoutingInfo owns
+// its tables from the context's pinned-table pool (srg_internal_table_get): freeing it returns them
+// still page-locked, so the next build skips the prefault + page-locking.  Host-only C++: no HIP
+// calls here.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -45,6 +48,33 @@ struct Counters {
     Shard& of(uint64_t k) { return shard[(k * 0x9E3779B97F4A7C15ull) >> 58]; }
 };
 
+// an n x n host table: from the context's pool (single context), else plain heap memory
+struct HostTable {
+    srg_table* pooled = nullptr;
+    std::unique_ptr<unsigned char[]> own;
+    void* p = nullptr;
+    HostTable() = default;
+    HostTable(const HostTable&) = delete;
+    HostTable& operator=(const HostTable&) = delete;
+    void alloc(srg_ctx* ctx, size_t bytes) {
+        reset();
+        if (ctx) {
+            pooled = srg_internal_table_get(ctx, bytes, &p);
+            if (!pooled) throw std::bad_alloc();
+        } else {
+            own.reset(new unsigned char[std::max<size_t>(bytes, 1)]);
+            p = own.get();
+        }
+    }
+    void reset() {
+        if (pooled) srg_internal_table_put(pooled);
+        pooled = nullptr;
+        own.reset();
+        p = nullptr;
+    }
+    ~HostTable() { reset(); }
+};
+
 }  // namespace
 
 struct srg_routing_info {
@@ -54,12 +84,14 @@ struct srg_routing_info {
     // Latencies are kept either as the build's certified u32 keys (key = latency / unit, exact; the
     // diagonal's raw self-loop latencies in diag) -- 0.4 GB less D2H and host memory at C3 -- or,
     // when the build needed u64 keys or ran on several ranks, as u64 ns in lat.
-    std::unique_ptr<uint64_t[]> lat;
-    std::unique_ptr<uint32_t[]> key;
+    HostTable t_lat, t_key, t_loss;
+    uint64_t* lat = nullptr;
+    uint32_t* key = nullptr;
     std::vector<uint64_t> diag;
     uint64_t unit = 1;
-    std::unique_ptr<float[]> loss;
-    std::once_flag widened;          // tables(): the u64 view of a key table, built on first use
+    float* loss = nullptr;
+    std::unique_ptr<uint64_t[]> lat_wide;  // tables(): the u64 view of a key table, built on first use
+    std::once_flag widened;
     uint64_t min_lat = UINT64_MAX;
     // GML id -> position: a direct table when the ids are dense enough, else a hash map
     std::vector<uint32_t> pos_direct;
@@ -75,13 +107,17 @@ struct srg_routing_info {
 
 namespace {
 
-// compute(nodes, n, out_lat, out_loss, stats, errbuf, errlen): one of the host entry points
-using Compute = std::function<int(const uint32_t*, uint32_t, uint64_t*, float*, srg_stats*, char*, size_t)>;
-// compute_keys(nodes, n, out_key, out_diag, out_loss, unit, stats, errbuf, errlen): the key-table entry
-using ComputeKeys = std::function<int(const uint32_t*, uint32_t, uint32_t*, uint64_t*, float*, uint64_t*, srg_stats*,
-                                      char*, size_t)>;
+// compute(nodes, n, out_lat, out_loss, tab_lat, tab_loss, stats, errbuf, errlen): one of the host
+// entry points (tab_*: the tables' pool handles, null for heap tables)
+using Compute = std::function<int(const uint32_t*, uint32_t, uint64_t*, float*, srg_table*, srg_table*, srg_stats*,
+                                  char*, size_t)>;
+// compute_keys(nodes, n, out_key, out_diag, out_loss, unit, tab_key, tab_loss, stats, errbuf, errlen):
+// the key-table entry
+using ComputeKeys = std::function<int(const uint32_t*, uint32_t, uint32_t*, uint64_t*, float*, uint64_t*, srg_table*,
+                                      srg_table*, srg_stats*, char*, size_t)>;
 
-int build_routing_info(const Compute& compute, const ComputeKeys& compute_keys, const srg_edge_list* graph,
+// ctx: the context whose pool holds the tables (null: heap tables)
+int build_routing_info(srg_ctx* ctx, const Compute& compute, const ComputeKeys& compute_keys, const srg_edge_list* graph,
                        const uint32_t* gml_ids, uint32_t num_ids, int use_shortest_paths, srg_routing_info** out,
                        srg_stats* stats, char* errbuf, size_t errlen) {
     *out = nullptr;
@@ -103,28 +139,34 @@ int build_routing_info(const Compute& compute, const ComputeKeys& compute_keys, 
             nodes[i] = f->second;
         }
         auto* ri = new srg_routing_info();
+        std::unique_ptr<srg_routing_info> hold(ri);
         ri->n = num_ids;
         ri->ids.assign(gml_ids, gml_ids + num_ids);
         const size_t nn = (size_t)num_ids * num_ids;
-        ri->loss.reset(new float[std::max<size_t>(nn, 1)]);
+        ri->t_loss.alloc(ctx, nn * 4);
+        ri->loss = (float*)ri->t_loss.p;
         srg_stats local{};
         srg_stats* st = stats ? stats : &local;
         int rc = SRG_INTERNAL_NEED_U64;
         if (compute_keys) {
-            ri->key.reset(new uint32_t[std::max<size_t>(nn, 1)]);
+            ri->t_key.alloc(ctx, nn * 4);
+            ri->key = (uint32_t*)ri->t_key.p;
             ri->diag.resize(num_ids);
-            rc = compute_keys(nodes.data(), num_ids, ri->key.get(), ri->diag.data(), ri->loss.get(), &ri->unit, st,
-                              errbuf, errlen);
+            rc = compute_keys(nodes.data(), num_ids, ri->key, ri->diag.data(), ri->loss, &ri->unit, ri->t_key.pooled,
+                              ri->t_loss.pooled, st, errbuf, errlen);
             if (rc == SRG_INTERNAL_NEED_U64) {
-                ri->key.reset();
+                ri->t_key.reset();
+                ri->key = nullptr;
                 ri->diag.clear();
                 ri->unit = 1;
             }
         }
         if (rc == SRG_INTERNAL_NEED_U64) {
-            ri->lat.reset(new uint64_t[std::max<size_t>(nn, 1)]);
-            rc = compute(nodes.data(), num_ids, ri->lat.get(), ri->loss.get(), st, errbuf, errlen);
+            ri->t_lat.alloc(ctx, nn * 8);
+            ri->lat = (uint64_t*)ri->t_lat.p;
+            rc = compute(nodes.data(), num_ids, ri->lat, ri->loss, ri->t_lat.pooled, ri->t_loss.pooled, st, errbuf, errlen);
         }
+        hold.release();
         if (rc != SRG_OK) {
             delete ri;
             // .context("Failed to compute shortest paths between graph nodes") (sim_config.rs:446-447)
@@ -138,7 +180,7 @@ int build_routing_info(const Compute& compute, const ComputeKeys& compute_keys, 
             return rc;
         }
         ri->min_lat = st->min_latency_ns;
-        if (!use_shortest_paths) ri->min_lat = nn ? *std::min_element(ri->lat.get(), ri->lat.get() + nn) : UINT64_MAX;
+        if (!use_shortest_paths) ri->min_lat = nn ? *std::min_element(ri->lat, ri->lat + nn) : UINT64_MAX;
         if (stats) stats->table_keys = ri->key ? 1 : 0;
         uint32_t max_id = 0;
         for (uint32_t id : ri->ids) max_id = std::max(max_id, id);
@@ -194,7 +236,14 @@ int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint3
                 "(SRG_OPT_GATHER_OUTPUT 0); use srg_routing_info_build_multi or SRG_OPT_GATHER_OUTPUT 1");
         return SRG_ERR_ARG;
     }
-    Compute f = [&](const uint32_t* nodes, uint32_t n, uint64_t* lat, float* loss, srg_stats* st, char* eb, size_t el) {
+    // one rank: the tables come from the context's pool (a rank of a group writes its shared table
+    // through the group's page-locking instead)
+    srg_ctx* pool_ctx = nr == 1 ? ctx : nullptr;
+    Compute f = [&](const uint32_t* nodes, uint32_t n, uint64_t* lat, float* loss, srg_table* tl, srg_table* ts,
+                    srg_stats* st, char* eb, size_t el) {
+        if (tl && ts)
+            return srg_internal_compute_table(ctx, graph, nodes, n, use_shortest_paths, lat, nullptr, nullptr, loss,
+                                              nullptr, tl, ts, st, eb, el);
         return use_shortest_paths ? srg_compute_shortest_paths(ctx, graph, nodes, n, lat, loss, st, eb, el)
                                   : srg_get_direct_paths(ctx, graph, nodes, n, lat, loss, st, eb, el);
     };
@@ -202,10 +251,11 @@ int srg_routing_info_build(srg_ctx* ctx, const srg_edge_list* graph, const uint3
     ComputeKeys fk = nullptr;
     if (use_shortest_paths && nr == 1)
         fk = [&](const uint32_t* nodes, uint32_t n, uint32_t* key, uint64_t* diag, float* loss, uint64_t* unit,
-                 srg_stats* st, char* eb, size_t el) {
-            return srg_internal_compute_keys(ctx, graph, nodes, n, key, diag, loss, unit, st, eb, el);
+                 srg_table* tk, srg_table* ts, srg_stats* st, char* eb, size_t el) {
+            return srg_internal_compute_table(ctx, graph, nodes, n, 1, nullptr, key, diag, loss, unit, tk, ts, st, eb,
+                                              el);
         };
-    return build_routing_info(f, fk, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
+    return build_routing_info(pool_ctx, f, fk, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
 }
 
 int srg_routing_info_build_multi(srg_multi* m, const srg_edge_list* graph, const uint32_t* gml_ids, uint32_t num_ids,
@@ -215,11 +265,12 @@ int srg_routing_info_build_multi(srg_multi* m, const srg_edge_list* graph, const
         put_err(errbuf, errlen, "null argument");
         return SRG_ERR_ARG;
     }
-    Compute f = [&](const uint32_t* nodes, uint32_t n, uint64_t* lat, float* loss, srg_stats* st, char* eb, size_t el) {
+    Compute f = [&](const uint32_t* nodes, uint32_t n, uint64_t* lat, float* loss, srg_table*, srg_table*, srg_stats* st,
+                    char* eb, size_t el) {
         return use_shortest_paths ? srg_multi_compute_shortest_paths(m, graph, nodes, n, lat, loss, st, eb, el)
                                   : srg_multi_get_direct_paths(m, graph, nodes, n, lat, loss, st, eb, el);
     };
-    return build_routing_info(f, nullptr, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
+    return build_routing_info(nullptr, f, nullptr, graph, gml_ids, num_ids, use_shortest_paths, out, stats, errbuf, errlen);
 }
 
 void srg_routing_info_free(srg_routing_info* ri) { delete ri; }
@@ -267,17 +318,18 @@ void srg_routing_info_tables(const srg_routing_info* ri, const uint64_t** latenc
         auto* m = const_cast<srg_routing_info*>(ri);
         std::call_once(m->widened, [m] {
             const size_t nn = (size_t)m->n * m->n;
-            m->lat.reset(new uint64_t[std::max<size_t>(nn, 1)]);
+            m->lat_wide.reset(new uint64_t[std::max<size_t>(nn, 1)]);
+            m->lat = m->lat_wide.get();
             for (uint32_t a = 0; a < m->n; ++a) {
-                const uint32_t* kr = m->key.get() + (size_t)a * m->n;
-                uint64_t* lr = m->lat.get() + (size_t)a * m->n;
+                const uint32_t* kr = m->key + (size_t)a * m->n;
+                uint64_t* lr = m->lat + (size_t)a * m->n;
                 for (uint32_t b = 0; b < m->n; ++b) lr[b] = (uint64_t)kr[b] * m->unit;
                 lr[a] = m->diag[a];
             }
         });
     }
-    if (latency_ns) *latency_ns = ri ? ri->lat.get() : nullptr;
-    if (packet_loss) *packet_loss = ri ? ri->loss.get() : nullptr;
+    if (latency_ns) *latency_ns = ri ? ri->lat : nullptr;
+    if (packet_loss) *packet_loss = ri ? ri->loss : nullptr;
     if (gml_ids) *gml_ids = ri ? ri->ids.data() : nullptr;
     if (n) *n = ri ? ri->n : 0;
 }

@@ -158,6 +158,13 @@ class Router:
         if rc != N.SRG_OK:
             _raise(rc, f"srg_set_option({option}, {value}) failed")
 
+    def get_option(self, option):
+        v = ctypes.c_double()
+        rc = N.lib().srg_get_option(self._h, int(option), ctypes.byref(v))
+        if rc != N.SRG_OK:
+            _raise(rc, f"srg_get_option({option}) failed")
+        return v.value
+
     def close(self):
         if getattr(self, "_h", None):
             N.lib().srg_destroy(self._h)

@@ -51,4 +51,4 @@ def test_no_cpu_fallback_without_gpu():
 
 def test_struct_layouts():
     assert ctypes.sizeof(N.EdgeList) == 4 + 4 + 8 + 5 * 8
-    assert ctypes.sizeof(N.Stats) == 8 * 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 8 + 8 + 4 + 4
+    assert ctypes.sizeof(N.Stats) == 8 * 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 8 + 4 + 4 + 8 + 8 + 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8
