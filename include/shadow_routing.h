@@ -211,9 +211,6 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_CREATE_MS_RUNTIME 37  /* read-only: srg_create's HIP-runtime part (device count, device context;
                                       * the first context of a process pays the runtime's initialisation) */
 #define SRG_OPT_CREATE_MS_LIBRARY 38  /* read-only: srg_create's own part (streams, mailbox, SDMA agents, events) */
-#define SRG_OPT_SCAN_KERNEL 39       /* tight-predecessor scan kernel: 5 = tight_v5 (sources on the lanes, the entry
-                                     * stream uniform), 6 = tight_v6 (entries on the lanes, -D of the target tile
-                                     * in LDS); 0 (default) = auto.  Same PRED, bit-exact either way */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

@@ -53,7 +53,6 @@ SRG_OPT_TABLE_POOL_BYTES = 35
 SRG_OPT_TABLE_POOL_IDLE_BYTES = 36
 SRG_OPT_CREATE_MS_RUNTIME = 37
 SRG_OPT_CREATE_MS_LIBRARY = 38
-SRG_OPT_SCAN_KERNEL = 39
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libshadow_routing.so")
 SOURCES = [os.path.join(CSRC, "routing.hip"), os.path.join(CSRC, "gml.cpp"), os.path.join(CSRC, "comm.hip"),
            os.path.join(CSRC, "routing_info.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "kernels.hip.h"), os.path.join(CSRC, "tight_sparse.hip.h"), os.path.join(CSRC, "tight_v6.hip.h"), os.path.join(CSRC, "comm.h"), os.path.join(CSRC, "sparse.hip.h"), os.path.join(CSRC, "events.hip.h"), os.path.join(CSRC, "edge_codec.h"), os.path.join(CSRC, "xchg.hip.h"), os.path.join(CSRC, "internal.h"), os.path.join(CSRC, "guards.h"), os.path.join(ROOT, "include", "shadow_routing.h")]
+DEPS = SOURCES + [os.path.join(CSRC, "kernels.hip.h"), os.path.join(CSRC, "tight_sparse.hip.h"), os.path.join(CSRC, "comm.h"), os.path.join(CSRC, "sparse.hip.h"), os.path.join(CSRC, "events.hip.h"), os.path.join(CSRC, "edge_codec.h"), os.path.join(CSRC, "xchg.hip.h"), os.path.join(CSRC, "internal.h"), os.path.join(CSRC, "guards.h"), os.path.join(ROOT, "include", "shadow_routing.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SRG_OFFLOAD_ARCH", "gfx950")
 

@@ -40,7 +40,6 @@
 #include "guards.h"
 #include "edge_codec.h"
 #include "tight_sparse.hip.h"
-#include "tight_v6.hip.h"
 #include "comm.h"
 #include "sparse.hip.h"
 #include "events.hip.h"
@@ -772,7 +771,6 @@ struct srg_ctx {
     const uint32_t* sim_edges = nullptr;  // simulated rank: the edge list whose other slices are resident
     size_t sim_E = 0;
     int scan_groups = 0;             // host entry: v5 scan launches interleaved with the loss rows (0 = auto: 3) (SRG_OPT_SCAN_GROUPS)
-    int scan_kernel = 0;             // tight scan: 5 = tight_v5 (source lanes), 6 = tight_v6 (entry lanes), 0 = auto (SRG_OPT_SCAN_KERNEL)
     int loss_chunks = 0;             // k_loss_rows launches (0 = auto: 8 when the host entry ships rows early, else 1) (SRG_OPT_LOSS_CHUNKS)
     srg::Comm* comm = nullptr;       // null = single GPU
     // srg_multi: the caller's output arrays are page-locked once for every rank (portable); the
@@ -787,7 +785,7 @@ struct srg_ctx {
     hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr, ev_e = nullptr;
     std::mutex mu;
     DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
-    DevBuf b_W, b_WL, b_D, b_PRED, b_pmax, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
+    DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
     DevBuf b_stats, b_flags, b_multi, b_pos, b_cnt;
     // sparse tight scan
     DevBuf b_ecnt, b_eoff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu, b_grpe, b_cscent,
@@ -818,7 +816,7 @@ struct srg_ctx {
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
-                          &b_D, &b_PRED, &b_pmax, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
+                          &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
                           &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc, &b_odiag,
@@ -2388,36 +2386,16 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // pair-lane LDS scan (tight_v5); u64 keys run it on the keys' low words (exact together with
     // the loss pass's multi-predecessor check, tight_sparse.hip.h)
     const bool v5lo = sizeof(K) == 8;
-    const bool use6 = c.scan_kernel == 6;  // (auto: tight_v5 until measured otherwise)
     const uint32_t SB = V5_SB;
-    static_assert(V6_SB == V5_SB, "tight_v6 shares tight_v5's DST and source-block cuts");
-    const uint32_t nK6 = (V + V6_UC - 1) / V6_UC;
-    const size_t NQ6 = (size_t)nw64 * nK6;
     const size_t npad = ((size_t)nloc + SB - 1) / SB * SB;
     const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
     const uint32_t NT = nw64 * 64;
     const uint32_t nK5 = (V + V5_UC - 1) / V5_UC, nbTT5 = (NT + V5_TT - 1) / V5_TT;
     const size_t NG5 = (size_t)nbTT5 * nK5 * V5_WAVES;
     uint32_t* v5_cnt = (uint32_t*)c.b_ecnt.get((size_t)nbTT5 * nK5 * V5_TT * 4);
-    uint32_t* v5_goff = (uint32_t*)c.b_eoff.get((std::max(NG5, NQ6) + 1) * 4);  // (v6: entry offsets per (tile, chunk))
+    uint32_t* v5_goff = (uint32_t*)c.b_eoff.get((NG5 + 1) * 4);
     uint64_t E_ess = 0, E_layout = 0;
-    if (use6) {
-        uint32_t* v6_glen = (uint32_t*)c.b_rlen.get((NQ6 + 1) * 4);
-        HIP_CHECK(hipMemsetAsync(v6_glen, 0, (NQ6 + 1) * 4, st));
-        k_v6_count<<<(unsigned)((NQ6 * 64 + 255) / 256), 256, 0, st>>>(ess, V, nw64, nK6, v6_glen, indeg);
-        HIP_CHECK(hipGetLastError());
-        size_t ta = 0, tc = 0;
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, v6_glen, v5_goff, (int)(NQ6 + 1), st));
-        void* tmp = c.b_scantmp.get(std::max(ta, tc));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, ta, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tc, v6_glen, v5_goff, (int)(NQ6 + 1), st));
-        rb_async(c, MS_TAIL0, cscoff + NT, st);
-        rb_async(c, MS_TAIL1, v5_goff + NQ6, st);
-        HIP_CHECK(hipStreamSynchronize(st));
-        E_ess = rb_get<uint32_t>(c, MS_TAIL0);
-        E_layout = rb_get<uint32_t>(c, MS_TAIL1);
-    } else {
+    {
         uint32_t* v5_glen = (uint32_t*)c.b_rlen.get((NG5 + 1) * 4);
         HIP_CHECK(hipMemsetAsync(v5_cnt, 0, (size_t)nbTT5 * nK5 * V5_TT * 4, st));
         HIP_CHECK(hipMemsetAsync(v5_glen, 0, (NG5 + 1) * 4, st));
@@ -2450,12 +2428,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         float* ent_b = (float*)c.b_entb.get(Eb * 4);
         uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
         HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
-        static_assert(V5_SLACK >= V6_SLACK, "record slack");
         uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
-        if (use6) {
-            k_v6_fill<K><<<(unsigned)((NQ6 * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK6, v5_goff, cscoff,
-                                                                            cscfill, rec, ent_w, ent_u, ent_b, cscent);
-        } else {
+        {
             const size_t nwaves = (size_t)nw64 * nK5;
             k_v5_fill<K><<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK5, v5_cnt,
                                                                                   v5_goff, cscoff, cscfill, rec, ent_w,
@@ -2490,11 +2464,6 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             // after it and shipped while later groups scan (loss rows on a second stream beside the
             // next group's scan were starved of CUs: 24.7 ms vs 20.8)
             const uint32_t ng = interleave ? std::min<uint32_t>(scan_groups, nbS5) : 1u;
-            uint32_t* PMAX = use6 ? (uint32_t*)c.b_pmax.get((size_t)nloc * Vp * 4) : nullptr;
-            if (use6) {  // hits: min into PRED (from PRED_NONE), max into PMAX (from 0)
-                HIP_CHECK(hipMemsetAsync(PRED, 0xFF, (size_t)nloc * Vp * 4, st));
-                HIP_CHECK(hipMemsetAsync(PMAX, 0, (size_t)nloc * Vp * 4, st));
-            }
             for (uint32_t gi = 0; gi < ng; ++gi) {
                 // group bounds on multiples of 8 source blocks: every XCD gets the same number of
                 // blocks per launch (20 blocks = 3/3/3/3/2/2/2/2 ran 33 % long)
@@ -2510,20 +2479,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 };
                 const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                 if (c1 == c0) continue;
-                if (use6) {
-                    const uint32_t nblk = (nw64 + 7) / 8 * ((c1 - c0 + 7) / 8);
-                    tight_v6<<<8u * 64u * ((nblk + 7) / 8), V6_WAVES * 64, 0, st>>>(
-                        DSTs, npad, dsts_bytes, lnodes, nloc, nw64, c1, nK6, c0, v5_goff, rec, PRED, PMAX, Vp, inf_check);
-                    const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);
-                    if (r1 > r0)
-                        k_v6_combine<<<dim3((V + 1023) / 1024, r1 - r0), 256, 0, st>>>(PRED + (size_t)r0 * Vp, PMAX + (size_t)r0 * Vp,
-                                                                                     r1 - r0, V, Vp);
-                } else {
-                    const uint32_t nblk = (nbTT5 + 3) / 4 * ((c1 - c0 + 7) / 8);
-                    tight_v5<<<8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
-                        DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0, v5_goff,
-                        (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
-                }
+                const uint32_t nblk = (nbTT5 + 3) / 4 * ((c1 - c0 + 7) / 8);
+                tight_v5<<<8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                    DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0, v5_goff,
+                    (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
                 HIP_CHECK(hipGetLastError());
                 if (interleave) {
                     const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);
@@ -3985,10 +3944,6 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
             ctx->test_fault = (int)value;
             return SRG_OK;
-        case SRG_OPT_SCAN_KERNEL:
-            if (value != 0 && value != 5 && value != 6) return SRG_ERR_ARG;
-            ctx->scan_kernel = (int)value;
-            return SRG_OK;
         case SRG_OPT_TABLE_POOL_BYTES: {
             if (!(value >= 0.0 && value <= 1e15)) return SRG_ERR_ARG;
             std::lock_guard<std::mutex> pl(ctx->tpool->mu);
@@ -4039,7 +3994,6 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
             break;
         }
         case SRG_OPT_CREATE_MS_RUNTIME: *value = ctx->ms_create_runtime; break;
-        case SRG_OPT_SCAN_KERNEL: *value = ctx->scan_kernel; break;
         case SRG_OPT_CREATE_MS_LIBRARY: *value = ctx->ms_create_lib; break;
         default: return SRG_ERR_ARG;
     }
