@@ -53,6 +53,7 @@ SRG_OPT_TABLE_POOL_BYTES = 35
 SRG_OPT_TABLE_POOL_IDLE_BYTES = 36
 SRG_OPT_CREATE_MS_RUNTIME = 37
 SRG_OPT_CREATE_MS_LIBRARY = 38
+SRG_OPT_FW_XCD_ORDER = 39
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2

@@ -907,7 +907,7 @@ struct LineMap {
     }
 };
 
-// Bulk of pivot L: this rank's stored tiles (triangle indices tiles[0 .. gridDim.x)) except
+// Bulk of pivot L: this rank's stored tiles (triangle indices tiles[0 .. gridDim.x), -1 = none) except
 // those in lines x0, x1 (the pivot's own line, final, and the next pivot's line, updated by the
 // chain).  C in D (row stride ld), operands from line L's buffer.
 // maxI: tiles of block-rows past it have not received their edges yet (the host entry's FW beside
@@ -916,8 +916,10 @@ template <class K, int T, int KC>
 __global__ void __launch_bounds__(256, 3) fw_bulk_lb(K* __restrict__ D, size_t ld, const K* __restrict__ lb, int L,
                                                      int x0, int x1, LineMap lm, const int* __restrict__ tiles,
                                                      int maxI) {
+    const int t = tiles[blockIdx.x];
+    if (t < 0) return;  // (a slot past a short XCD run, routing.hip xcd_tile_order)
     int I, J;
-    tri_tile(lm.nb, tiles[blockIdx.x], I, J);
+    tri_tile(lm.nb, t, I, J);
     if (I == x0 || I == x1 || J == x0 || J == x1 || I > maxI) return;  // whole workgroup
     constexpr size_t TT = (size_t)T * T;
     fw_core<K, T, T, KC>(D + (size_t)I * T * ld + (size_t)J * T, ld, lb + lm.slot(I, L) * TT, I > L,
