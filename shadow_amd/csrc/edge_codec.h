@@ -18,6 +18,14 @@ namespace srg {
 // checks still cover the whole slice then.  Blocks of 1 K edges: a vectorisable narrowing loop,
 // a vectorisable exception-flag loop, then a scan of the flags 8 at a time (a branchy one-pass
 // loop ran the host conversion at 7-9.5 ms for C3 against 5-7 ms for the u16 narrowing).
+// ring stores bypass the cache (the DMA reads the ring; no read-for-ownership of its lines);
+// plain stores under g++ (the CPU round-trip test)
+#if defined(__clang__)
+#define SRG_NT_STORE(v, p) __builtin_nontemporal_store((v), (p))
+#else
+#define SRG_NT_STORE(v, p) (*(p) = (v))
+#endif
+
 inline bool seq_encode_slice(const uint32_t* src, const uint32_t* dst, const uint64_t* lat, uint32_t* hl, size_t a,
                              size_t z, std::vector<uint32_t>& ex, size_t cap, uint32_t& orx, uint64_t& orl) {
     constexpr size_t BLK = 1024;
@@ -29,7 +37,7 @@ inline bool seq_encode_slice(const uint32_t* src, const uint32_t* dst, const uin
         const size_t b1 = b0 + BLK < z ? b0 + BLK : z, nb = b1 - b0;
         for (size_t i = b0; i < b1; ++i) {
             const uint64_t l = lat[i];
-            hl[i] = (uint32_t)l;
+            SRG_NT_STORE((uint32_t)l, &hl[i]);
             ol |= l;
             ox |= src[i] | dst[i];
         }
@@ -62,6 +70,7 @@ inline bool seq_encode_slice(const uint32_t* src, const uint32_t* dst, const uin
     }
     orx |= ox;
     orl |= ol;
+    __builtin_ia32_sfence();  // the non-temporal stores drained before the slot is handed to the DMA
     return !dense;
 }
 
