@@ -2350,7 +2350,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             D, Vp, lnodes, nloc, nodes, n,
             // (an edge of >= INF keys counts as absent: the bound is never above INF, which stays legal)
             (K)std::min<uint64_t>(min_edge_key(P.es.min_lat_inv, P.unit), (uint64_t)KeyOps<K>::INF), P.flags);
-    if (reduce_flag(&P.flags->impossible))
+    // (a simulated rank -- SRG_OPT_SIMULATE_RANK, timing only -- never receives its peers' line
+    // segments, so its table is not a result and the guard does not apply)
+    const bool simulated = c.comm && std::strcmp(c.comm->kind(), "simulated") == 0;
+    if (reduce_flag(&P.flags->impossible) && !simulated)
         fail(SRG_ERR_INTERNAL, "FW produced an impossible table: a used pair's latency is below the smallest edge "
                                "latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
     const uint32_t inf_any = reduce_flag(&P.flags->inf_in_used_row);

@@ -1,6 +1,8 @@
 """The symmetric FW bulk launched in XCD Z-order runs (SRG_OPT_FW_XCD_ORDER = 1, routing.hip
 xcd_tile_order) computes the same closure as triangle order: bit-identical tables through the host
-entry (with and without the FW beside the H2D) and on a simulated rank of a 3-rank group."""
+entry (with and without the FW beside the H2D).  Also: a simulated rank (SRG_OPT_SIMULATE_RANK, a
+timing aid whose table is not a result: no peer data) runs to the end -- the impossible-table guard
+does not apply to it."""
 import numpy as np
 import pytest
 
@@ -28,3 +30,14 @@ def test_xcd_order_matches(V, overlap):
     assert a.stats["path_kind"] == N.SRG_PATH_DENSE_U32
     assert np.array_equal(a.latency_ns, b.latency_ns)
     assert np.array_equal(a.packet_loss.view(np.uint32), b.packet_loss.view(np.uint32))
+
+
+@pytest.mark.parametrize("sim", [2000, 8007])
+def test_simulated_rank_runs(sim):
+    e = synth.atlas_like(2600, seed=2601)
+    r = Router(0)
+    r.set_option(N.SRG_OPT_SIMULATE_RANK, sim)
+    r.set_option(N.SRG_OPT_GATHER_OUTPUT, 0)
+    t = r.compute_shortest_paths(e, list(range(2600)))
+    r.close()
+    assert t.stats["nranks"] == sim // 1000 and t.stats["rank"] == sim % 1000
