@@ -3264,9 +3264,8 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
                     orl |= l;
                     hs[i] = (uint16_t)x;
                     hd[i] = (uint16_t)y;
-                    SRG_NT_STORE((uint32_t)l, &hl[i]);
+                    hl[i] = (uint32_t)l;
                 }
-                __builtin_ia32_sfence();
             }
             if (with_loss) std::memcpy(hb + a, g->packet_loss + e0 + a, (z - a) * 4);  // f32 as is
             if (orl >> 32) bad.store(true, std::memory_order_relaxed);
