@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <deque>
 #include <cstdio>
@@ -2156,12 +2157,22 @@ struct FwOverlap {
             if (I > splitA)  // (only after the H2D: the submitting thread splits every landed row)
                 k_w_split<false><<<dim3((unsigned)(Vp / 64), 2), 256, 0, st>>>(KW, Vp, 0, W, WL, D, (uint32_t)(2 * I));
         if (next > 0 && newA > A) {
-            // the newly complete block-rows (A, newA] catch up in ONE launch over all their tiles;
-            // pivot groups sized for ~3 workgroups per CU, each a K = 128 pg product
+            // the newly complete block-rows (A, newA] catch up in ONE launch over all their tiles,
+            // each workgroup a K = 128 pg product over a group of the pivots run so far.  The
+            // group count minimises waves x (pg + merge): a grid just past the 768 slots (3 per CU)
+            // ran a second, nearly empty wave of full-length workgroups -- rounding ceil(768 /
+            // tiles) groups up did that in most C3 launches (816-918 workgroups).  Host entry
+            // 47.7-48.1 vs 48.1-50.1 ms in alternating runs (profiles/r05/catchup/)
             int tiles = 0;
             for (int I = A + 1; I <= newA; ++I) tiles += nb - I;
-            const int groups = std::max(1, std::min(next, (catchup_wgs + tiles - 1) / tiles));
-            const int pg = (next + groups - 1) / groups;
+            int pg = next;
+            double best = 1e300;
+            for (int g = 1; g <= next; ++g) {
+                const int p = (next + g - 1) / g, gg = (next + p - 1) / p;
+                const double waves = std::ceil((double)tiles * gg / catchup_wgs);
+                const double cost = waves * (p + 0.25);  // (0.25: C load + atomicMin merge, in pivots)
+                if (cost < best - 1e-9) best = cost, pg = p;
+            }
             set_lds(fw_catchup<T>, lb_lds<uint32_t, T, 16>());
             fw_catchup<T><<<dim3(tiles, (next + pg - 1) / pg), 256, lb_lds<uint32_t, T, 16>(), st>>>(
                 D, Vp, fw->lball, (size_t)nb * TT, A + 1, nb, next, pg);
