@@ -8,7 +8,7 @@
 // Layout (all in HBM):
 //   DST [Vt x npad] u32  DST[u][r] = D[nodes[r]][u]  (sources on the fast axis -> lanes)
 //   pair records per (128-target tile, 64-row u-chunk, 16-target wave slice), see tight_v5;
-//   ent_w[e] = W[u][t] (exact key), ent_u[e] = u, ent_b[e] = 1 - loss(u,t) per entry e
+//   ent_w[e] = W[u][t] (exact key), ent_ub[e] = {u, bits of 1 - loss(u,t)} per entry e
 //   csc_off[t] .. csc_off[t+1]: entry indices whose target is t (multi-predecessor slow path)
 // Kernels: k_ess_mask (essential bitmask), k_build_dst, k_v5_count / k_v5_fill (records),
 // tight_v5 (the scan), k_loss_rows (per-row left fold in LDS) and k_loss_round_sparse (the
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) k_v5_count(const unsigned long long* __re
     if ((lane % V5_TW) == 0) glen[((size_t)b * nK + k) * V5_WAVES + tt / V5_TW] = (p + 3) / 4 * 4;
 }
 
-// records rec[e] = (lo | tl << 16, w) for entry e = 2 * pair + slot, plus ent_w / ent_u / ent_b
+// records rec[e] = (lo | tl << 16, w) for entry e = 2 * pair + slot, plus ent_w / ent_ub
 // (k_loss_rows) and the CSC lists (any order: the MULTI fold is a min)
 // K = u64 (the u64-key path): records carry the low 32 bits of w (the scan then works on the
 // low words of the keys, see tight_v5), ent_w the exact key (the loss pass's multi-predecessor
@@ -124,8 +124,7 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ goff,
                                                   const uint32_t* __restrict__ csc_off, uint32_t* __restrict__ csc_fill,
                                                   uint2* __restrict__ rec, K* __restrict__ ent_w,
-                                                  uint32_t* __restrict__ ent_u, float* __restrict__ ent_b,
-                                                  uint32_t* __restrict__ csc_ent) {
+                                                  uint2* __restrict__ ent_ub, uint32_t* __restrict__ csc_ent) {
     const uint32_t lane = threadIdx.x & 63;
     const size_t wv = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
     if (wv >= (size_t)nw64 * nK) return;
@@ -149,24 +148,21 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
         const K w = W[(size_t)u * ld + t];
         rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), (uint32_t)w);  // the pair's target: first slot only
         ent_w[e] = w;
-        ent_u[e] = u;
-        ent_b[e] = __fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]));
+        ent_ub[e] = make_uint2(u, __float_as_uint(__fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]))));
         csc_ent[cbase + atomicAdd(&csc_fill[t], 1u)] = (uint32_t)e;
         ++e;
     }
     if (c & 1u) {  // odd run: a sentinel second slot (w = INF is never tight on a reachable target)
         rec[e] = make_uint2(0u, KeyOps<uint32_t>::INF);
         ent_w[e] = KeyOps<K>::INF;
-        ent_u[e] = 0;
-        ent_b[e] = 1.0f;
+        ent_ub[e] = make_uint2(0u, __float_as_uint(1.0f));
     }
     if (j == V5_TW - 1) {  // the slice's group padding
         const uint32_t total = incl;
         for (size_t q = 2 * ((size_t)pbase + total); q < 2 * (size_t)goff[g + 1]; ++q) {
             rec[q] = make_uint2(0u, KeyOps<uint32_t>::INF);
             ent_w[q] = KeyOps<K>::INF;
-            ent_u[q] = 0;
-            ent_b[q] = 1.0f;
+            ent_ub[q] = make_uint2(0u, __float_as_uint(1.0f));
         }
     }
 }
@@ -309,8 +305,8 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,
                                     size_t npad, const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
-                                    const uint32_t* __restrict__ ent_u, const K* __restrict__ ent_w,
-                                    const float* __restrict__ ent_b, const uint32_t* __restrict__ csc_off,
+                                    const uint2* __restrict__ ent_ub, const K* __restrict__ ent_w,
+                                    const uint32_t* __restrict__ csc_off,
                                     const uint32_t* __restrict__ csc_ent, const float* __restrict__ Lin,
                                     float* __restrict__ Lout, uint32_t* __restrict__ changed_flag) {
     const size_t total = (size_t)n * V;
@@ -326,15 +322,16 @@ __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ld
         } else if (p == PRED_NONE) {
             v = 1.0f;
         } else if (p != PRED_MULTI) {
-            v = fold_loss(Lrow[ent_u[p]], ent_b[p]);
+            const uint2 ub = ent_ub[p];
+            v = fold_loss(Lrow[ub.x], __uint_as_float(ub.y));
         } else {
             const K dst = DST[t * npad + r];
             v = 1.0f;
             for (uint32_t k = csc_off[t]; k < csc_off[t + 1]; ++k) {
                 const uint32_t e = csc_ent[k];
-                const uint32_t u = ent_u[e];
-                if (KeyOps<K>::add(DST[(size_t)u * npad + r], ent_w[e]) != dst) continue;
-                const float cnd = fold_loss(Lrow[u], ent_b[e]);
+                const uint2 ub = ent_ub[e];
+                if (KeyOps<K>::add(DST[(size_t)ub.x * npad + r], ent_w[e]) != dst) continue;
+                const float cnd = fold_loss(Lrow[ub.x], __uint_as_float(ub.y));
                 v = cnd < v ? cnd : v;
             }
         }
@@ -363,8 +360,7 @@ constexpr size_t loss_rows_lds(uint32_t V) { return (size_t)V * 12 + LM_T * (4 +
 template <class K>
 __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__ PRED, size_t ldp, uint32_t V,
                                                      const uint32_t* __restrict__ nodes, uint32_t n,
-                                                     const uint32_t* __restrict__ ent_u,
-                                                     const float* __restrict__ ent_b, const K* __restrict__ ent_w,
+                                                     const uint2* __restrict__ ent_ub, const K* __restrict__ ent_w,
                                                      const K* __restrict__ DST, size_t npad,
                                                      const uint32_t* __restrict__ csc_off,
                                                      const uint32_t* __restrict__ csc_ent,
@@ -404,8 +400,9 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
                 u = U_MLIST + i;
             }
         } else {
-            u = ent_u[p];
-            bb = ent_b[p];
+            const uint2 ub = ent_ub[p];  // (one 8-B gather per target: u and 1 - loss together)
+            u = ub.x;
+            bb = __uint_as_float(ub.y);
         }
         U[t] = u;
         Bf[t] = bb;
@@ -418,12 +415,13 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
         const K dst = DST[(size_t)t * npad + r];
         for (uint32_t k = csc_off[t] + threadIdx.x; k < csc_off[t + 1]; k += blockDim.x) {
             const uint32_t e = csc_ent[k];
-            const uint32_t uu = ent_u[e];
+            const uint2 ub = ent_ub[e];
+            const uint32_t uu = ub.x;
             if (KeyOps<K>::add(DST[(size_t)uu * npad + r], ent_w[e]) != dst) continue;
             const uint32_t j = atomicAdd(&m_n[i], 1u);
             if (j < LM_E) {
                 m_u[i * LM_E + j] = uu;
-                m_b[i * LM_E + j] = ent_b[e];
+                m_b[i * LM_E + j] = __uint_as_float(ub.y);
             }
         }
     }
@@ -446,9 +444,10 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
                     const K dst = DST[(size_t)t * npad + r];
                     for (uint32_t k = csc_off[t]; k < csc_off[t + 1]; ++k) {
                         const uint32_t e = csc_ent[k];
-                        const uint32_t uu = ent_u[e];
+                        const uint2 ub = ent_ub[e];
+                        const uint32_t uu = ub.x;
                         if (KeyOps<K>::add(DST[(size_t)uu * npad + r], ent_w[e]) != dst) continue;
-                        const float cnd = fold_loss(L[uu], ent_b[e]);
+                        const float cnd = fold_loss(L[uu], __uint_as_float(ub.y));
                         v = cnd < v ? cnd : v;
                     }
                 } else {
