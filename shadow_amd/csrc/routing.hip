@@ -2501,7 +2501,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // essential bitmask (V^2/8 bytes): every rank holds the whole D and W, so each builds all of it
     const uint32_t nw64 = (V + 63) / 64;
     unsigned long long* ess = (unsigned long long*)c.b_ess.get((size_t)V * nw64 * 8);
-    k_ess_mask<K><<<grid_for((size_t)V * nw64 * 64, 256 * 64), 256, 0, st>>>(W, D, Vp, V, 0u, V, nw64, ess);
+    k_ess_mask<K><<<V, 256, 0, st>>>(W, D, Vp, V, 0u, V, nw64, ess);
     uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
     uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
     HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
@@ -2544,16 +2544,16 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     if (sparse) {
         scan_kind = SRG_SCAN_SPARSE;
         const size_t Eb = E_layout + 256;
-        uint32_t* cscfill = (uint32_t*)c.b_cscfill.get((size_t)nw64 * 64 * 4);
+        uint32_t* cscpos = (uint32_t*)c.b_cscfill.get((size_t)nbTT5 * nK5 * V5_TT * 4);
         K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
         uint2* ent_ub = (uint2*)c.b_grpe.get(Eb * 8);  // {u, 1 - loss bits}: one gather in the loss pass
         uint32_t* cscent = (uint32_t*)c.b_cscent.get(std::max<uint64_t>(E_ess, 1) * 4);
-        HIP_CHECK(hipMemsetAsync(cscfill, 0, (size_t)nw64 * 64 * 4, st));
+        k_v5_cscpos<<<(NT + 255) / 256, 256, 0, st>>>(v5_cnt, cscoff, NT, nK5, cscpos);
         uint2* rec = (uint2*)c.b_entkey.get((Eb + V5_SLACK) * 8);
         {
             const size_t nwaves = (size_t)nw64 * nK5;
             k_v5_fill<K><<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, W, WL, Vp, V, nw64, nK5, v5_cnt,
-                                                                                  v5_goff, cscoff, cscfill, rec, ent_w,
+                                                                                  v5_goff, cscpos, rec, ent_w,
                                                                                   ent_ub, cscent);
         }
         HIP_CHECK(hipGetLastError());

@@ -27,24 +27,51 @@ namespace srg {
 // ESS[u][w64] (u64): bit `lane` set <=> edge u -> t = 64*w64 + lane is essential.  Computed by
 // the owner of row u (its rows of D are the only ones it has in the multi-GPU layout) and
 // then all-gathered: V^2/8 bytes instead of the V^2 keys of D.
+// One workgroup per row u (blockIdx.x = u - u0).  u32 keys: each lane reads 4 targets of W and of D
+// as 16-B loads (a wave covers 4 words), its nibble ORed into the word of its 16-lane group by a
+// 4-step butterfly; u64 keys: one target per lane and a ballot per word.  (A grid-stride loop over
+// (u, word) pairs with a 64-bit division per word ran at ~1.6 TB/s, one word per wave at ~2.2.)
 template <class K>
 __global__ void __launch_bounds__(256) k_ess_mask(const K* __restrict__ W, const K* __restrict__ D, size_t ld,
                                                    uint32_t V, uint32_t u0, uint32_t u1, uint32_t nw64,
                                                    unsigned long long* __restrict__ ess) {
-    const uint32_t lane = threadIdx.x & 63;
-    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
-    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
-    const size_t total = (size_t)nw64 * (u1 - u0);
-    for (size_t q = wave; q < total; q += nwaves) {
-        const uint32_t u = u0 + (uint32_t)(q / nw64), w64 = (uint32_t)(q % nw64);
-        const uint32_t t = w64 * 64 + lane;
-        bool e = false;
-        if (t < V && t != u) {
-            const K w = W[(size_t)u * ld + t];
-            e = (w != KeyOps<K>::INF) && (w == D[(size_t)u * ld + t]);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t u = u0 + blockIdx.x;
+    if (u >= u1) return;
+    const K* Wu = W + (size_t)u * ld;
+    const K* Du = D + (size_t)u * ld;
+    unsigned long long* eu = ess + (size_t)u * nw64;
+    if constexpr (sizeof(K) == 4) {
+        // (ld is a multiple of 64 keys: a 16-B load below ld stays inside the padded row)
+        for (uint32_t w0 = wave * 4; w0 < nw64; w0 += 16) {
+            const uint32_t t = w0 * 64 + lane * 4;
+            uint4 a = make_uint4(0u, 0u, 0u, 0u), d = make_uint4(1u, 1u, 1u, 1u);
+            if (t < ld) {  // (the words past nw64 in this step: nothing read past the row)
+                a = *reinterpret_cast<const uint4*>(Wu + t);
+                d = *reinterpret_cast<const uint4*>(Du + t);
+            }
+            const uint32_t av[4] = {a.x, a.y, a.z, a.w}, dv[4] = {d.x, d.y, d.z, d.w};
+            unsigned long long nib = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                nib |= (unsigned long long)(t + j < V && t + j != u && av[j] != KeyOps<K>::INF && av[j] == dv[j]) << j;
+            unsigned long long v = nib << (4 * (lane & 15));
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) v |= __shfl_xor(v, o, 64);
+            const uint32_t w = w0 + (lane >> 4);
+            if ((lane & 15) == 0 && w < nw64) eu[w] = v;
         }
-        const unsigned long long m = __ballot(e);
-        if (lane == 0) ess[(size_t)u * nw64 + w64] = m;
+    } else {
+        for (uint32_t w0 = wave; w0 < nw64; w0 += 4) {
+            const uint32_t t = w0 * 64 + lane;
+            bool e = false;
+            if (t < V && t != u) {
+                const K w = Wu[t];
+                e = (w != KeyOps<K>::INF) && (w == Du[t]);
+            }
+            const unsigned long long m = __ballot(e);
+            if (lane == 0) eu[w0] = m;
+        }
     }
 }
 
@@ -112,6 +139,22 @@ __global__ void __launch_bounds__(256) k_v5_count(const unsigned long long* __re
     if ((lane % V5_TW) == 0) glen[((size_t)b * nK + k) * V5_WAVES + tt / V5_TW] = (p + 3) / 4 * 4;
 }
 
+// CSC positions without atomics: thread t walks the chunks k in order, pos[b][k][tt] = csc_off[t] +
+// the entries of t in chunks before k (cnt from k_v5_count); k_v5_fill then stores each target's
+// entries at consecutive positions (an atomicAdd per entry held every fill wave on its return)
+__global__ void __launch_bounds__(256) k_v5_cscpos(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ csc_off,
+                                                    uint32_t NT, uint32_t nK, uint32_t* __restrict__ pos) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NT) return;
+    const uint32_t b = t / V5_TT, tt = t % V5_TT;
+    uint32_t run = csc_off[t];
+    for (uint32_t k = 0; k < nK; ++k) {
+        const size_t i = ((size_t)b * nK + k) * V5_TT + tt;
+        pos[i] = run;
+        run += cnt[i];
+    }
+}
+
 // records rec[e] = (lo | tl << 16, w) for entry e = 2 * pair + slot, plus ent_w / ent_ub
 // (k_loss_rows) and the CSC lists (any order: the MULTI fold is a min)
 // K = u64 (the u64-key path): records carry the low 32 bits of w (the scan then works on the
@@ -122,7 +165,7 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
                                                   const K* __restrict__ W, const uint32_t* __restrict__ WL,
                                                   size_t ld, uint32_t V, uint32_t nw64, uint32_t nK,
                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ goff,
-                                                  const uint32_t* __restrict__ csc_off, uint32_t* __restrict__ csc_fill,
+                                                  const uint32_t* __restrict__ csc_pos,
                                                   uint2* __restrict__ rec, K* __restrict__ ent_w,
                                                   uint2* __restrict__ ent_ub, uint32_t* __restrict__ csc_ent) {
     const uint32_t lane = threadIdx.x & 63;
@@ -142,14 +185,14 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
     const uint32_t pbase = goff[g];
     size_t e = 2 * ((size_t)pbase + incl - p);
     const uint32_t u0 = k * V5_UC, u1 = min(V, u0 + V5_UC);
-    const uint32_t cbase = t < V ? csc_off[t] : 0u;
+    uint32_t cp = csc_pos[((size_t)b * nK + k) * V5_TT + tt];  // (k_v5_cscpos)
     for (uint32_t u = u0; u < u1; ++u) {
         if (!((ess[(size_t)u * nw64 + w64] >> lane) & 1ull)) continue;
         const K w = W[(size_t)u * ld + t];
         rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), (uint32_t)w);  // the pair's target: first slot only
         ent_w[e] = w;
         ent_ub[e] = make_uint2(u, __float_as_uint(__fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]))));
-        csc_ent[cbase + atomicAdd(&csc_fill[t], 1u)] = (uint32_t)e;
+        csc_ent[cp++] = (uint32_t)e;
         ++e;
     }
     if (c & 1u) {  // odd run: a sentinel second slot (w = INF is never tight on a reachable target)
