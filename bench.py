@@ -275,8 +275,7 @@ def apply_options(router, args):
                       ("h2d_codec", "H2D_CODEC"),
                       ("late_loss", "LATE_LOSS"), ("edge_shard", "EDGE_SHARD"), ("scan_groups", "SCAN_GROUPS"),
                       ("loss_chunks", "LOSS_CHUNKS"), ("d2h_mode", "D2H_MODE"), ("fw_line_split", "FW_LINE_SPLIT"),
-                      ("fw_step", "FW_STEP"), ("fw_overlap", "FW_OVERLAP"), ("fw_xcd_order", "FW_XCD_ORDER"),
-                      ("sparse_hubs", "SPARSE_HUBS")):
+                      ("fw_step", "FW_STEP"), ("fw_overlap", "FW_OVERLAP"), ("fw_xcd_order", "FW_XCD_ORDER")):
         v = getattr(args, flag)
         if v is not None:
             router.set_option(getattr(N, "SRG_OPT_" + opt), v)
@@ -563,7 +562,6 @@ def main():
                     help="sparse: bucket width = max edge latency / this (0 = plain Bellman-Ford)")
     ap.add_argument("--fw-symmetric", type=int, default=None, help="dense u32: 0 = general FW on undirected graphs too")
     ap.add_argument("--fw-xcd-order", type=int, default=None, help="symmetric FW bulk: 1 = Z-order runs per XCD")
-    ap.add_argument("--sparse-hubs", type=int, default=None, help="sparse: hub rows bounding the initial labels (0/128/256/384/512)")
     ap.add_argument("--d2h-mode", type=int, default=None, help="host entry D2H engine: 1 = SDMA (default), 0 = hipMemcpyAsync")
     ap.add_argument("--h2d-codec", type=int, default=None, help="host entry: 1 = narrowed edge list over PCIe (default), 0 = plain")
     ap.add_argument("--late-loss", type=int, default=None,

@@ -112,8 +112,7 @@ typedef struct srg_stats {
                                    (its certification passed), 0 = the build ran FW after the H2D   */
     int32_t d2h_key_rows;       /* host entry, u64 output: 1 = the latency rows crossed PCIe as the build's
                                    u32 keys (4 B instead of 8 per pair) and were widened on the host  */
-    int32_t sparse_hubs;        /* sparse path: hub rows that bounded the initial labels (SRG_OPT_SPARSE_HUBS;
-                                   0 = none: off, directed, wide labels, or no room for the bounds)   */
+    int32_t reserved0;
     double ms_key_widen;        /* its widening + key-copy wall time on the helper thread (overlapped
                                    with the loss pass; the part after the kernels is in ms_d2h)     */
 } srg_stats;
@@ -216,12 +215,6 @@ void srg_destroy(srg_ctx* ctx);
                                      * Z-order runs, one list per pivot (each XCD a compact block of the triangle,
                                      * its line-buffer operands L2-resident: C3 bulk HBM traffic 1.38x -> 1.12x of
                                      * the C tiles); 0 = triangle order (consecutive tiles round-robin) */
-#define SRG_OPT_SPARSE_HUBS 40       /* sparse path, undirected graphs, u32 labels: number of hub vertices (the
-                                     * highest-degree ones; 0 or a multiple of 128 up to 512) whose exact
-                                     * latency rows bound every batch's initial labels from above
-                                     * (min over hubs h of D[h][s] + D[h][v], loss 1.0), so the sweeps start
-                                     * near the fixpoint.  Skipped when the bound table (V x sources x 4 B)
-                                     * would not fit a quarter of the free HBM. */
 int srg_set_option(srg_ctx* ctx, int option, double value);
 /* current value of an option (SRG_OK), or SRG_ERR_ARG for an unknown option */
 int srg_get_option(srg_ctx* ctx, int option, double* value);

@@ -54,7 +54,6 @@ SRG_OPT_TABLE_POOL_IDLE_BYTES = 36
 SRG_OPT_CREATE_MS_RUNTIME = 37
 SRG_OPT_CREATE_MS_LIBRARY = 38
 SRG_OPT_FW_XCD_ORDER = 39
-SRG_OPT_SPARSE_HUBS = 40
 SRG_ALGO_AUTO = 0
 SRG_ALGO_DENSE = 1
 SRG_ALGO_SPARSE = 2
@@ -141,7 +140,7 @@ class Stats(ctypes.Structure):
         ("fw_overlap_pivots", ctypes.c_int32),
         ("fw_overlap_kept", ctypes.c_int32),
         ("d2h_key_rows", ctypes.c_int32),
-        ("sparse_hubs", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
         ("ms_key_widen", ctypes.c_double),
     ]
 

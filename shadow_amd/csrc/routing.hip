@@ -853,21 +853,18 @@ struct srg_ctx {
     DevBuf b_odiag;
     int fw_overlap = 1;                 // host entry: FW starts while the edge list arrives (SRG_OPT_FW_OVERLAP)
     int fw_xcd_order = 1;               // symmetric FW bulk: tiles dealt to the XCDs in Z-order runs (SRG_OPT_FW_XCD_ORDER)
-    int sparse_hubs = 0;                // sparse: hub rows bounding the initial labels (SRG_OPT_SPARSE_HUBS)
     int test_fault = 0;                 // TEST HOOK (SRG_OPT_TEST_FAULT): 1 = zero D after FW, 2 = stale FW sync words
     std::shared_ptr<TablePool> tpool = std::make_shared<TablePool>();  // RoutingInfo's pinned tables
     double ms_create_runtime = 0, ms_create_lib = 0;  // srg_create: HIP runtime / device init vs the library's own
     // packet-event batches (events.hip.h): key / index ping-pong buffers, tile histograms
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
-    DevBuf b_hubH, b_hubHs, b_hubUB, b_hubinf;  // sparse hub bounds: hub rows, the lanes' rows, UBT, a HUB_INF row
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
                           &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
                           &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc, &b_odiag,
-                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered,
-                          &b_hubH, &b_hubHs, &b_hubUB, &b_hubinf})
+                          &b_ek0, &b_ek1, &b_eh0, &b_eh1, &b_ei0, &b_ei1, &b_ehist, &b_eoffs, &b_ered})
             b->release();
         delete comm;
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
@@ -2854,57 +2851,6 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     HIP_CHECK(hipGetLastError());
     const double ms_build = tm.lap();
 
-    // hub bounds (SRG_OPT_SPARSE_HUBS, sparse.hip.h): exact latency rows of the k highest-degree
-    // vertices (in-place Bellman-Ford sweeps over all vertices, 64 hubs per wave), then
-    // UBT[v][lane] = min over hubs of D[h][v] + D[h][src(lane)] for every batch lane (one min-plus
-    // product on the FW's pair-packed core) -- the batches' initial labels
-    const uint32_t* d_ubt = nullptr;
-    size_t ldu = 0;
-    int hub_sweeps = 0;
-    if (c.sparse_hubs > 0 && !wide && !g.directed && nbatch && P.max_key < HUB_INF && V >= 2u * (uint32_t)c.sparse_hubs) {
-        const uint32_t k = (uint32_t)c.sparse_hubs;
-        const size_t Vp = ((size_t)V + 127) / 128 * 128, R = ((size_t)nbatch * 64 + 127) / 128 * 128;
-        size_t fb = 0, tb2 = 0;
-        HIP_CHECK(hipMemGetInfo(&fb, &tb2));
-        if (Vp * R * 4 <= fb / 4) {
-            std::vector<uint32_t> hv(V);
-            for (uint32_t v = 0; v < V; ++v) hv[v] = v;
-            std::partial_sort(hv.begin(), hv.begin() + k, hv.end(), [&](uint32_t x, uint32_t y) {
-                const uint32_t dx = h_off[x + 1] - h_off[x], dy = h_off[y + 1] - h_off[y];
-                return dx != dy ? dx > dy : x < y;
-            });
-            uint32_t* H = (uint32_t*)c.b_hubH.get(Vp * k * 4);
-            k_fill<uint32_t><<<grid_for(Vp * k), kThreads, 0, st>>>(H, Vp * k, HUB_INF);
-            uint32_t* d_hubs = (uint32_t*)c.b_hubinf.get(128 * 4 + (size_t)k * 4) + 128;
-            HIP_CHECK(hipMemcpyAsync(d_hubs, hv.data(), (size_t)k * 4, hipMemcpyHostToDevice, st));
-            k_hub_seed<<<(k + 255) / 256, 256, 0, st>>>(H, k, d_hubs);
-            uint32_t* hflag = fl + 8;
-            const unsigned sgrid = (unsigned)(((size_t)V * (k / 64) * 64 + 255) / 256);
-            for (;;) {
-                HIP_CHECK(hipMemsetAsync(hflag, 0, 4, st));
-                k_hub_sweep<<<sgrid, 256, 0, st>>>(off, in_src, in_w, V, k, H, hflag);
-                HIP_CHECK(hipGetLastError());
-                ++hub_sweeps;
-                rb_async(c, MS_CHANGED, hflag, st);
-                HIP_CHECK(hipStreamSynchronize(st));
-                if (!rb_get<uint32_t>(c, MS_CHANGED)) break;
-                if (hub_sweeps > (int)V + 1) fail(SRG_ERR_INTERNAL, "hub sweeps did not converge");
-            }
-            uint32_t* Hs = (uint32_t*)c.b_hubHs.get(R * k * 4);
-            k_hub_gather<<<grid_for(R * k), kThreads, 0, st>>>(H, k, d_bsrc, nbatch * 64, (uint32_t)R, Hs);
-            uint32_t* infrow = (uint32_t*)c.b_hubinf.p;
-            k_fill<uint32_t><<<1, 128, 0, st>>>(infrow, 128, HUB_INF);
-            uint32_t* UBT = (uint32_t*)c.b_hubUB.get(Vp * R * 4);
-            set_lds(k_hub_ub, lb_lds<uint32_t, 128, 16>());
-            k_hub_ub<<<dim3((unsigned)(R / 128), (unsigned)(Vp / 128)), 256, lb_lds<uint32_t, 128, 16>(), st>>>(
-                H, Hs, k, infrow, UBT, R);
-            HIP_CHECK(hipGetLastError());
-            d_ubt = UBT;
-            ldu = R;
-        }
-    }
-    const double ms_hubs = tm.lap();
-
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
     // wide labels take the 128-VGPR budget: one workgroup per CU
@@ -2933,7 +2879,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
                      selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, gb, c.kout_key, c.kout_diag,
-                     in_w64, min_edge_key(P.es.min_lat_inv, P.unit), d_ubt, ldu};
+                     in_w64, min_edge_key(P.es.min_lat_inv, P.unit)};
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
@@ -2962,8 +2908,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                                "smallest edge latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
     if (std::getenv("SRG_DEBUG_SPARSE")) {
         const unsigned long long ev = (unsigned long long)hfl[2] | (unsigned long long)hfl[3] << 32;
-        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu, hubs %d (%d sweeps, %.2f ms)\n",
-                     nbatch, grid, hfl[1], ev, d_ubt ? c.sparse_hubs : 0, hub_sweeps, ms_hubs);
+        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu\n", nbatch, grid,
+                     hfl[1], ev);
     }
     if (hfl[0]) {
         // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
@@ -2994,8 +2940,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         stats->prof_relaxations += nloc;  // sparse: sources routed by the profiled launch
     }
     if (stats) {
-        stats->ms_build += ms_build + ms_hubs;
-        stats->sparse_hubs = d_ubt ? c.sparse_hubs : 0;
+        stats->ms_build += ms_build;
         stats->ms_fw += ms_sssp;
         stats->ms_exchange += ms_exchange;
         stats->path_kind = wide ? SRG_PATH_SPARSE_U64 : SRG_PATH_SPARSE_U32;
@@ -4124,10 +4069,6 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (value != 0 && value != 1) return SRG_ERR_ARG;
             ctx->fw_xcd_order = (int)value;
             return SRG_OK;
-        case SRG_OPT_SPARSE_HUBS:
-            if (!(value >= 0 && value <= 512) || (int)value != value || (int)value % 128) return SRG_ERR_ARG;
-            ctx->sparse_hubs = (int)value;
-            return SRG_OK;
         case SRG_OPT_TABLE_POOL_BYTES: {
             if (!(value >= 0.0 && value <= 1e15)) return SRG_ERR_ARG;
             std::lock_guard<std::mutex> pl(ctx->tpool->mu);
@@ -4179,7 +4120,6 @@ int srg_get_option(srg_ctx* ctx, int option, double* value) {
         }
         case SRG_OPT_CREATE_MS_RUNTIME: *value = ctx->ms_create_runtime; break;
         case SRG_OPT_FW_XCD_ORDER: *value = ctx->fw_xcd_order; break;
-        case SRG_OPT_SPARSE_HUBS: *value = ctx->sparse_hubs; break;
         case SRG_OPT_CREATE_MS_LIBRARY: *value = ctx->ms_create_lib; break;
         default: return SRG_ERR_ARG;
     }

@@ -196,84 +196,7 @@ struct SparseArgs {
     const uint64_t* in_w64;      // wide labels: u64 arc keys (`slots` then holds 16-byte labels)
     uint64_t min_key;            // smallest arc key: a used off-diagonal latency below it is impossible
                                  // (guards.h) -> flags[6]
-    const uint32_t* ubt = nullptr;  // hub bounds (k_hub_ub): UBT[v][bt * 64 + lane] >= the batch lane's latency
-                                    // key of v (>= HUB_INF: no bound); null = labels start at INF
-    size_t ldu = 0;
 };
-
-// ---- hub bounds (SRG_OPT_SPARSE_HUBS) ---------------------------------------------------------
-// Any labels that start at or above the fixpoint reach it: every relaxation keeps label >= the true
-// lexicographic label (PathProperties::add is monotone in both fields), and once a sweep has
-// evaluated every vertex from every in-arc, the usual induction along the tight DAG applies.  For
-// an undirected graph D[s][v] <= D[s][h] + D[h][v] for any hub h, so (min over hubs of that, loss
-// 1.0) is such a start; from it the sweeps only correct what the hubs did not get right (C4: label
-// changes per vertex-lane 2.7 -> 0.04 with 256 hubs in tools/sparse_sim.cpp).  Hub latency keys
-// are clamped at HUB_INF = 2^31 - 1, so a bound is a sum below 2^32 - 1 and the host only uses hubs
-// when every arc key is below 2^31 (a bound plus an arc then never saturates the u32 label).
-constexpr uint32_t HUB_INF = 0x7FFFFFFFu;
-
-// One in-place Bellman-Ford sweep of the hub rows H [V][k] (k hubs, multiple of 64; column j = hub
-// j's latency keys, HUB_INF = not reached yet): a wave per (vertex v, 64-hub chunk), lane = hub,
-// the min over v's in-arcs of H[u] + w.  *changed |= 1 if some label dropped; the host sweeps until
-// a sweep changes nothing (in place: a sweep may already use labels lowered earlier in it).
-__global__ void __launch_bounds__(256) k_hub_sweep(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
-                                                   const uint32_t* __restrict__ in_w, uint32_t V, uint32_t k,
-                                                   uint32_t* __restrict__ H, uint32_t* __restrict__ changed) {
-    const uint32_t lane = threadIdx.x & 63, nch = k / 64;
-    const size_t wv = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
-    if (wv >= (size_t)V * nch) return;  // whole wave
-    const uint32_t v = (uint32_t)(wv / nch), c = (uint32_t)(wv % nch);
-    const uint32_t* col = H + c * 64 + lane;
-    const uint32_t old = col[(size_t)v * k];
-    uint32_t best = old;
-    const uint32_t lo = in_off[v], hi = in_off[v + 1];
-    uint32_t a = lo;
-    for (; a + 4 <= hi; a += 4) {  // four rows in flight
-        uint32_t x[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = col[(size_t)in_src[a + q] * k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) best = min(best, min(__builtin_elementwise_add_sat(x[q], in_w[a + q]), HUB_INF));
-    }
-    for (; a < hi; ++a) best = min(best, min(__builtin_elementwise_add_sat(col[(size_t)in_src[a] * k], in_w[a]), HUB_INF));
-    const bool dropped = best < old;
-    if (dropped) H[(size_t)v * k + c * 64 + lane] = best;
-    if (__ballot(dropped) && lane == 0) atomicOr(changed, 1u);
-}
-
-// H[hubs[j]][j] = 0: each hub's own entry
-__global__ void k_hub_seed(uint32_t* __restrict__ H, uint32_t k, const uint32_t* __restrict__ hubs) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < k) H[(size_t)hubs[j] * k + j] = 0u;
-}
-
-// Hs[r][0..k) = H[src[r]][0..k) for the rows r < nrows (the batch lanes' sources), HUB_INF past them
-__global__ void __launch_bounds__(256) k_hub_gather(const uint32_t* __restrict__ H, uint32_t k, const uint32_t* __restrict__ src,
-                                                    uint32_t nsrc, uint32_t nrows, uint32_t* __restrict__ Hs) {
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)nrows * k; i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t r = (uint32_t)(i / k), j = (uint32_t)(i % k);
-        Hs[i] = r < nsrc ? H[(size_t)src[r] * k + j] : HUB_INF;
-    }
-}
-
-// UBT [Vp][R] (R = padded batch lanes): UBT[v][r] = min over hubs of H[v][h] + Hs[r][h], one 128 x 128
-// tile per workgroup (grid R/128 x Vp/128), the FW bulk's pair-packed min-plus core over k in chunks
-// of 128 (hub keys <= 2^31 - 1: no sum wraps).  The first chunk starts from a HUB_INF row (row
-// stride 0) and only writes; later chunks fold into the stored tile.
-__global__ void __launch_bounds__(256, 3) k_hub_ub(const uint32_t* __restrict__ H, const uint32_t* __restrict__ Hs, uint32_t k,
-                                                   const uint32_t* __restrict__ infrow, uint32_t* __restrict__ UBT, size_t ldu) {
-    const uint32_t rb = blockIdx.x, vb = blockIdx.y;
-    uint32_t* C = UBT + (size_t)vb * 128 * ldu + (size_t)rb * 128;
-    const uint32_t* A = H + (size_t)vb * 128 * k;
-    const uint32_t* B = Hs + (size_t)rb * 128 * k;
-    fw_core_lb_e<128, 128, 16, false>(const_cast<uint32_t*>(infrow), 0, A, false, B, false, k, [&](int r, int cc, uint64_t bits) {
-        *reinterpret_cast<uint64_t*>(C + (size_t)r * ldu + cc) = bits;
-    });
-    for (uint32_t k0 = 128; k0 < k; k0 += 128) {
-        __syncthreads();  // (the chunk's stores are re-read by the threads that wrote them)
-        fw_core_lb<128, 128, 16>(C, ldu, A + k0, false, B + k0, false, k, nullptr, 0);
-    }
-}
 
 // a vertex whose label dropped in some lanes is pushed now if some dropped lane's new latency is
 // below the bucket bound (requiring every dropped lane below it was measured slower)
@@ -336,29 +259,11 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
         __syncthreads();
         if (bt >= a.nbatch) break;
         const uint32_t my_src = a.batch_src[bt * 64 + lane];
-        // init: labels INF except the sources; changed = the sources; marks = their out-neighbours.
-        // With hub bounds (a.ubt): labels (bound, loss 1.0), and every vertex counts as changed and
-        // marked, so the first sweep evaluates every vertex from every in-arc.
-        const bool hub = !LB::wide && a.ubt != nullptr;
-        if constexpr (!LB::wide) {
-            if (hub) {
-                const uint32_t* ub = a.ubt + (size_t)bt * 64 + lane;
-                for (uint32_t v = wave; v < V; v += SP_WAVES) {
-                    const uint32_t b = ub[(size_t)v * a.ldu];
-                    lab.st((size_t)v * 64 + lane, (v == my_src) ? LB::zero()
-                                                  : b < HUB_INF ? ((unsigned long long)b << 32) | 0x3F800000ull  // 1.0f
-                                                                : LB::inf());
-                }
-            }
-        }
-        if (!hub)
-            for (uint32_t v = wave; v < V; v += SP_WAVES)
-                lab.st((size_t)v * 64 + lane, (v == my_src) ? LB::zero() : LB::inf());
-        auto all_v = [&](uint32_t w) {  // window w's vertices < V
-            return (w + 1 < nw || V % 64 == 0) ? ~0ull : (1ull << (V % 64)) - 1;
-        };
+        // init: labels INF except the sources; changed = the sources; marks = their out-neighbours
+        for (uint32_t v = wave; v < V; v += SP_WAVES)
+            lab.st((size_t)v * 64 + lane, (v == my_src) ? LB::zero() : LB::inf());
         for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
-            fprev[w] = hub ? all_v(w) : 0;
+            fprev[w] = 0;
             fcur[w] = 0;
             mark[w] = 0;
             mnext[w] = 0;
@@ -380,7 +285,7 @@ __global__ void __launch_bounds__(SP_THREADS, WPE) k_sparse_bf(SparseArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
-            mark[w] = hub ? all_v(w) : mnext[w];
+            mark[w] = mnext[w];
             mnext[w] = 0;
         }
         __syncthreads();
