@@ -208,9 +208,11 @@ void srg_destroy(srg_ctx* ctx);
                                      * them, so the next build skips the prefault + page-locking.  Bytes of idle
                                      * tables the pool keeps (default 8 GiB; 0 = free them at once) */
 #define SRG_OPT_TABLE_POOL_IDLE_BYTES 36  /* read-only: bytes of idle tables the pool holds now */
-#define SRG_OPT_CREATE_MS_RUNTIME 37  /* read-only: srg_create's HIP-runtime part (device count, device context;
-                                      * the first context of a process pays the runtime's initialisation) */
-#define SRG_OPT_CREATE_MS_LIBRARY 38  /* read-only: srg_create's own part (streams, mailbox, SDMA agents, events) */
+#define SRG_OPT_CREATE_MS_RUNTIME 37  /* read-only: srg_create's HIP-runtime part (device count, device context,
+                                      * the first stream, where the runtime initialises the device: the first
+                                      * context of a process pays the runtime's initialisation) */
+#define SRG_OPT_CREATE_MS_LIBRARY 38  /* read-only: srg_create's own part (three more streams, mailbox, SDMA
+                                      * agents, events) */
 #define SRG_OPT_FW_XCD_ORDER 39      /* symmetric FW bulk launch order: 1 (default) = the tiles dealt to the 8 XCDs as
                                      * Z-order runs, one list per pivot (each XCD a compact block of the triangle,
                                      * its line-buffer operands L2-resident: C3 bulk HBM traffic 1.38x -> 1.12x of

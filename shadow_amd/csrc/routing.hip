@@ -3939,9 +3939,13 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipSetDevice(device));
         HIP_CHECK(hipFree(nullptr));  // (the device's runtime context, if this process has none yet)
         lap("hipSetDevice");
+        // the first stream is where the runtime initialises the device for this process (80-145 ms
+        // on the boxes, the next streams ~5 ms each; creating the four from four threads at once took
+        // as long, profiles/r05/create/): counted as the runtime's part
+        HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        lap("stream main");
         c->ms_create_runtime = ms_since(tcreate);
         const auto tlib = std::chrono::steady_clock::now();
-        HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         // the FW lookahead chain (pivot close, row/col panels) is latency-critical: its workgroups
         // should be dispatched ahead of the bulk phase-3 tiles
         int prio_lo = 0, prio_hi = 0;
@@ -3949,7 +3953,7 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         HIP_CHECK(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
-        lap("streams");
+        lap("streams aux, comm, d2h");
         HIP_CHECK(hipHostMalloc((void**)&c->hbox, 64 * kMailSlots, hipHostMallocDefault));
         lap("mailbox");
         c->sdma.init(device);  // SDMA engine for the host entry's early D2H (else hipMemcpyAsync)
