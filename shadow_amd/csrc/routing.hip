@@ -455,11 +455,12 @@ __global__ void __launch_bounds__(256) k_wrap_edges(uint64_t E, const uint32_t* 
     if (__ballot(winf) && (threadIdx.x & 63) == 0) atomicOr(&flags->wrap_inf, 1u);
 }
 
+// (stride 2: the packed {u, 1 - loss} PRED rows of tight_v5<true>, marker in the first word)
 __global__ void __launch_bounds__(256) k_count_multi(const uint32_t* __restrict__ PRED, uint32_t n, uint32_t V,
-                                                     size_t ld, unsigned long long* out) {
-    const uint32_t* row = PRED + (size_t)blockIdx.x * ld;
+                                                     size_t ld, unsigned long long* out, uint32_t stride = 1) {
+    const uint32_t* row = PRED + (size_t)blockIdx.x * ld * stride;
     unsigned long long c = 0;
-    for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) c += row[t] == PRED_MULTI;
+    for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) c += row[(size_t)t * stride] == PRED_MULTI;
     if (c) atomicAdd(out, c);
 }
 
@@ -828,7 +829,7 @@ struct srg_ctx {
     hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr, ev_e = nullptr;
     std::mutex mu;
     DevBuf b_src, b_dst, b_lat, b_loss, b_ids, b_nodes, b_olat, b_oloss;  // host-entry staging
-    DevBuf b_W, b_WL, b_D, b_PRED, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
+    DevBuf b_W, b_WL, b_D, b_PRED, b_PRED2, b_L0, b_L1, b_mark, b_selfcnt, b_selflat, b_selfloss;
     DevBuf b_stats, b_flags, b_multi, b_pos, b_cnt;
     // sparse tight scan
     DevBuf b_ecnt, b_eoff, b_indeg, b_cscoff, b_cscfill, b_entkey, b_entw, b_entb, b_grpu, b_grpe, b_cscent,
@@ -860,7 +861,7 @@ struct srg_ctx {
     DevBuf b_ek0, b_ek1, b_eh0, b_eh1, b_ei0, b_ei1, b_ehist, b_eoffs, b_ered;
     ~srg_ctx() {
         for (DevBuf* b : {&b_src, &b_dst, &b_lat, &b_loss, &b_ids, &b_nodes, &b_olat, &b_oloss, &b_W, &b_WL,
-                          &b_D, &b_PRED, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
+                          &b_D, &b_PRED, &b_PRED2, &b_L0, &b_L1, &b_mark, &b_selfcnt, &b_selflat, &b_selfloss,
                           &b_stats, &b_flags, &b_multi, &b_pos, &b_cnt, &b_ecnt, &b_eoff, &b_indeg, &b_cscoff,
                           &b_cscfill, &b_entkey, &b_entw, &b_entb, &b_grpu, &b_grpe, &b_cscent, &b_gblk, &b_DST,
                           &b_scantmp, &b_ess, &b_rlen, &b_roff, &b_lnodes, &b_lpos, &b_red, &b_cflags, &b_tiles, &b_tslot, &b_outoff, &b_outdst, &b_xlb, &b_xflags, &b_xexc, &b_odiag,
@@ -2562,9 +2563,17 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         const uint32_t scan_groups = c.scan_groups ? (uint32_t)c.scan_groups : 3u;
         const bool interleave = sink_rows && lds_rows <= 150 * 1024 && scan_groups > 1;
         if (interleave) {
-            set_lds(k_loss_rows<K>, lds_rows);
+            set_lds(k_loss_rows<K, true>, lds_rows);
             HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
         }
+        // the per-row LDS loss pass reads PRED packed with each single predecessor's {u, 1 - loss}
+        // (k_pred_pack, after each scan group); the global-memory fold the entry indices
+        uint32_t* PREDK = lds_rows <= 150 * 1024 ? (uint32_t*)c.b_PRED2.get(nmax * Vp * 8) : nullptr;
+        auto pack_pred = [&](uint32_t r0, uint32_t r1) {
+            const uint32_t nsb = (r1 - r0 + 127) / 128, nt8 = (nbTT5 + 7) / 8;
+            k_pred_pack<<<8u * nt8 * nsb, 256, 0, st>>>(PRED, Vp, r0, r1, NT, nbTT5, nsb, ent_ub, (uint2*)PREDK);
+            HIP_CHECK(hipGetLastError());
+        };
         if (nloc) {
             const uint32_t nbS = (uint32_t)(npad / 64);
             K* DST = (K*)c.b_DST.get(dst_bytes);
@@ -2608,7 +2617,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 if (interleave) {
                     const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);
                     if (r1 <= r0) continue;
-                    k_loss_rows<K><<<r1 - r0, 1024, lds_rows, st>>>(PRED, Vp, V, lnodes, nloc, ent_ub, ent_w,
+                    pack_pred(r0, r1);
+                    k_loss_rows<K, true><<<r1 - r0, 1024, lds_rows, st>>>(PREDK, Vp, V, lnodes, nloc, ent_ub, ent_w,
                                                                    DST, npad, cscoff, cscent, P.selfloss, nodes, n,
                                                                    lpos, out_loss, &P.flags->changed, r0);
                     HIP_CHECK(hipGetLastError());
@@ -2626,15 +2636,16 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                 loss_written = true;
             } else if (lds_rows <= 150 * 1024) {
                 // per-row Gauss-Seidel in LDS, writes out_loss directly
-                set_lds(k_loss_rows<K>, lds_rows);
+                set_lds(k_loss_rows<K, true>, lds_rows);
                 HIP_CHECK(hipMemsetAsync(&P.flags->changed, 0, 4, st));
                 // host entry: row chunks, each chunk's loss rows sent as soon as it is done
+                pack_pred(0, nloc);
                 const uint32_t nchunk = std::max<uint32_t>(1, std::min<uint32_t>(c.loss_chunks ? c.loss_chunks : sink_rows ? 8 : 1, nloc));
                 for (uint32_t q = 0; q < nchunk; ++q) {
                     const uint32_t r0 = (uint32_t)((uint64_t)nloc * q / nchunk);
                     const uint32_t r1 = (uint32_t)((uint64_t)nloc * (q + 1) / nchunk);
                     if (r1 == r0) continue;
-                    k_loss_rows<K><<<r1 - r0, 1024, lds_rows, st>>>(PRED, Vp, V, lnodes, nloc, ent_ub, ent_w,
+                    k_loss_rows<K, true><<<r1 - r0, 1024, lds_rows, st>>>(PREDK, Vp, V, lnodes, nloc, ent_ub, ent_w,
                                                                    DST, npad, cscoff, cscent, P.selfloss, nodes, n,
                                                                    lpos, out_loss, &P.flags->changed, r0);
                     HIP_CHECK(hipGetLastError());

@@ -186,14 +186,31 @@ __global__ void __launch_bounds__(256) k_v5_fill(const unsigned long long* __res
     size_t e = 2 * ((size_t)pbase + incl - p);
     const uint32_t u0 = k * V5_UC, u1 = min(V, u0 + V5_UC);
     uint32_t cp = csc_pos[((size_t)b * nK + k) * V5_TT + tt];  // (k_v5_cscpos)
-    for (uint32_t u = u0; u < u1; ++u) {
-        if (!((ess[(size_t)u * nw64 + w64] >> lane) & 1ull)) continue;
-        const K w = W[(size_t)u * ld + t];
-        rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), (uint32_t)w);  // the pair's target: first slot only
-        ent_w[e] = w;
-        ent_ub[e] = make_uint2(u, __float_as_uint(__fsub_rn(1.0f, __uint_as_float(WL[(size_t)u * ld + t]))));
-        csc_ent[cp++] = (uint32_t)e;
-        ++e;
+    // eight rows per step: all their loads in flight before the stores (one row at a time, each
+    // lane's dependent load -> store chain ran the kernel at ~0.4 TB/s)
+    for (uint32_t ub = u0; ub < u1; ub += 8) {
+        bool on[8];
+        K wv[8];
+        uint32_t lv[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t u = ub + q;
+            on[q] = u < u1 && ((ess[(size_t)u * nw64 + w64] >> lane) & 1ull);
+            if (on[q]) {
+                wv[q] = W[(size_t)u * ld + t];
+                lv[q] = WL[(size_t)u * ld + t];
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            if (!on[q]) continue;
+            const uint32_t u = ub + q;
+            rec[e] = make_uint2(((u - u0) * 512u) | ((e & 1) ? 0u : (j << 16)), (uint32_t)wv[q]);  // the pair's target: first slot only
+            ent_w[e] = wv[q];
+            ent_ub[e] = make_uint2(u, __float_as_uint(__fsub_rn(1.0f, __uint_as_float(lv[q]))));
+            csc_ent[cp++] = (uint32_t)e;
+            ++e;
+        }
     }
     if (c & 1u) {  // odd run: a sentinel second slot (w = INF is never tight on a reachable target)
         rec[e] = make_uint2(0u, KeyOps<uint32_t>::INF);
@@ -344,6 +361,51 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
     }
 }
 
+// PRED rows [r0, r1) -> PK[r][t] = {u, bits of 1 - loss(u,t)} of the single tight predecessor's
+// entry, or {PRED_NONE / PRED_MULTI, 0}: the gather k_loss_rows would do per target, done here
+// target tile by target tile.  A tile's entries are one contiguous run (~0.8 MB at C3), so with
+// every workgroup of tile b on XCD b mod 8 (tiles taken in turn, all source blocks of a tile at
+// once) the run stays in that XCD's L2; the loss pass's rows gather across every tile's entries
+// (~62 MB at C3: Infinity-Cache misses, 680 us per launch there, 285 us on packed rows).
+// Grid: 8 * ntile8 * nsb workgroups of 256 (ntile8 = ceil(nbTT / 8), nsb = source blocks of 128).
+__global__ void __launch_bounds__(256) k_pred_pack(const uint32_t* __restrict__ PRED, size_t ldp, uint32_t r0,
+                                                   uint32_t r1, uint32_t NT, uint32_t nbTT, uint32_t nsb,
+                                                   const uint2* __restrict__ ent_ub, uint2* __restrict__ PK) {
+    const uint32_t xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const uint32_t b = xcd + 8 * (slot / nsb), sb = slot % nsb;
+    if (b >= nbTT) return;
+    const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8: 4 targets per thread
+    const uint32_t t = b * V5_TT + tx * 4;
+    if (t >= NT) return;  // (tight_v5 writes targets < NT = V rounded up to 64; a multiple of 4)
+    // four rows per step: 16 gathers in flight per thread
+    for (uint32_t i0 = ty; i0 < 128; i0 += 32) {
+        uint32_t pv[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = r0 + sb * 128 + i0 + 8 * k;
+            uint4 p = make_uint4(PRED_NONE, PRED_NONE, PRED_NONE, PRED_NONE);
+            if (r < r1) p = *reinterpret_cast<const uint4*>(PRED + (size_t)r * ldp + t);
+            pv[k][0] = p.x;
+            pv[k][1] = p.y;
+            pv[k][2] = p.z;
+            pv[k][3] = p.w;
+        }
+        uint2 q[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[k][j] = pv[k][j] < PRED_MULTI ? ent_ub[pv[k][j]] : make_uint2(pv[k][j], 0u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = r0 + sb * 128 + i0 + 8 * k;
+            if (r >= r1) break;
+            uint4* o = reinterpret_cast<uint4*>(PK + (size_t)r * ldp + t);
+            o[0] = make_uint4(q[k][0].x, q[k][0].y, q[k][1].x, q[k][1].y);
+            o[1] = make_uint4(q[k][2].x, q[k][2].y, q[k][3].x, q[k][3].y);
+        }
+    }
+}
+
 // Jacobi round of the left fold over the tight DAG, entries variant.
 template <class K>
 __global__ void k_loss_round_sparse(const uint32_t* __restrict__ PRED, size_t ldp, const K* __restrict__ DST,
@@ -400,7 +462,8 @@ constexpr uint32_t U_MLIST = 0xF0000000u;  // U_MLIST + i: multi target i of the
 constexpr uint32_t LM_T = 32, LM_E = 16;
 constexpr size_t loss_rows_lds(uint32_t V) { return (size_t)V * 12 + LM_T * (4 + 4 + LM_E * 8) + 16; }
 
-template <class K>
+// PK: PRED rows as tight_v5<true> writes them ({u, 1 - loss} or {marker, 0}, ldp uint2 per row)
+template <class K, bool PK>
 __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__ PRED, size_t ldp, uint32_t V,
                                                      const uint32_t* __restrict__ nodes, uint32_t n,
                                                      const uint2* __restrict__ ent_ub, const K* __restrict__ ent_w,
@@ -422,12 +485,14 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
     __shared__ uint32_t changed, nm;
     const uint32_t r = row0 + blockIdx.x;  // launched in row chunks (host entry: D2H per chunk)
     const uint32_t s = nodes[r];
-    const uint32_t* prow = PRED + (size_t)r * ldp;
+    const uint32_t* prow = PRED + (size_t)r * ldp * (PK ? 2 : 1);
     if (threadIdx.x == 0) nm = 0;
     if (threadIdx.x < LM_T) m_n[threadIdx.x] = 0;
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < V; t += blockDim.x) {
-        const uint32_t p = prow[t];
+        uint2 pk = make_uint2(0u, 0u);
+        if constexpr (PK) pk = reinterpret_cast<const uint2*>(prow)[t];
+        const uint32_t p = PK ? pk.x : prow[t];
         uint32_t u;
         float bb = 1.0f, l = 1.0f;
         if (t == s) {
@@ -443,7 +508,7 @@ __global__ void __launch_bounds__(1024) k_loss_rows(const uint32_t* __restrict__
                 u = U_MLIST + i;
             }
         } else {
-            const uint2 ub = ent_ub[p];  // (one 8-B gather per target: u and 1 - loss together)
+            const uint2 ub = PK ? pk : ent_ub[p];  // (one 8-B gather per target: u and 1 - loss together)
             u = ub.x;
             bb = __uint_as_float(ub.y);
         }
