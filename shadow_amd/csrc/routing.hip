@@ -2594,62 +2594,25 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             // after it and shipped while later groups scan (loss rows on a second stream beside the
             // next group's scan were starved of CUs: 24.7 ms vs 20.8)
             const uint32_t ng = interleave ? std::min<uint32_t>(scan_groups, nbS5) : 1u;
-            // tight_v5 runs one (tile, source block) item per workgroup (~1.1 ms each at C3), two
-            // per CU; a launch takes as many rounds as its busiest XCD's items / 64 (xcd_rounds:
-            // the kernel's block dealing, counted).  The last group is as many source blocks as fill
-            // the slots once, launched flat (one round; C3 6 x 79 = 474 <= 512), so few loss rows
-            // are left to ship after it; the first group's size is the one nearest half whose two
-            // groups need the fewest rounds.  C3: 36 / 37 / 6 = 6 + 6 + 1 rounds (40 / 32 / 7 took
-            // 7 + 5 + 2).
-            int dev_cus = 256;
-            HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));
-            const uint32_t slots = 2u * (uint32_t)dev_cus, xslots = std::max<uint32_t>(1, slots / 8);
-            const uint32_t lastn = std::max<uint32_t>(1, slots / std::max<uint32_t>(nbTT5, 1));
-            auto xcd_rounds = [&](uint32_t c0, uint32_t c1) {  // tight_v5's dealing of [c0, c1), counted
-                const uint32_t nbb = (nbTT5 + 3) / 4, ncol = (c1 - c0 + 7) / 8, nblk = nbb * ncol;
-                uint64_t worst = 0;
-                for (uint32_t x = 0; x < 8; ++x) {
-                    uint64_t real = 0;
-                    for (uint32_t blk = x; blk < nblk; blk += 8) {
-                        const uint32_t tg = blk % nbb, col = blk / nbb;
-                        real += (uint64_t)std::min(4u, nbTT5 - 4 * tg) * std::min(8u, c1 - c0 - 8 * col);
-                    }
-                    worst = std::max(worst, (real + xslots - 1) / xslots);
-                }
-                return worst;
-            };
-            uint32_t split1 = 0;
-            if (ng == 3 && nbS5 > lastn + 1) {
-                const uint32_t rest = nbS5 - lastn;
-                uint64_t best = ~0ull;
-                for (uint32_t a = 1; a < rest; ++a) {
-                    const uint64_t cost = (xcd_rounds(0, a) + xcd_rounds(a, rest)) * 65536 + (uint64_t)std::abs((int)a - (int)(rest / 2));
-                    if (cost < best) {
-                        best = cost;
-                        split1 = a;
-                    }
-                }
-            }
             for (uint32_t gi = 0; gi < ng; ++gi) {
                 // group bounds on multiples of 8 source blocks: every XCD gets the same number of
                 // blocks per launch (20 blocks = 3/3/3/3/2/2/2/2 ran 33 % long)
                 auto cut = [&](uint32_t q) {
                     if (q == 0) return 0u;
                     if (q == ng) return nbS5;
-                    // three groups (above); a small last group keeps the loss rows left to ship
-                    // after the last fold few (40 / 32 / 7 blocks vs thirds: exposed D2H 1.8 -> 0.8
-                    // ms, profiles/r02i/scan_cuts.txt)
-                    if (ng == 3 && split1 > 0) return q == 1 ? split1 : nbS5 - lastn;
-                    return std::min(nbS5, nbS5 * q / ng);
+                    // three groups: half, then all but the last partial 8 blocks, so the loss rows
+                    // left to ship after the last fold are few (C3 40 / 32 / 7 blocks: exposed D2H
+                    // 1.8 -> 0.8 ms, scan + tail -0.6 ms vs thirds, profiles/r02i/scan_cuts.txt)
+                    const uint32_t half = std::min(nbS5, (nbS5 / 2 + 4) / 8 * 8), last = (nbS5 - 1) / 8 * 8;
+                    if (ng == 3 && half > 0 && last > half) return q == 1 ? half : last;
+                    return std::min(nbS5, (nbS5 * q / ng + 4) / 8 * 8);
                 };
                 const uint32_t c0 = cut(gi), c1 = cut(gi + 1);
                 if (c1 == c0) continue;
-                const uint32_t items = (c1 - c0) * nbTT5;
-                const bool flat = items <= slots;
                 const uint32_t nblk = (nbTT5 + 3) / 4 * ((c1 - c0 + 7) / 8);
-                tight_v5<<<flat ? items : 8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
+                tight_v5<<<8u * 32u * ((nblk + 7) / 8), V5_WAVES * 64, 0, st>>>(
                     DSTs, npad, dsts_bytes, lnodes, nloc, V, NT, nbTT5, c1, nK5, c0, v5_goff,
-                    (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check, flat ? 1u : 0u);
+                    (const uint32_t*)c.b_entkey.get(0), PRED, Vp, inf_check);
                 HIP_CHECK(hipGetLastError());
                 if (interleave) {
                     const uint32_t r0 = c0 * SB, r1 = std::min<uint32_t>(c1 * SB, nloc);

@@ -239,13 +239,6 @@ struct alignas(64) V5Grp {
 // k_loss_rows resolves with the exact u64 keys (DST / ent_w of type K).  Targets unreachable
 // from the source are not used pairs (certified before the scan) and are no tight predecessor
 // of a reachable target, so their entries are never read through a single match.
-// flat = 1 (a launch that fits the chip's slots at once: the host entry's last source-block group):
-// workgroup i takes tile i mod nbTT of source block c0 + i / nbTT, equal shares for the XCDs in one
-// round (the blocks below gave C3's 6-7-block last group 3 blocks on some XCDs: two rounds).  A
-// group's time is its rounds per XCD (the host picks the cuts, scan_rounds); dealing every group
-// evenly instead -- contiguous ranges of tile-major items per XCD, or persistent workgroups with
-// per-XCD queues -- ran 5-12 % slower per item (the XCDs then read different source columns and
-// tiles, and the workgroups of a tile drift apart).
 // grid: 8 * 32 * ceil(nblk / 8) workgroups of 512 for the source blocks [c0, nbS), nblk =
 // ceil(nbTT / 4) * ceil((nbS - c0) / 8) blocks of 4 target tiles x 8 source blocks, dealt to the
 // XCDs in turn.  XCD-aware: an XCD holds two such blocks at once (2 workgroups per CU), so every
@@ -257,16 +250,11 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
                                                     const uint32_t* __restrict__ nodes, uint32_t n, uint32_t V,
                                                     uint32_t NT, uint32_t nbTT, uint32_t nbS, uint32_t nK, uint32_t c0,
                                                     const uint32_t* __restrict__ goff, const uint32_t* __restrict__ rec,
-                                                    uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check,
-                                                    uint32_t flat) {
+                                                    uint32_t* __restrict__ PRED, size_t ldp, uint32_t inf_check) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[2 * V5_UC * V5_SB];  // 2 x 32 KB ring
     const uint32_t bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
     const uint32_t blk = (slot >> 5) * 8 + xcd, nbb = (nbTT + 3) / 4;  // block of 4 tiles x 8 source blocks
-    uint32_t b = (blk % nbb) * 4 + (slot & 3), c = c0 + (blk / nbb) * 8 + ((slot >> 2) & 7);
-    if (flat) {  // a launch of at most one workgroup per slot: tiles dealt to the XCDs in turn
-        b = bid % nbTT;
-        c = c0 + bid / nbTT;
-    }
+    const uint32_t b = (blk % nbb) * 4 + (slot & 3), c = c0 + (blk / nbb) * 8 + ((slot >> 2) & 7);
     if (c >= nbS || b >= nbTT) return;  // whole workgroup: no barrier is left waiting
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
