@@ -926,6 +926,28 @@ __global__ void __launch_bounds__(256, 3) fw_bulk_lb(K* __restrict__ D, size_t l
                          lb + lm.slot(J, L) * TT, J >= L, T, nullptr, 0);
 }
 
+// The bulk for launches below one round of the chip's slots (several ranks: C3 at G = 8 holds 395
+// tiles per pivot against 768 slots): each tile as four 64 x 64 quadrants (grid (tiles, 4)), the
+// quadrant products of fw_line_lb<S = 2>, so the launch fills the CUs.
+template <class K, int T, int KC>
+__global__ void __launch_bounds__(256, 4) fw_bulk_lb_q(K* __restrict__ D, size_t ld, const K* __restrict__ lb, int L,
+                                                       int x0, int x1, LineMap lm, const int* __restrict__ tiles,
+                                                       int maxI) {
+    const int t = tiles[blockIdx.x];
+    if (t < 0) return;
+    int I, J;
+    tri_tile(lm.nb, t, I, J);
+    if (I == x0 || I == x1 || J == x0 || J == x1 || I > maxI) return;  // whole workgroup
+    constexpr size_t TT = (size_t)T * T;
+    constexpr int TM = T / 2;
+    const int qi = (int)blockIdx.y >> 1, qj = (int)blockIdx.y & 1;
+    const bool acol = I > L, bcol = J >= L;
+    const K* Ab = lb + lm.slot(I, L) * TT + (acol ? (size_t)qi * TM : (size_t)qi * TM * T);
+    const K* Bb = lb + lm.slot(J, L) * TT + (bcol ? (size_t)qj * TM : (size_t)qj * TM * T);
+    fw_core<K, TM, T, KC>(D + ((size_t)I * T + (size_t)qi * TM) * ld + (size_t)J * T + qj * TM, ld, Ab, acol, Bb, bcol, T,
+                          nullptr, 0);
+}
+
 // Late tiles (the host entry's FW beside the H2D, routing.hip FwOverlap; one rank, u32 keys): the
 // tiles (I, J >= I) of block-row I, whose edges landed after the bulks of pivots [0, P) ran without
 // them, catch up on pivots p in group blockIdx.y (pg pivots per group):

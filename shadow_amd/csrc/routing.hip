@@ -1681,7 +1681,7 @@ struct SymFw {
     K* D;
     size_t Vp;
     hipStream_t st;
-    int nb, G, g, split = 1, ntile = 0, prio = kChainPrio;
+    int nb, G, g, split = 1, bulk_split = 1, ntile = 0, prio = kChainPrio;
     bool multi = false, prof = false, keep_lines = false;
     LineMap lm{1, 1};
     size_t lds_bulk = 0;
@@ -1745,6 +1745,16 @@ struct SymFw {
         // took 45-117 us per pivot, the one-workgroup FW closure 159 us beside the bulk: r03b/).
         const int bulk_tiles = nb * (nb + 1) / 2 / G;
         split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
+        // a bulk below one round of the slots (3 per CU) runs as quadrants (fw_bulk_lb_q): sim 8:0
+        // bulk launch 59.5 -> 48.6 us, FW 6.24-6.28 -> 6.02-6.04 ms (profiles/r05/chain/)
+        if (sizeof(K) == 4 && T == 128 && G > 1) {
+            int cus = 256;
+            HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
+            if (bulk_tiles < 3 * cus) {
+                bulk_split = 2;
+                set_lds(fw_bulk_lb_q<K, T, 32>, lb_lds<K, T / 2, 32>());
+            }
+        }
         set_lds(fw_line_lb<K, T, 1>, lb_lds<K, T, line_kc<1>()>());
         set_lds(fw_line_lb<K, T, 2>, lb_lds<K, T / 2, line_kc<2>()>());
         set_lds(fw_line_lb<K, T, 4>, lb_lds<K, T / 4, line_kc<4>()>());
@@ -1840,14 +1850,19 @@ struct SymFw {
         // the remaining tiles of kb (the dominant kernel), overlapped with the chain of k1
         const bool timed = prof && ntile > 0 && k1 < nb && maxI >= nb - 1;
         if (timed) HIP_CHECK(hipEventRecord(c.prof_events[2 * *prof_n], st));
+        auto bulk = [&](int nl, const int* list) {
+            if (bulk_split == 2)
+                fw_bulk_lb_q<K, T, 32><<<dim3(nl, 4), 256, lb_lds<K, T / 2, 32>(), st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1,
+                                                                                         lm, list, maxI);
+            else
+                fw_bulk_lb<K, T, KCS><<<nl, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, list, maxI);
+        };
         if (!bulk_off.empty() && maxI >= nb - 1) {  // (beside the H2D, with rows still missing: triangle order,
                                                     // which spreads the missing rows' idle slots over the XCDs)
             const int nl = bulk_off[kb + 1] - bulk_off[kb];
-            if (nl > 0)
-                fw_bulk_lb<K, T, KCS><<<nl, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm,
-                                                                  tiles + ntile + bulk_off[kb], maxI);
+            if (nl > 0) bulk(nl, tiles + ntile + bulk_off[kb]);
         } else if (ntile > 0) {
-            fw_bulk_lb<K, T, KCS><<<ntile, 256, lds_bulk, st>>>(D, Vp, lbk, kb, kb, k1 < nb ? k1 : -1, lm, tiles, maxI);
+            bulk(ntile, tiles);
         }
         HIP_CHECK(hipGetLastError());
         if (timed) {
