@@ -844,6 +844,7 @@ struct srg_ctx {
     bool hop_values = false;            // this build's hops use the signals (stream_hop)
     unsigned long long hop_bound_ticks = 200000000ull;  // a value hop's wait bound (100 MHz ticks; SymFw::begin)
     hipEvent_t ev_fwreset = nullptr;    // SymFw::begin: the chain stream after the reset of the FW sync words
+    hipEvent_t ev_dst = nullptr;        // the scan's DST columns built (on the aux stream, beside the entry fill)
     int fw_line_split = 0;              // symmetric FW: line sub-tiles per dimension (0 = auto) (SRG_OPT_FW_LINE_SPLIT)
     int fw_step = -1;                   // symmetric FW's line exchange between ranks (SRG_OPT_FW_STEP, chain_xmode)
     DevBuf b_xlb, b_xflags;             // line buffers (kept lines / the exchange's three), peers' arrival flags
@@ -871,7 +872,7 @@ struct srg_ctx {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         for (uint32_t* p : sig)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate, ev_fwreset})
+        for (hipEvent_t e : {ev_a, ev_b, ev_c, ev_d, ev_e, ev_ledges, ev_lin, ev_ldone, ev_wlate, ev_fwreset, ev_dst})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_ov) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_lring)
@@ -2559,6 +2560,28 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                         E_layout + 256 < 0xF0000000ull && dst_bytes < 0xFFFFFFFFull;
     if (sparse) {
         scan_kind = SRG_SCAN_SPARSE;
+        // the scan's DST (D columns of the used sources, + their low words for u64 keys) on the aux
+        // stream, beside the entry fill: it reads D only (st is past FW)
+        K* DST = nullptr;
+        const uint32_t* DSTs = nullptr;
+        uint32_t dsts_bytes = 0;
+        if (nloc) {
+            hipStream_t ax = c.aux_stream;
+            const uint32_t nbS = (uint32_t)(npad / 64);
+            DST = (K*)c.b_DST.get(dst_bytes);
+            k_build_dst<K><<<dim3(nw64, nbS), 256, 0, ax>>>(D, Vp, lnodes, nloc, DST, npad);
+            DSTs = (const uint32_t*)DST;
+            dsts_bytes = (uint32_t)std::min<size_t>(dst_bytes, 0xFFFFFFFFull);
+            if (v5lo) {
+                const size_t cnt = dst_bytes / 8;
+                uint32_t* lo = (uint32_t*)c.b_DST2.get(cnt * 4);
+                k_low_words<<<grid_for(cnt), kThreads, 0, ax>>>(reinterpret_cast<const uint64_t*>(DST), cnt, lo);
+                DSTs = lo;
+                dsts_bytes = (uint32_t)(cnt * 4);
+            }
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipEventRecord(c.ev_dst, ax));
+        }
         const size_t Eb = E_layout + 256;
         uint32_t* cscpos = (uint32_t*)c.b_cscfill.get((size_t)nbTT5 * nK5 * V5_TT * 4);
         K* ent_w = (K*)c.b_entw.get(Eb * sizeof(K));
@@ -2590,19 +2613,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
             HIP_CHECK(hipGetLastError());
         };
         if (nloc) {
-            const uint32_t nbS = (uint32_t)(npad / 64);
-            K* DST = (K*)c.b_DST.get(dst_bytes);
-            k_build_dst<K><<<dim3(nw64, nbS), 256, 0, st>>>(D, Vp, lnodes, nloc, DST, npad);
-            // the scan's DST: the keys themselves (u32), or their low words (u64 keys)
-            const uint32_t* DSTs = (const uint32_t*)DST;
-            uint32_t dsts_bytes = (uint32_t)std::min<size_t>(dst_bytes, 0xFFFFFFFFull);
-            if (v5lo) {
-                const size_t cnt = dst_bytes / 8;
-                uint32_t* lo = (uint32_t*)c.b_DST2.get(cnt * 4);
-                k_low_words<<<grid_for(cnt), kThreads, 0, st>>>(reinterpret_cast<const uint64_t*>(DST), cnt, lo);
-                DSTs = lo;
-                dsts_bytes = (uint32_t)(cnt * 4);
-            }
+            HIP_CHECK(hipStreamWaitEvent(st, c.ev_dst, 0));  // (the scan's DST, built on the aux stream)
             const uint32_t inf_check = v5lo ? 0u : 1u;
             const uint32_t nbS5 = (uint32_t)(npad / SB);
             // host entry: the scan runs in source-block groups, each group's loss rows folded right
@@ -3988,7 +3999,8 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
         // stream would share a hardware queue (GPU_MAX_HW_QUEUES = 4) with the main stream and
         // serialise the W build and FW behind the loss DMAs (measured: build 1.0 -> 3.6 ms)
         c->loss_stream = c->d2h_stream;
-        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate, &c->ev_fwreset})
+        for (hipEvent_t* e : {&c->ev_a, &c->ev_b, &c->ev_c, &c->ev_d, &c->ev_e, &c->ev_ledges, &c->ev_wlate, &c->ev_fwreset,
+                              &c->ev_dst})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         int wv = 0;
         if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && wv) {
