@@ -2415,6 +2415,62 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         c.comm->allgatherv(out, offs.data(), lens.data(), cs);
     };
 
+    // ---- essential edges (W[u][t] == D[u][t]) counted into the scan's pair-record layout ----
+    // One rank: on the comm stream (idle after the H2D), beside the certification / extract and
+    // their flag read-backs on st, which read D only; several ranks: on st (cs carries collectives).
+    hipStream_t es = multi ? st : c.comm_stream;
+    auto drain_es = [&]() {  // (before an early return: a rerun may reallocate these buffers)
+        if (es != st) HIP_CHECK(hipStreamSynchronize(es));
+    };
+    constexpr int TS = 64;
+    constexpr int VE = 16 / (int)sizeof(K);
+    const size_t nmax = std::max<uint32_t>(nloc, 1);
+    uint32_t* PRED = (uint32_t*)c.b_PRED.get(nmax * Vp * 4);
+    unsigned long long* multi_cnt = (unsigned long long*)c.b_multi.get(8);
+    int rounds = 0;
+    unsigned long long nmulti = 0;
+    uint64_t n_ess = 0;
+    int scan_kind = SRG_SCAN_NONE;
+    bool loss_written = false;  // out_loss already filled by the per-row kernel
+    float* Lfin = nullptr;
+    double ms_scan = 0;
+    HIP_CHECK(hipMemsetAsync(multi_cnt, 0, 8, st));
+    // essential bitmask (V^2/8 bytes): every rank holds the whole D and W, so each builds all of it
+    const uint32_t nw64 = (V + 63) / 64;
+    unsigned long long* ess = (unsigned long long*)c.b_ess.get((size_t)V * nw64 * 8);
+    k_ess_mask<K><<<V, 256, 0, es>>>(W, D, Vp, V, 0u, V, nw64, ess);
+    uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
+    uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
+    HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, es));
+    // pair-lane LDS scan (tight_v5); u64 keys run it on the keys' low words (exact together with
+    // the loss pass's multi-predecessor check, tight_sparse.hip.h)
+    const bool v5lo = sizeof(K) == 8;
+    const uint32_t SB = V5_SB;
+    const size_t npad = ((size_t)nloc + SB - 1) / SB * SB;
+    const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
+    const uint32_t NT = nw64 * 64;
+    const uint32_t nK5 = (V + V5_UC - 1) / V5_UC, nbTT5 = (NT + V5_TT - 1) / V5_TT;
+    const size_t NG5 = (size_t)nbTT5 * nK5 * V5_WAVES;
+    uint32_t* v5_cnt = (uint32_t*)c.b_ecnt.get((size_t)nbTT5 * nK5 * V5_TT * 4);
+    uint32_t* v5_goff = (uint32_t*)c.b_eoff.get((NG5 + 1) * 4);
+    uint64_t E_ess = 0, E_layout = 0;
+    {
+        uint32_t* v5_glen = (uint32_t*)c.b_rlen.get((NG5 + 1) * 4);
+        HIP_CHECK(hipMemsetAsync(v5_cnt, 0, (size_t)nbTT5 * nK5 * V5_TT * 4, es));
+        HIP_CHECK(hipMemsetAsync(v5_glen, 0, (NG5 + 1) * 4, es));
+        const size_t nwaves = (size_t)nw64 * nK5;
+        k_v5_count<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, es>>>(ess, V, nw64, nK5, v5_cnt, v5_glen, indeg);
+        HIP_CHECK(hipGetLastError());
+        size_t ta = 0, tc = 0;
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), es));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, v5_glen, v5_goff, (int)(NG5 + 1), es));
+        const size_t tbytes = std::max(ta, tc);
+        void* tmp = c.b_scantmp.get(tbytes);
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, ta, indeg, cscoff, (int)(NT + 1), es));
+        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tc, v5_glen, v5_goff, (int)(NG5 + 1), es));
+        HIP_CHECK(hipGetLastError());
+    }
+
     // u32 certification: no saturated key in any used row (every rank must agree)
     HIP_CHECK(hipMemsetAsync(&P.flags->inf_in_used_row, 0, 4, st));
     HIP_CHECK(hipMemsetAsync(&P.flags->impossible, 0, 4, st));
@@ -2436,6 +2492,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         const unsigned __int128 bound = (unsigned __int128)P.max_key * (V > 1 ? V - 1 : 1);
         if (bound >= KeyOps<uint32_t>::INF) {
             if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));  // the u64 rerun rewrites WL
+            drain_es();
             return false;
         }
         fail(SRG_ERR_UNREACHABLE,
@@ -2462,6 +2519,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         if (reduce_flag(&P.flags->wrap_inf)) {
             if (sizeof(K) == 4) {  // a vertex past the u32 keys: decide on the u64 keys
                 if (wl_late) HIP_CHECK(hipStreamWaitEvent(st, c.ev_wlate, 0));
+                drain_es();
                 return false;
             }
             fail(SRG_ERR_LATENCY_RANGE, "a vertex has no path below 2^62 latency units on a graph whose u64 latency "
@@ -2501,56 +2559,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         sink->lat_sent = true;
     }
 
-    // ---- essential edges, tight-predecessor scan, loss ----
-    constexpr int TS = 64;
-    constexpr int VE = 16 / (int)sizeof(K);
-    const size_t nmax = std::max<uint32_t>(nloc, 1);
-    uint32_t* PRED = (uint32_t*)c.b_PRED.get(nmax * Vp * 4);
-    unsigned long long* multi_cnt = (unsigned long long*)c.b_multi.get(8);
-    int rounds = 0;
-    unsigned long long nmulti = 0;
-    uint64_t n_ess = 0;
-    int scan_kind = SRG_SCAN_NONE;
-    bool loss_written = false;  // out_loss already filled by the per-row kernel
-    float* Lfin = nullptr;
-    double ms_scan = 0;
-    HIP_CHECK(hipMemsetAsync(multi_cnt, 0, 8, st));
-    // essential bitmask (V^2/8 bytes): every rank holds the whole D and W, so each builds all of it
-    const uint32_t nw64 = (V + 63) / 64;
-    unsigned long long* ess = (unsigned long long*)c.b_ess.get((size_t)V * nw64 * 8);
-    k_ess_mask<K><<<V, 256, 0, st>>>(W, D, Vp, V, 0u, V, nw64, ess);
-    uint32_t* indeg = (uint32_t*)c.b_indeg.get(((size_t)nw64 * 64 + 1) * 4);
-    uint32_t* cscoff = (uint32_t*)c.b_cscoff.get(((size_t)nw64 * 64 + 1) * 4);
-    HIP_CHECK(hipMemsetAsync(indeg, 0, ((size_t)nw64 * 64 + 1) * 4, st));
-    // pair-lane LDS scan (tight_v5); u64 keys run it on the keys' low words (exact together with
-    // the loss pass's multi-predecessor check, tight_sparse.hip.h)
-    const bool v5lo = sizeof(K) == 8;
-    const uint32_t SB = V5_SB;
-    const size_t npad = ((size_t)nloc + SB - 1) / SB * SB;
-    const size_t dst_bytes = (size_t)nw64 * 64 * std::max<size_t>(npad, 64) * sizeof(K);
-    const uint32_t NT = nw64 * 64;
-    const uint32_t nK5 = (V + V5_UC - 1) / V5_UC, nbTT5 = (NT + V5_TT - 1) / V5_TT;
-    const size_t NG5 = (size_t)nbTT5 * nK5 * V5_WAVES;
-    uint32_t* v5_cnt = (uint32_t*)c.b_ecnt.get((size_t)nbTT5 * nK5 * V5_TT * 4);
-    uint32_t* v5_goff = (uint32_t*)c.b_eoff.get((NG5 + 1) * 4);
-    uint64_t E_ess = 0, E_layout = 0;
+    // ---- tight-predecessor scan, loss (the essential entries were counted above) ----
     {
-        uint32_t* v5_glen = (uint32_t*)c.b_rlen.get((NG5 + 1) * 4);
-        HIP_CHECK(hipMemsetAsync(v5_cnt, 0, (size_t)nbTT5 * nK5 * V5_TT * 4, st));
-        HIP_CHECK(hipMemsetAsync(v5_glen, 0, (NG5 + 1) * 4, st));
-        const size_t nwaves = (size_t)nw64 * nK5;
-        k_v5_count<<<(unsigned)((nwaves * 64 + 255) / 256), 256, 0, st>>>(ess, V, nw64, nK5, v5_cnt, v5_glen, indeg);
-        HIP_CHECK(hipGetLastError());
-        size_t ta = 0, tc = 0;
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, v5_glen, v5_goff, (int)(NG5 + 1), st));
-        const size_t tbytes = std::max(ta, tc);
-        void* tmp = c.b_scantmp.get(tbytes);
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, ta, indeg, cscoff, (int)(NT + 1), st));
-        HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tc, v5_glen, v5_goff, (int)(NG5 + 1), st));
-        rb_async(c, MS_TAIL0, cscoff + NT, st);
-        rb_async(c, MS_TAIL1, v5_goff + NG5, st);
-        HIP_CHECK(hipStreamSynchronize(st));
+        rb_async(c, MS_TAIL0, cscoff + NT, es);
+        rb_async(c, MS_TAIL1, v5_goff + NG5, es);
+        HIP_CHECK(hipStreamSynchronize(es));
         E_ess = rb_get<uint32_t>(c, MS_TAIL0);
         E_layout = 2ull * rb_get<uint32_t>(c, MS_TAIL1);
     }
@@ -3001,6 +3014,7 @@ void compute_device(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32
                     float* out_loss, hipStream_t st, srg_stats* stats, HostSink* sink = nullptr,
                     FwOverlap* ov = nullptr) {
     HIP_CHECK(hipStreamSynchronize(c.aux_stream));  // nothing of an aborted call still writes WL / PRED
+    HIP_CHECK(hipStreamSynchronize(c.comm_stream));  // ... or the essential-entry counts
     if (g.V == 0) {
         if (n) fail(SRG_ERR_ARG, "nodes given for an empty graph");
         return;
