@@ -983,7 +983,7 @@ T rb_get(const srg_ctx& c, int slot) {
     std::memcpy(&v, c.hbox + 64 * slot, sizeof(T));
     return v;
 }
-enum MailSlot { MS_EDGESTATS, MS_FLAGS, MS_TIMEOUT, MS_REDUCE, MS_TAIL0, MS_TAIL1, MS_NMULTI, MS_CHANGED, MS_MIN };
+enum MailSlot { MS_EDGESTATS, MS_FLAGS, MS_TIMEOUT, MS_REDUCE, MS_TAIL0, MS_TAIL1, MS_NMULTI, MS_CHANGED, MS_MIN, MS_REDUCE2 };
 
 // Common validation: nodes in range & unique, edge endpoints, self-loop counts, latency range.
 struct Prelude {
@@ -2482,10 +2482,21 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     // (a simulated rank -- SRG_OPT_SIMULATE_RANK, timing only -- never receives its peers' line
     // segments, so its table is not a result and the guard does not apply)
     const bool simulated = c.comm && std::strcmp(c.comm->kind(), "simulated") == 0;
-    if (reduce_flag(&P.flags->impossible) && !simulated)
+    // both of k_certify's flags with one read-back when one rank (each read-back is a stream drain)
+    uint32_t impossible = 0, inf_any = 0;
+    if (multi) {
+        impossible = reduce_flag(&P.flags->impossible);
+        inf_any = reduce_flag(&P.flags->inf_in_used_row);
+    } else {
+        rb_async(c, MS_REDUCE, &P.flags->impossible, st);
+        rb_async(c, MS_REDUCE2, &P.flags->inf_in_used_row, st);
+        HIP_CHECK(hipStreamSynchronize(st));
+        impossible = rb_get<uint32_t>(c, MS_REDUCE);
+        inf_any = rb_get<uint32_t>(c, MS_REDUCE2);
+    }
+    if (impossible && !simulated)
         fail(SRG_ERR_INTERNAL, "FW produced an impossible table: a used pair's latency is below the smallest edge "
                                "latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
-    const uint32_t inf_any = reduce_flag(&P.flags->inf_in_used_row);
     if (sizeof(K) == 4 && inf_any) {
         // a used pair at INF: unreachable -- unless some path could reach 2^31-1 ns, in which case
         // the u64 keys decide (the u32 FW work is redone)
