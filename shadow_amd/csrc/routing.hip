@@ -2633,7 +2633,8 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         uint32_t* PREDK = lds_rows <= 150 * 1024 ? (uint32_t*)c.b_PRED2.get(nmax * Vp * 8) : nullptr;
         auto pack_pred = [&](uint32_t r0, uint32_t r1) {
             const uint32_t nsb = (r1 - r0 + 127) / 128, nt8 = (nbTT5 + 7) / 8;
-            k_pred_pack<<<8u * nt8 * nsb, 256, 0, st>>>(PRED, Vp, r0, r1, NT, nbTT5, nsb, ent_ub, (uint2*)PREDK);
+            k_pred_pack<<<8u * nt8 * nsb, 256, 0, st>>>(PRED, Vp, r0, r1, NT, nbTT5, nsb, ent_ub, (uint2*)PREDK,
+                                                        multi_cnt);
             HIP_CHECK(hipGetLastError());
         };
         if (nloc) {
@@ -2675,7 +2676,7 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
                     sink->send_rows(st, out_loss, sink->loss, pl.p0 + r0, r1 - r0, 4);
                 }
             }
-            k_count_multi<<<nloc, kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);
+            if (!PREDK) k_count_multi<<<nloc, kThreads, 0, st>>>(PRED, nloc, V, Vp, multi_cnt);  // (else k_pred_pack counted)
             HIP_CHECK(hipGetLastError());
             ms_scan = tm.lap();
             if (interleave) {  // loss rows already folded and shipped, group by group

@@ -368,15 +368,18 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
 // once) the run stays in that XCD's L2; the loss pass's rows gather across every tile's entries
 // (~62 MB at C3: Infinity-Cache misses, 680 us per launch there, 285 us on packed rows).
 // Grid: 8 * ntile8 * nsb workgroups of 256 (ntile8 = ceil(nbTT / 8), nsb = source blocks of 128).
+// (also counts the PRED_MULTI pairs it passes into *multi: the build's multi_pred_pairs)
 __global__ void __launch_bounds__(256) k_pred_pack(const uint32_t* __restrict__ PRED, size_t ldp, uint32_t r0,
                                                    uint32_t r1, uint32_t NT, uint32_t nbTT, uint32_t nsb,
-                                                   const uint2* __restrict__ ent_ub, uint2* __restrict__ PK) {
+                                                   const uint2* __restrict__ ent_ub, uint2* __restrict__ PK,
+                                                   unsigned long long* __restrict__ multi) {
     const uint32_t xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     const uint32_t b = xcd + 8 * (slot / nsb), sb = slot % nsb;
     if (b >= nbTT) return;
     const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8: 4 targets per thread
     const uint32_t t = b * V5_TT + tx * 4;
-    if (t >= NT) return;  // (tight_v5 writes targets < NT = V rounded up to 64; a multiple of 4)
+    const bool tv = t < NT;  // (tight_v5 writes targets < NT = V rounded up to 64; a multiple of 4)
+    uint32_t nm = 0;
     // four rows per step: 16 gathers in flight per thread
     for (uint32_t i0 = ty; i0 < 128; i0 += 32) {
         uint32_t pv[4][4];
@@ -384,7 +387,7 @@ __global__ void __launch_bounds__(256) k_pred_pack(const uint32_t* __restrict__ 
         for (int k = 0; k < 4; ++k) {
             const uint32_t r = r0 + sb * 128 + i0 + 8 * k;
             uint4 p = make_uint4(PRED_NONE, PRED_NONE, PRED_NONE, PRED_NONE);
-            if (r < r1) p = *reinterpret_cast<const uint4*>(PRED + (size_t)r * ldp + t);
+            if (tv && r < r1) p = *reinterpret_cast<const uint4*>(PRED + (size_t)r * ldp + t);
             pv[k][0] = p.x;
             pv[k][1] = p.y;
             pv[k][2] = p.z;
@@ -394,15 +397,23 @@ __global__ void __launch_bounds__(256) k_pred_pack(const uint32_t* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[k][j] = pv[k][j] < PRED_MULTI ? ent_ub[pv[k][j]] : make_uint2(pv[k][j], 0u);
+            for (int j = 0; j < 4; ++j) {
+                q[k][j] = pv[k][j] < PRED_MULTI ? ent_ub[pv[k][j]] : make_uint2(pv[k][j], 0u);
+                nm += pv[k][j] == PRED_MULTI;  // (rows past r1 hold PRED_NONE)
+            }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t r = r0 + sb * 128 + i0 + 8 * k;
-            if (r >= r1) break;
+            if (!tv || r >= r1) break;
             uint4* o = reinterpret_cast<uint4*>(PK + (size_t)r * ldp + t);
             o[0] = make_uint4(q[k][0].x, q[k][0].y, q[k][1].x, q[k][1].y);
             o[1] = make_uint4(q[k][2].x, q[k][2].y, q[k][3].x, q[k][3].y);
         }
+    }
+    if (__ballot(nm != 0)) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(multi, (unsigned long long)nm);
     }
 }
 

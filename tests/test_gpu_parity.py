@@ -700,3 +700,40 @@ def test_late_loss_matches_with_loss(router, kind):
     rows = [0, 1, len(nodes) - 1]
     lat, loss = oracle.compute_shortest_paths(g.as_tuple(), nodes, rows=rows, mode=2, nthreads=8)
     assert np.array_equal(out[1].latency_ns[rows], lat) and bits_equal(out[1].packet_loss[rows], loss)
+
+
+@pytest.mark.parametrize("entry", ["host", "device"])
+def test_multi_pred_pairs_count(router, entry):
+    """stats.multi_pred_pairs (counted by k_pred_pack on the per-row loss path) equals the number of
+    used pairs (s, t), s != t, with two or more latency-tight essential in-edges, counted here from
+    the oracle's latencies (ties forced by a 1..3 latency range)."""
+    V = 300
+    g = synth.random_graph(V, 0.05, 231, lat_hi=3, parallel=0.2)
+    nodes = list(range(V))
+    lat, _ = oracle.compute_shortest_paths(g.as_tuple(), nodes)
+    D = lat.astype(np.int64)
+    np.fill_diagonal(D, 0)
+    W = np.full((V, V), np.iinfo(np.int64).max // 4, dtype=np.int64)
+    m = g.src != g.dst
+    s_, d_, w_ = g.src[m].astype(np.int64), g.dst[m].astype(np.int64), g.latency_ns[m].astype(np.int64)
+    np.minimum.at(W, (s_, d_), w_)
+    np.minimum.at(W, (d_, s_), w_)
+    ess = W == D  # (u, t) essential: the edge is itself a shortest path
+    expect = 0
+    for s in range(V):
+        tight = (D[s][:, None] + W == D[s][None, :]) & ess  # [u, t]
+        cnt = tight.sum(axis=0)
+        cnt[s] = 0
+        expect += int((cnt >= 2).sum())
+    if entry == "host":
+        t = router.compute_shortest_paths(g, nodes)
+        st = t.stats
+    else:
+        import torch
+        from shadow_amd.device import DeviceGraph, compute_shortest_paths_device
+        dev = torch.device("cuda", 0)
+        ol = torch.empty((V, V), dtype=torch.int64, device=dev)
+        os_ = torch.empty((V, V), dtype=torch.float32, device=dev)
+        st = compute_shortest_paths_device(router, DeviceGraph(g), torch.arange(V, dtype=torch.int32, device=dev), ol, os_)
+    assert st["scan_kind"] == N.SRG_SCAN_SPARSE
+    assert expect > 0 and st["multi_pred_pairs"] == expect
