@@ -119,6 +119,11 @@ def cpu_baselines(edges, target_s, desc, sources=256):
                       f"(HashMap-score petgraph Dijkstra + linear nodes.contains + HashMap merge, mod.rs:190-208) on "
                       f"{th} threads, {s0:.1f}s",
             "extrapolated": True, "full_run_estimate_s": round(V / ref, 1),
+            # rayon's default pool is every core (mod.rs:190-191); the box grants this job a CPU share,
+            # so the all-core figure is the measured per-thread rate x the affinity core count (the
+            # per-source runs are independent: linear in cores, an upper estimate, not a measurement)
+            "all_cores_estimate": {"value": round(ref * info["affinity_cpus"] / th, 3), "cores": info["affinity_cpus"],
+                                   "basis": f"measured {th}-thread rate x {info['affinity_cpus']}/{th} (linear scaling assumed)"},
             **info,
             "best": {"value": round(best, 3), "unit": "source-SSSPs/s", "cores": th,
                      "algorithm": ("dense-matrix Dijkstra, O(V^2) per source" if dense else
@@ -200,10 +205,9 @@ def init_strong_router(local, dev):
     """RCCL-backed router for the multi-GPU build, with an agreed go/no-go on every rank: librccl
     must load everywhere before the collective init, and a small multi-rank build must equal the
     single-GPU build bit for bit.  (None, reason) -> the caller runs independent replicas."""
-    import numpy as np
     import torch
     import torch.distributed as dist
-    from shadow_amd import Router, synth
+    from shadow_amd import Router, gate
     from shadow_amd import dist as sd
 
     def agree(ok):
@@ -226,18 +230,17 @@ def init_strong_router(local, dev):
         router = None
     if not agree(router is not None):
         return None, "RCCL communicator init failed"
-    g = synth.random_graph(300, 0.05, 1234, lat_hi=1000)
-    nodes = list(range(300))
+    # the same gate as the one-process rank group (shadow_amd.gate): dense, symmetric-FW and sparse
+    # builds through the communicator equal to this GPU alone, bit for bit, on every rank
+    single = Router(local)
     try:
-        got = router.compute_shortest_paths(g, nodes)
-        ref = Router(local).compute_shortest_paths(g, nodes)
-        ok = np.array_equal(got.latency_ns, ref.latency_ns) and np.array_equal(
-            got.packet_loss.view(np.uint32), ref.packet_loss.view(np.uint32))
-    except Exception as e:  # noqa: BLE001
-        log(f"multi-rank sanity build: {e}")
-        ok = False
+        ok, why = gate.compare_builds(router.compute_shortest_paths, single.compute_shortest_paths, gate.gate_cases())
+    finally:
+        single.close()
+    if not ok:
+        log(f"multi-rank sanity build: {why}")
     if not agree(ok):
-        return None, "multi-rank sanity check failed"
+        return None, "multi-rank sanity check failed" + (f" ({why})" if why else "")
     return router, None
 
 
@@ -414,7 +417,8 @@ def routing_info_times(edges, V, args, steps=3):
             "host_register_ms": {"cold": round(cold_reg, 2), "steady": round(st["ms_host_register"], 2)}, **create}
 
 
-def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg, extra):
+def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg, extra, scaling=None,
+         steps_ms=None):
     n = args.steps
     brk = ("ms_h2d", "ms_build", "ms_fw", "ms_scan", "ms_loss", "ms_extract", "ms_exchange", "ms_d2h", "ms_total")
     entry_desc = ("host entry srg_compute_shortest_paths: host edge list in, host n x n table out "
@@ -423,12 +427,14 @@ def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, rooflin
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "source-SSSPs/s", "n_gpus": world, "steps": n,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+        "scaling": scaling or ("strong" if world > 1 else "weak"), "vs_baseline": None,
         "dtype": "u64+f32" if kind == 1 else "u32+f32", "data": "synthetic",
         "config": {"workload": f"{gdesc}, all {V} nodes used, {entry_desc}", "entry": args.entry, "vertices": V,
                    "edges": int(edges.num_edges), "global_batch": V,
                    "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind)), **extra_cfg},
         "apsp_wall_ms": round(ms_per_step, 3),
+        # per-step wall times of the timed loop (this rank's clock; value uses the whole loop's max over ranks)
+        "step_ms": steps_ms,
         "ms_h2d": round(agg.get("ms_h2d", 0) / n, 3), "ms_d2h": round(agg.get("ms_d2h", 0) / n, 3),
         "d2h_overlapped_GB": round(agg.get("d2h_overlapped_bytes", 0) / n / 1e9, 3),
         # page-locking of the caller's output rows on a helper thread (hidden unless it outlasts
@@ -441,6 +447,14 @@ def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, rooflin
         "roofline": roofline, "cpu_baseline": cpu, **extra,
     }
     print(json.dumps(line), flush=True)
+
+
+def step_stats(ts):
+    """median of the timed steps (>= 5 after 1 warm-up by default) plus min / max, ms."""
+    import numpy as np
+    a = np.asarray(ts, dtype=np.float64) * 1e3
+    return {"median": round(float(np.median(a)), 3), "min": round(float(a.min()), 3), "max": round(float(a.max()), 3),
+            "all": [round(float(x), 3) for x in a]}
 
 
 def run_steps(step, args, label):
@@ -473,6 +487,12 @@ def bench_multi(args):
     edges, gdesc, seed = make_edges(args)
     V = args.vertices
     log(f"[multi{G}] generated {gdesc}: {edges.num_edges} edges")
+    # go/no-go before anything is timed: small builds through the rank group must equal one GPU's
+    # bit for bit (mod.rs:219: a table is whole or an error); otherwise independent replicas, labelled
+    ok, reason = multi_gate(G, args)
+    if not ok:
+        log(f"[multi{G}] multi-device build refused by the gate ({reason}): running {G} independent replicas")
+        return bench_replicas_inproc(args, G, edges, gdesc, seed, reason)
     router, cold_ms = cold_call(lambda: MultiRouter(list(range(G))), args, edges, V)
     log(f"[multi{G}] cold call (srg_multi_create + first call, unfaulted outputs): {cold_ms:.1f} ms")
     h_nodes = np.arange(V, dtype=np.uint32)
@@ -489,9 +509,12 @@ def bench_multi(args):
     for d in range(G):
         torch.cuda.synchronize(d)
     agg = {}
+    ts = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        t1 = time.perf_counter()
         s = step()
+        ts.append(time.perf_counter() - t1)
         for k, v in s.items():
             if isinstance(v, (int, float)):
                 agg[k] = agg.get(k, 0) + v
@@ -505,7 +528,80 @@ def bench_multi(args):
          {"parallelism": f"multi{G} (one process, srg_multi: in-process group, pull collectives over xGMI)",
           "output": "full table in one host array (each GPU writes its sources' rows over its own PCIe link)",
           "cold_call_ms": round(cold_ms, 1)},
-         {"verified_rows": ver})
+         {"verified_rows": ver}, steps_ms=step_stats(ts))
+
+
+def multi_gate(G, args):
+    """(ok, reason): the in-process rank group over G devices against device 0 alone
+    (shadow_amd.gate: dense, symmetric-FW and sparse cases, latency and loss bit for bit)."""
+    from shadow_amd import MultiRouter, Router, gate
+    multi = single = None
+    try:
+        multi = MultiRouter(list(range(G)))
+        single = Router(0)
+        for r in (multi, single):
+            apply_options(r, args)
+        return gate.compare_builds(multi.compute_shortest_paths, single.compute_shortest_paths, gate.gate_cases())
+    except Exception as e:  # noqa: BLE001
+        return False, f"rank group setup: {type(e).__name__}: {e}"
+    finally:
+        for r in (multi, single):
+            if r is not None:
+                r.close()
+
+
+def bench_replicas_inproc(args, G, edges, gdesc, seed, reason):
+    """Fallback of bench_multi: G independent full builds per step, one per device, each on a host
+    thread of its own (the C ABI releases the GIL), each into its own host table: weak scaling."""
+    import threading
+
+    import numpy as np
+    from shadow_amd import Router
+    from shadow_amd import _native as N
+    V = args.vertices
+    routers = [Router(d) for d in range(G)]
+    for r in routers:
+        apply_options(r, args)
+    h_nodes = np.arange(V, dtype=np.uint32)
+    tabs = [(np.zeros((V, V), dtype=np.uint64), np.zeros((V, V), dtype=np.float32)) for _ in range(G)]
+    stats = [None] * G
+
+    def one(d):
+        stats[d] = routers[d].compute_shortest_paths(edges, h_nodes, tabs[d][0], tabs[d][1]).stats
+
+    def step():
+        th = [threading.Thread(target=one, args=(d,)) for d in range(G)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if any(x is None for x in stats):
+            raise RuntimeError("a replica build failed")
+        return stats[0]
+
+    s = run_steps(step, args, f"replicas{G}")
+    routers[0].set_option(N.SRG_OPT_PROFILING, 0 if args.no_profile else 1)
+    agg = {}
+    ts = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t1 = time.perf_counter()
+        s = step()
+        ts.append(time.perf_counter() - t1)
+        for k, v in s.items():
+            if isinstance(v, (int, float)):
+                agg[k] = agg.get(k, 0) + v
+    elapsed = time.perf_counter() - t0
+    ms = elapsed * 1e3 / args.steps
+    kind = s["path_kind"]
+    ver = verify_rows(edges, tabs[0][0], tabs[0][1], V) if not args.no_verify else None
+    roof = roofline_for(agg, kind, args, edges, V, workload_key(args, V, seed, 1), kind == 0
+                        and args.fw_symmetric != 0 and not edges.directed)
+    emit(args, V, gdesc, edges, kind, G, G * V * args.steps / elapsed, ms, agg, s, roof, None,
+         {"parallelism": f"replicas{G} (one process, one full build per GPU per step)", "fallback": reason},
+         {"verified_rows": ver}, scaling="weak", steps_ms=step_stats(ts))
+    for r in routers:
+        r.close()
 
 
 def shared_table(V, rank, tag):
@@ -678,9 +774,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     agg = {}
+    ts = []
     t_start = time.perf_counter()
     for i in range(args.steps):
+        t1 = time.perf_counter()
         s = step()
+        if args.entry != "host":
+            torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t1)
         for k, v in s.items():
             if isinstance(v, (int, float)):
                 agg[k] = agg.get(k, 0) + v
@@ -760,7 +861,7 @@ def main():
                 extra_cfg["cold_call_breakdown_ms"] = dict(COLD_BREAKDOWN)
         emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, roofline, cpu, extra_cfg,
              {"device_entry_ms": round(dev_ms, 3) if dev_ms is not None else None, "verified_rows": ver,
-              "routing_info": ri_times})
+              "routing_info": ri_times}, steps_ms=step_stats(ts))
     if world > 1:
         dist.barrier()
         if shm is not None and rank == 0:

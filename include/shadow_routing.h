@@ -198,7 +198,9 @@ void srg_destroy(srg_ctx* ctx);
                                      * (s, d), s <= d -- a GML complete graph: each block-row of W is split and
                                      * caught up on the pivots already run as soon as its edges have landed);
                                      * 0 = FW after the whole list (any list falls back to that by itself) */
-#define SRG_OPT_TEST_FAULT 34         /* TEST HOOK ONLY (never set in production): 1 = overwrite the closed FW matrix
+#define SRG_OPT_TEST_FAULT 34         /* TEST BUILD ONLY: compiled in only with -DSRG_TEST_HOOKS (the test library
+                                     * libshadow_routing_testhooks.so); the product library refuses any value
+                                     * but 0 with SRG_ERR_ARG.  1 = overwrite the closed FW matrix
                                      * with zeros after FW (a lost synchronisation's result: the build must fail
                                      * with SRG_ERR_INTERNAL, not return it); 2 = nonzero FW sync words and zero
                                      * line buffers before each symmetric FW (a recycled allocation: the build
@@ -206,7 +208,10 @@ void srg_destroy(srg_ctx* ctx);
 #define SRG_OPT_TABLE_POOL_BYTES 35  /* RoutingInfo tables (srg_routing_info_build, one rank) come from a pool of
                                      * page-locked host tables on the context; freeing a RoutingInfo returns
                                      * them, so the next build skips the prefault + page-locking.  Bytes of idle
-                                     * tables the pool keeps (default 8 GiB; 0 = free them at once) */
+                                     * tables the pool keeps (default: no byte cap, only the most recently freed
+                                     * table pair; setting a byte cap replaces that count cap; 0 = free them at
+                                     * once).  Idle tables stay page-locked (not reclaimable by the OS) until
+                                     * reused, trimmed or srg_destroy */
 #define SRG_OPT_TABLE_POOL_IDLE_BYTES 36  /* read-only: bytes of idle tables the pool holds now */
 #define SRG_OPT_CREATE_MS_RUNTIME 37  /* read-only: srg_create's HIP-runtime part (device count, device context,
                                       * the first stream, where the runtime initialises the device: the first

@@ -25,7 +25,7 @@ namespace srg {
 inline void narrow_block(const uint32_t* src, const uint32_t* dst, const uint64_t* lat, uint32_t* hl, size_t b0,
                          size_t b1, uint64_t& ol, uint32_t& ox) {
     size_t i = b0;
-#if defined(__clang__)
+#if defined(__clang__) && (defined(__x86_64__) || defined(__i386__))
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     typedef uint64_t v4q __attribute__((ext_vector_type(4)));
     for (; i < b1 && ((uintptr_t)(hl + i) & 15); ++i) {  // head up to a 16-B boundary of the ring
@@ -68,7 +68,7 @@ inline bool seq_encode_slice(const uint32_t* src, const uint32_t* dst, const uin
         ex.push_back(dst[i]);
         dense = ex.size() > cap;  // (then latencies and checks only)
     };
-#if defined(__clang__)
+#if defined(__clang__) && (defined(__x86_64__) || defined(__i386__))
     // one pass: 4 edges per step, the narrowed latencies stored non-temporally (narrow_block), the
     // exception test on the same registers against the edges one back; a step with an exception
     // (C3: one in ~670 edges) records it in order.  (A separate flag pass over each 1 K block read

@@ -35,4 +35,16 @@ SRG_GUARD_HD inline uint64_t min_edge_key(unsigned long long min_lat_inv, uint64
     return unit > 1 ? mn / unit : mn;
 }
 
+// The symmetric FW's timeout word (zeroed per build; the first raiser's code stays, later raisers
+// compare-and-swap from 0): 1 = a pivot-closure grid barrier, 2 = a cross-stream value hop,
+// 3 = a line-exchange wait for a peer's arrival word (xchg.hip.h poll_until).  The host reports the
+// kernel that gave up, so a hang is looked for where it happened.
+inline const char* fw_timeout_message(uint32_t code) {
+    switch (code) {
+        case 2: return "FW chain: a cross-stream hop waited past its bound (mis-ordered enqueue)";
+        case 3: return "FW line exchange: a peer's arrival word did not come within the bound (peer stalled or gone)";
+        default: return "FW pivot closure: a grid barrier timed out (workgroups not co-resident)";
+    }
+}
+
 }  // namespace srg

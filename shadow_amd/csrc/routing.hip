@@ -43,6 +43,7 @@
 #include "tight_sparse.hip.h"
 #include "comm.h"
 #include "sparse.hip.h"
+#include "sparse_ds.hip.h"
 #include "events.hip.h"
 #include "xchg.hip.h"
 
@@ -644,6 +645,7 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 // (the caller is worker 0) and returns when all are done.
 struct HostPool {
     std::vector<std::thread> th;
+    std::mutex run_mu;  // one job at a time: job / pending / gen are shared (callers on several threads queue)
     std::mutex mu;
     std::condition_variable cv, done_cv;
     std::function<void(int, int)> job;
@@ -671,6 +673,7 @@ struct HostPool {
             });
     }
     void run(const std::function<void(int, int)>& f) {
+        std::lock_guard<std::mutex> serial(run_mu);
         {
             std::lock_guard<std::mutex> lk(mu);
             job = f;
@@ -758,11 +761,15 @@ struct TablePool {
     std::mutex mu;
     std::vector<srg_table*> idle;
     size_t idle_bytes = 0;
-    size_t limit = (size_t)8 << 30;  // idle bytes kept (SRG_OPT_TABLE_POOL_BYTES)
+    // idle bytes kept (SRG_OPT_TABLE_POOL_BYTES); by default no byte cap but only the most recently
+    // freed pair (a RoutingInfo's latency + loss tables): page-locked memory the OS cannot reclaim
+    // stays bounded by one table set per context
+    size_t limit = ~(size_t)0;
+    size_t max_idle = 2;  // idle tables kept (0 = no count cap once a byte cap is set)
     bool open = true;
     static void destroy(srg_table* t);
     void trim_locked(size_t keep) {  // the oldest idle tables first
-        while (idle_bytes > keep && !idle.empty()) {
+        while ((idle_bytes > keep || (max_idle && idle.size() > max_idle)) && !idle.empty()) {
             srg_table* t = idle.front();
             idle.erase(idle.begin());
             idle_bytes -= t->cap;
@@ -1796,6 +1803,7 @@ struct SymFw {
         // timeout word; zeroed per build (a multiple of 16 bytes from the allocation's start)
         cflags = (uint32_t*)c.b_cflags.get(((size_t)nb * 16 + 4) * 4);
         c.fw_timeout = cflags + (size_t)nb * 16;
+#ifdef SRG_TEST_HOOKS
         if (c.test_fault == 2) {
             // TEST HOOK: the state of a recycled allocation -- nonzero sync words, zero line buffers --
             // in place before this build's reset (the value-hop race of rounds 3-4, stream_hop)
@@ -1803,6 +1811,7 @@ struct SymFw {
             if (keep_lines) HIP_CHECK(hipMemsetAsync(lball, 0, (size_t)nb * nb * TT * sizeof(K), c.aux_stream));
             HIP_CHECK(hipStreamSynchronize(c.aux_stream));
         }
+#endif
         HIP_CHECK(hipMemsetAsync(cflags, 0, ((size_t)nb * 16 + 4) * 4, st));
         // the chain stream's kernels (hop waits, closures, the exchange) read and count in these
         // words: the chain stream waits for their reset by an EVENT (a value hop's wait kernel would
@@ -2339,11 +2348,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
     if (sym_fw_for<K, T>(c, g)) rb_async(c, MS_TIMEOUT, c.fw_timeout, st);  // read after FW, on its stream
     const double ms_fw = tm.lap();
     if (sym_fw_for<K, T>(c, g) && rb_get<uint32_t>(c, MS_TIMEOUT))
-        fail(SRG_ERR_HIP, rb_get<uint32_t>(c, MS_TIMEOUT) == 2
-                              ? "FW chain: a cross-stream hop waited past its bound (mis-ordered enqueue)"
-                              : "FW pivot closure: a grid barrier timed out (workgroups not co-resident)");
+        fail(SRG_ERR_HIP, fw_timeout_message(rb_get<uint32_t>(c, MS_TIMEOUT)));
+#ifdef SRG_TEST_HOOKS
     if (c.test_fault == 1)  // TEST HOOK (SRG_OPT_TEST_FAULT): a lost synchronisation's result, for the guard
         HIP_CHECK(hipMemsetAsync(D, 0, VV * sizeof(K), st));
+#endif
     if (wl_late) {
         // WL = min loss among the min-latency parallel edges (what k_w_split gives), from the
         // losses that crossed PCIe during FW.  Built here, after FW, rather than beside it: on a
@@ -2541,7 +2550,10 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
 
     // latency outputs (+ diagonal self-loops) of the own rows, right after FW
     HIP_CHECK(hipMemsetAsync(&P.flags->unreachable_used_pair, 0, 4, st));
-    if (nloc && P.ident && n % 4 == 0)
+    // k_extract_ident moves rows by 16-B vectors: the caller's arrays (a device-entry torch view may be
+    // offset) must be 16-B aligned too (row offsets are, since n % 4 == 0)
+    const bool al16 = (((uintptr_t)out_lat | (uintptr_t)c.kout_key) & 15u) == 0;
+    if (nloc && P.ident && n % 4 == 0 && al16)
         k_extract_ident<K><<<nloc, 256, 0, st>>>(D, Vp, lnodes, n, P.selflat, out_lat, P.flags, P.unit, c.kout_key,
                                                  c.kout_diag);
     else if (nloc)
@@ -2908,8 +2920,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     uint32_t* d_brow = (uint32_t*)c.b_lpos.get(brow.size() * 4);
     HIP_CHECK(hipMemcpyAsync(d_bsrc, bsrc.data(), bsrc.size() * 4, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_brow, brow.data(), brow.size() * 4, hipMemcpyHostToDevice, st));
-    uint32_t* fl = (uint32_t*)c.b_red.get(64);
-    HIP_CHECK(hipMemsetAsync(fl, 0, 64, st));
+    uint32_t* fl = (uint32_t*)c.b_red.get(128);
+    HIP_CHECK(hipMemsetAsync(fl, 0, 128, st));
     HIP_CHECK(hipGetLastError());
     const double ms_build = tm.lap();
 
@@ -2919,16 +2931,25 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     const int wpc = wide ? 1 : 2;
     uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nbatch, (uint32_t)dev_cus * (uint32_t)wpc));
 
-    // label slots (V x 64 x 8 B per resident batch, 16 B when wide) within about half of the free HBM
+    // u32 latency keys take the two-phase kernel (latency-only delta-stepping, then the loss fold
+    // over the tight arcs, sparse_ds.hip.h); wide labels keep the lexicographic sweeps.
+    // SRG_SPARSE_KERNEL=bf selects the lexicographic sweeps for u32 keys too (A/B)
+    const char* sk = std::getenv("SRG_SPARSE_KERNEL");
+    const bool two_phase = !wide && !(sk && std::strcmp(sk, "bf") == 0);
+    // per resident batch: labels V x 64 x 8 B (16 B wide); two-phase: u32 latency + f32 loss
+    // labels, a u64 tight mask per arc and a u64 final-lane mask per vertex
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t slot_bytes = (size_t)V * 64 * (wide ? 16 : 8);
-    grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes, 1)));
+    const size_t slot_bytes = (size_t)V * 64 * (wide ? 16 : two_phase ? 4 : 8);
+    const size_t ds_extra = two_phase ? (size_t)V * 64 * 4 + (size_t)std::max<uint32_t>(arcs, 1) * 8 + (size_t)V * 8 : 0;
+    grid = (uint32_t)std::max<size_t>(
+        1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes + ds_extra, 1)));
     const uint32_t nwv = (V + 63) / 64;
-    const size_t bitmap_bytes = (size_t)nwv * 5 * 8;
+    const size_t bitmap_bytes = two_phase ? ds_state_bytes(V) : (size_t)nwv * 5 * 8;
+    const size_t scr_bytes = two_phase ? ds_scratch_bytes() : sp_scratch_bytes();
     // bitmaps in LDS while a CU still fits the requested workgroups, else in global memory
-    const bool gbits = c.sparse_global_bitmaps || bitmap_bytes + sp_scratch_bytes() > (size_t)160 * 1024 / wpc;
-    const size_t lds = (gbits ? 0 : bitmap_bytes) + sp_scratch_bytes();
+    const bool gbits = c.sparse_global_bitmaps || bitmap_bytes + scr_bytes > (size_t)160 * 1024 / wpc;
+    const size_t lds = (gbits ? 0 : bitmap_bytes) + scr_bytes;
     if (nbatch) {
         unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * slot_bytes);
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
@@ -2938,10 +2959,24 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         // (128 VGPRs, no spills) ran 2.5x / 1.2x slower
         auto kern = gbits ? k_sparse_bf<SP_G, true> : k_sparse_bf<SP_G, false>;
         if (wide) kern = gbits ? k_sparse_bf<SP_G, true, 4, LabelU64> : k_sparse_bf<SP_G, false, 4, LabelU64>;
+        if (two_phase) {
+            // rows in flight per wave (phases 1 / 2a, fold): SRG_DS_G = 8 | 16 | 32 (A/B)
+            const char* gs = std::getenv("SRG_DS_G");
+            const int gsel = gs ? std::atoi(gs) : 8;
+            // (8 rows: 16 and 32 spill more at the 64-VGPR budget and measured 375 / 712 ms against 293
+            // on C4, profiles/r06/sparse_ds/c4_g*.json)
+            kern = gbits ? k_sparse_ds<true, 8, 8> : k_sparse_ds<false, 8, 8>;
+            if (gsel == 16) kern = gbits ? k_sparse_ds<true, 16, 8> : k_sparse_ds<false, 16, 8>;
+        }
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
                      selflat, selfloss, out_lat, out_loss, fl, P.unit, ~0ull, gb, c.kout_key, c.kout_diag,
-                     in_w64, min_edge_key(P.es.min_lat_inv, P.unit)};
+                     in_w64, min_edge_key(P.es.min_lat_inv, P.unit), nullptr, nullptr, nullptr, arcs};
+        if (two_phase) {
+            a.lo_slots = (float*)c.b_WL.get((size_t)grid * V * 64 * 4);
+            a.tmask = (unsigned long long*)c.b_PRED.get((size_t)grid * std::max<uint32_t>(arcs, 1) * 8);
+            a.fmask = (unsigned long long*)c.b_L0.get((size_t)grid * V * 8);
+        }
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
@@ -2960,18 +2995,30 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     // every rank agrees on the outcome before any exchange
     if (multi) {
         c.comm->allreduce_max_u32(fl, 2, st);
-        c.comm->allreduce_max_u32(fl + 5, 2, st);
+        c.comm->allreduce_max_u32(fl + 5, 3, st);  // saturated, impossible, fold incomplete
     }
-    uint32_t hfl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(hfl, fl, 32, hipMemcpyDeviceToHost, st));
+    uint32_t hfl[20] = {};
+    HIP_CHECK(hipMemcpyAsync(hfl, fl, 80, hipMemcpyDeviceToHost, st));
     const double ms_sssp = tm.lap();
+    if (hfl[7])
+        fail(SRG_ERR_INTERNAL, "the sparse build's loss fold left a used pair without a final loss");
     if (hfl[6])
         fail(SRG_ERR_INTERNAL, "the sparse build produced an impossible table: a used pair's latency is below the "
                                "smallest edge latency (" + std::to_string(~P.es.min_lat_inv) + " ns)");
     if (std::getenv("SRG_DEBUG_SPARSE")) {
         const unsigned long long ev = (unsigned long long)hfl[2] | (unsigned long long)hfl[3] << 32;
-        std::fprintf(stderr, "sparse: %u batches, grid %u, max sweeps %u, lane evaluations %llu\n", nbatch, grid,
-                     hfl[1], ev);
+        const unsigned long long p2 = (unsigned long long)hfl[10] | (unsigned long long)hfl[11] << 32;
+        std::fprintf(stderr,
+                     "sparse: %s, %u batches, grid %u, max sweeps %u, lane evaluations %llu, fold sweeps %u, "
+                     "fold row pulls %llu, arcs %u\n",
+                     two_phase ? "two-phase" : "lexicographic", nbatch, grid, hfl[1], ev, hfl[8], p2, arcs);
+        if (two_phase) {  // per-phase wall clock summed over workgroups (100 MHz), as ms per workgroup
+            double t[4];
+            for (int p = 0; p < 4; ++p)
+                t[p] = (double)((unsigned long long)hfl[12 + 2 * p] | (unsigned long long)hfl[13 + 2 * p] << 32) / 1e5 / grid;
+            std::fprintf(stderr, "sparse phases (ms per workgroup): latency %.1f, tight masks %.1f, fold %.1f, output %.1f\n",
+                         t[0], t[1], t[2], t[3]);
+        }
     }
     if (hfl[0]) {
         // a used pair came out INF: only a relaxation that saturated the u32 key can have hidden a
@@ -4130,7 +4177,12 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             ctx->fw_overlap = (int)value;
             return SRG_OK;
         case SRG_OPT_TEST_FAULT:
+            // test hooks exist only in the test build (libshadow_routing_testhooks.so, -DSRG_TEST_HOOKS);
+            // the product library accepts 0 (off) and refuses the rest
             if (value != 0 && value != 1 && value != 2) return SRG_ERR_ARG;
+#ifndef SRG_TEST_HOOKS
+            if (value != 0) return SRG_ERR_ARG;
+#endif
             ctx->test_fault = (int)value;
             return SRG_OK;
         case SRG_OPT_FW_XCD_ORDER:
@@ -4141,6 +4193,7 @@ int srg_set_option(srg_ctx* ctx, int option, double value) {
             if (!(value >= 0.0 && value <= 1e15)) return SRG_ERR_ARG;
             std::lock_guard<std::mutex> pl(ctx->tpool->mu);
             ctx->tpool->limit = (size_t)value;
+            ctx->tpool->max_idle = 0;  // an explicit byte cap replaces the one-pair default
             ctx->tpool->trim_locked(ctx->tpool->limit);
             return SRG_OK;
         }

@@ -196,6 +196,11 @@ struct SparseArgs {
     const uint64_t* in_w64;      // wide labels: u64 arc keys (`slots` then holds 16-byte labels)
     uint64_t min_key;            // smallest arc key: a used off-diagonal latency below it is impossible
                                  // (guards.h) -> flags[6]
+    // two-phase kernel (k_sparse_ds, sparse_ds.hip.h): `slots` then holds u32 latency labels
+    float* lo_slots;             // [gridDim.x][V][64] loss labels
+    unsigned long long* tmask;   // [gridDim.x][arcs] tight-lane masks per in-arc
+    unsigned long long* fmask;   // [gridDim.x][V] final-lane masks of the loss fold
+    uint32_t arcs;
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some dropped lane's new latency is

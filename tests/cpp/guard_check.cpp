@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 #include "../../shadow_amd/csrc/guards.h"
@@ -58,6 +59,11 @@ int main() {
     if (certify<uint64_t>(D64, V, all, all, min_key) || !certify<uint64_t>(Z64, V, all, all, min_key))
         return std::fprintf(stderr, "u64 keys\n"), 1;
     if (srg::min_edge_key(0, unit) != 0) return std::fprintf(stderr, "no edges\n"), 1;
+    // the FW timeout word names the kernel that gave up (code 3 is the line exchange)
+    const std::string m1 = srg::fw_timeout_message(1), m2 = srg::fw_timeout_message(2), m3 = srg::fw_timeout_message(3);
+    if (m1.find("pivot closure") == std::string::npos || m2.find("cross-stream hop") == std::string::npos ||
+        m3.find("line exchange") == std::string::npos || m3.find("arrival word") == std::string::npos)
+        return std::fprintf(stderr, "timeout messages\n"), 1;
     std::printf("ok\n");
     return 0;
 }

@@ -96,6 +96,22 @@ def test_pool_recycles_page_locked_tables():
     r.close()
 
 
+def test_pool_keeps_one_idle_pair_by_default():
+    """Without a byte cap the pool keeps only the most recently freed table pair: two RoutingInfos freed
+    leave the idle bytes of one (page-locked host memory stays bounded per context)."""
+    e = synth.atlas_like(2600, seed=26)
+    ids = list(range(2600))
+    r = Router(0)
+    a = generate_routing_info(e, ids, True, r)
+    b = generate_routing_info(e, ids, True, r)
+    a.close()
+    one = r.get_option(N.SRG_OPT_TABLE_POOL_IDLE_BYTES)
+    assert one >= 2 * 2600 * 2600 * 4
+    b.close()
+    assert r.get_option(N.SRG_OPT_TABLE_POOL_IDLE_BYTES) == one
+    r.close()
+
+
 def test_routing_info_outlives_its_router():
     """A RoutingInfo owns its pooled tables past srg_destroy of the context that built them."""
     e = synth.atlas_like(2600, seed=27)
