@@ -129,9 +129,16 @@ typedef struct srg_stats {
 
 typedef struct srg_ctx srg_ctx; /* opaque: owns device workspace; one HIP device */
 
-/* Create a context bound to HIP device `device` (one process per GPU). */
+/* Create a context bound to HIP device `device` (one process per GPU).  Besides the HIP runtime's
+ * device initialisation it warms what the first host-entry call would otherwise pay on the routing
+ * path: the kernels' code object on the device, each stream's first dispatch, the H2D codec's worker
+ * pool and page-locked rings, the first H2D / D2H / SDMA copies (SRG_CREATE_WARM=0 in the environment
+ * skips that, for A/B).  Shadow creates its context before parsing the GML, so this
+ * runs off the routing path.  Replaces nothing in the reference: the context is the device state that
+ * compute_shortest_paths (mod.rs:183-228) needs and Rust's CPU path does not have. */
 int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen);
 void srg_destroy(srg_ctx* ctx);
+
 
 /* Context options.
  *   SRG_OPT_PROFILING         1 = HIP-event timing of every dominant-kernel launch (stats.prof_*)
@@ -217,7 +224,7 @@ void srg_destroy(srg_ctx* ctx);
                                       * the first stream, where the runtime initialises the device: the first
                                       * context of a process pays the runtime's initialisation) */
 #define SRG_OPT_CREATE_MS_LIBRARY 38  /* read-only: srg_create's own part (three more streams, mailbox, SDMA
-                                      * agents, events) */
+                                      * agents, events, the warm-up) */
 #define SRG_OPT_FW_XCD_ORDER 39      /* symmetric FW bulk launch order: 1 (default) = the tiles dealt to the 8 XCDs as
                                      * Z-order runs, one list per pivot (each XCD a compact block of the triangle,
                                      * its line-buffer operands L2-resident: C3 bulk HBM traffic 1.38x -> 1.12x of

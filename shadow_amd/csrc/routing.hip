@@ -1752,13 +1752,17 @@ struct SymFw {
         // pivot closure is one launch of 64 workgroups either way (fw_close_sq; eight squaring launches
         // took 45-117 us per pivot, the one-workgroup FW closure 159 us beside the bulk: r03b/).
         const int bulk_tiles = nb * (nb + 1) / 2 / G;
-        split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 1024 ? 2 : 4;
+        // (C2, nb = 32, 528 tiles: quadrant lines, host entry 7.16-7.27 vs 7.39-8.76 ms with 32 x 32,
+        // profiles/r06/c2/)
+        split = c.fw_line_split ? c.fw_line_split : bulk_tiles >= 2048 ? 1 : bulk_tiles >= 512 ? 2 : 4;
         // a bulk below one round of the slots (3 per CU) runs as quadrants (fw_bulk_lb_q): sim 8:0
         // bulk launch 59.5 -> 48.6 us, FW 6.24-6.28 -> 6.02-6.04 ms (profiles/r05/chain/)
-        if (sizeof(K) == 4 && T == 128 && G > 1) {
+        // (one rank too: C2, nb = 32, 528 tiles; SRG_FW_BULK_Q = 0 / 1 forces it off / on for A/B)
+        const char* bq = std::getenv("SRG_FW_BULK_Q");
+        if (sizeof(K) == 4 && T == 128 && !(bq && bq[0] == '0')) {
             int cus = 256;
             HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
-            if (bulk_tiles < 3 * cus) {
+            if (bulk_tiles < 3 * cus || (bq && bq[0] == '1')) {
                 bulk_split = 2;
                 set_lds(fw_bulk_lb_q<K, T, 32>, lb_lds<K, T / 2, 32>());
             }
@@ -3353,6 +3357,33 @@ T* stage_in(DevBuf& b, const T* host, size_t count, hipStream_t st) {
 // all_seq: every chunk of the slice went sequential-pair: its u32 latencies are in b_n32l and its
 // exceptions (GLOBAL edge index, src, dst) in c.slice_exc -- the edge-sharded exchange then ships
 // that form (4 B per edge) instead of the u16 narrowing (8 B).
+// the host entry's codec worker pool and its page-locked rings (first use, or srg_create's warm-up)
+constexpr size_t kCodecChunk = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
+constexpr int kRingSlots = 3;
+void ensure_pool(srg_ctx& c) {
+    if (c.pool) return;
+    c.pool = new HostPool();
+    const unsigned hw = std::thread::hardware_concurrency();
+    int nt = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+    if (const char* e = std::getenv("SRG_CODEC_THREADS")) nt = std::max(1, std::atoi(e));  // experiments
+    c.pool->start(nt);
+}
+void ensure_rings(srg_ctx& c) {
+    const size_t slot = kCodecChunk * 16;
+    if (c.h_ring_bytes < slot * kRingSlots) {
+        if (c.h_ring) HIP_CHECK(hipHostFree(c.h_ring));
+        c.h_ring = nullptr;
+        c.h_ring_bytes = 0;
+        HIP_CHECK(hipHostMalloc(&c.h_ring, slot * kRingSlots, hipHostMallocDefault));
+        c.h_ring_bytes = slot * kRingSlots;
+    }
+    for (hipEvent_t& e : c.ev_ring)
+        if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c.h_lring) HIP_CHECK(hipHostMalloc(&c.h_lring, kCodecChunk * 4 * kRingSlots, hipHostMallocDefault));
+    for (hipEvent_t* e : {&c.ev_lring[0], &c.ev_lring[1], &c.ev_lring[2], &c.ev_lin, &c.ev_ldone})
+        if (!*e) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+}
+
 bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, size_t a0, size_t a1, bool with_loss,
               bool& all_narrow, bool& all_seq, const ChunkFn& on_chunk) {
     all_narrow = true;
@@ -3360,25 +3391,11 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
     c.slice_exc.clear();
     const auto t_setup = std::chrono::steady_clock::now();
     const size_t E = g->num_edges, A = a1 - a0;
-    constexpr size_t CE = (size_t)2 << 20;  // edges per chunk: 32 MB narrowed (+ loss)
-    constexpr int NB = 3;                   // ring slots
+    constexpr size_t CE = kCodecChunk;  // edges per chunk: 32 MB narrowed (+ loss)
+    constexpr int NB = kRingSlots;      // ring slots
     const size_t slot = CE * 16;
-    if (!c.pool) {
-        c.pool = new HostPool();
-        const unsigned hw = std::thread::hardware_concurrency();
-        int nt = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
-        if (const char* e = std::getenv("SRG_CODEC_THREADS")) nt = std::max(1, std::atoi(e));  // experiments
-        c.pool->start(nt);
-    }
-    if (c.h_ring_bytes < slot * NB) {
-        if (c.h_ring) HIP_CHECK(hipHostFree(c.h_ring));
-        c.h_ring = nullptr;
-        c.h_ring_bytes = 0;
-        HIP_CHECK(hipHostMalloc(&c.h_ring, slot * NB, hipHostMallocDefault));
-        c.h_ring_bytes = slot * NB;
-    }
-    for (hipEvent_t& e : c.ev_ring)
-        if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ensure_pool(c);
+    ensure_rings(c);
     uint16_t* s16 = (uint16_t*)c.b_n16s.get(E * 2);
     uint16_t* d16 = (uint16_t*)c.b_n16d.get(E * 2);
     uint32_t* l32 = (uint32_t*)c.b_n32l.get(E * 4);
@@ -3528,11 +3545,9 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
 // share the PCIe link); loss_arrive() later joins it and orders the readers after the last DMA.
 void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, LateLoss& L, size_t a0 = 0,
                      size_t a1 = ~(size_t)0) {
-    constexpr size_t CE = (size_t)2 << 20;
-    constexpr int NB = 3;
-    if (!c.h_lring) HIP_CHECK(hipHostMalloc(&c.h_lring, CE * 4 * NB, hipHostMallocDefault));
-    for (hipEvent_t* e : {&c.ev_lring[0], &c.ev_lring[1], &c.ev_lring[2], &c.ev_lin, &c.ev_ldone})
-        if (!*e) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    constexpr size_t CE = kCodecChunk;
+    constexpr int NB = kRingSlots;
+    ensure_rings(c);
     L.ev_in = c.ev_lin;
     L.ev_done = c.ev_ldone;
     HIP_CHECK(hipEventRecord(c.ev_ledges, st));
@@ -4021,6 +4036,36 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
 
 extern "C" {
 
+__global__ void k_warm(uint32_t* p) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) p[0] = 0;
+}
+
+// srg_create's warm-up (SRG_CREATE_WARM=0 skips it, for A/B): what the first host-entry call would
+// otherwise pay on the routing path -- the code object's load on the device (the first launch), each
+// stream's first dispatch, the codec worker pool, the page-locked H2D rings (96 + 24 MB), the first
+// copy of each kind (H2D and D2H by the runtime, D2H on the SDMA engine).  Shadow creates its context
+// before parsing the GML, so this runs off the routing path.
+void warm_context(srg_ctx& c) {
+    ensure_pool(c);
+    ensure_rings(c);
+    uint32_t* d = (uint32_t*)c.b_red.get(128);
+    const hipStream_t ss[4] = {c.stream, c.aux_stream, c.comm_stream, c.d2h_stream};
+    for (hipStream_t s : ss) k_warm<<<1, 64, 0, s>>>(d);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(d, c.h_ring, 64, hipMemcpyHostToDevice, c.comm_stream));
+    HIP_CHECK(hipMemcpyAsync(c.h_lring, d + 16, 64, hipMemcpyDeviceToHost, c.d2h_stream));
+    for (hipStream_t s : ss) HIP_CHECK(hipStreamSynchronize(s));
+    if (c.sdma.ok) {
+        hsa_signal_t sg;
+        if (hsa_signal_create(1, 0, nullptr, &sg) == HSA_STATUS_SUCCESS) {
+            if (hsa_amd_memory_async_copy_on_engine(c.h_ring, c.sdma.cpu, d, c.sdma.gpu, 64, 0, nullptr, sg,
+                                                    (hsa_amd_sdma_engine_id_t)c.sdma.engine, true) == HSA_STATUS_SUCCESS)
+                hsa_signal_wait_scacquire(sg, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            hsa_signal_destroy(sg);
+        }
+    }
+}
+
 int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
     if (!out) {
         set_err(errbuf, errlen, "null argument");
@@ -4083,6 +4128,11 @@ int srg_create(srg_ctx** out, int device, char* errbuf, size_t errlen) {
             HIP_CHECK(hipStreamSynchronize(c->stream));
         }
         lap("events, signals");
+        const char* wv_env = std::getenv("SRG_CREATE_WARM");
+        if (!(wv_env && wv_env[0] == '0')) {
+            warm_context(*c);
+            lap("warm-up (module, rings, copies)");
+        }
         c->ms_create_lib = ms_since(tlib);
         std::lock_guard<std::mutex> lk(g_dev_mu);
         ++g_dev_ctx[device];

@@ -303,10 +303,8 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
             const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q]);
             const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane(goff[q + 1]);
             const uint32_t vb = (k & 1u) * (V5_UC * V5_SB * 4u) + lane * 8u;
-            if (p0 < p1) {
-                V5Grp cur = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)p0);
-                for (uint32_t p = p0; p < p1; p += 4) {
-                    const V5Grp nxt = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p + 4));
+            // one 4-pair group: 8 staged-row reads, 16 checks per lane, the hit test
+            auto group = [&](const V5Grp& cur, uint32_t p) {
                     uint2 A[8];
 #pragma unroll
                     for (uint32_t i = 0; i < 4; ++i) {
@@ -332,7 +330,21 @@ __global__ void __launch_bounds__(512, 4) tight_v5(const uint32_t* __restrict__ 
                             sth[tl] = sh;
                         }
                     }
-                    cur = nxt;
+            };
+            // two record groups in flight in two fixed SGPR sets, loop unrolled by 2: no 16-register
+            // copy of the prefetched group per iteration and half the loop-counter work (both were
+            // scalar instructions of the loop, which issues more SALU than the CU's one per cycle
+            // covers at 16 waves: 1.73e9 SALU per C3 launch, profiles/r05/scan_v6/)
+            if (p0 < p1) {
+                V5Grp ga = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)p0);
+                V5Grp gb = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p0 + 4));
+                for (uint32_t p = p0;; p += 8) {
+                    group(ga, p);
+                    if (p + 4 >= p1) break;
+                    ga = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p + 8));
+                    group(gb, p + 4);
+                    if (p + 8 >= p1) break;
+                    gb = *reinterpret_cast<const V5Grp*>(rec + 4 * (size_t)(p + 12));
                 }
             }
         }
