@@ -3478,9 +3478,13 @@ bool codec_in(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream_t st, 
             HIP_CHECK(hipStreamSynchronize(st));  // no DMA may still read the ring
             return false;
         }
-        // the host is busy (narrowing this chunk took longer than shipping it plain would at
-        // ~55 GB/s): the remaining edges go plain, straight from the caller's arrays
-        bool slow = ch + 1 < nch && dt > (double)ne * 20.0 / 55e9 * 1e3;
+        // the host is busy (narrowing takes longer than shipping the chunks plain would at ~55 GB/s):
+        // the remaining edges go plain, straight from the caller's arrays.  Judged on the average over
+        // the chunks so far, past the first, with a 1.5x margin: shipping plain also gives up the FW
+        // beside the H2D (~5 ms at C3), and a single chunk slowed by the caller's fresh table being
+        // faulted in beside it (0.79 ms against 0.76) switched a C3 first call over (round 6)
+        const double plain_ms = (double)ne * 20.0 / 55e9 * 1e3;
+        bool slow = ch + 1 < nch && ch >= 1 && t_conv / (double)(ch + 1) > 1.5 * plain_ms;
         if (const char* f = std::getenv("SRG_CODEC_SLOW_AFTER")) slow = ch + 1 < nch && ch >= (size_t)std::atoll(f);  // tests
         if (chunk_seq) {
             // the workers' exception lists, in order, as SoA (index | src | dst) where the u16

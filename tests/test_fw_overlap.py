@@ -44,6 +44,10 @@ def test_overlap_matches_after_h2d(V, order, monkeypatch, capfd):
         e = gml_order(e)
     nodes = list(range(V))
     monkeypatch.setenv("SRG_DEBUG_OVERLAP", "1")
+    # (the codec's host-slow switch ships the rest plain when narrowing a chunk takes longer than
+    # shipping it would -- a busy shared host -- and the overlap then falls back by design; this test
+    # is about the overlap's result, so the switch is held off)
+    monkeypatch.setenv("SRG_CODEC_SLOW_AFTER", "1000000")
     t1 = build(e, nodes, 1)
     err = capfd.readouterr().err
     assert "fw-overlap: ok=1" in err, err
@@ -60,6 +64,7 @@ def test_overlap_subset_nodes_and_pivots_during_h2d(monkeypatch, capfd):
     e = synth.atlas_like(V, seed=77)
     nodes = np.random.default_rng(5).permutation(V)[: V // 3].tolist()
     monkeypatch.setenv("SRG_DEBUG_OVERLAP", "1")
+    monkeypatch.setenv("SRG_CODEC_SLOW_AFTER", "1000000")  # (as above)
     t1 = build(e, nodes, 1)
     err = capfd.readouterr().err
     early = int(err.split("pivots_during_h2d=")[1].split()[0])
@@ -146,7 +151,7 @@ def test_fault_hooks_in_the_test_build():
         r.set_option(N.SRG_OPT_TEST_FAULT, 1)
     assert ei.value.code == N.SRG_ERR_ARG
     r.close()
-    env = dict(os.environ, SRG_LIB_PATH=lib, SRG_DEBUG_OVERLAP="1")
+    env = dict(os.environ, SRG_LIB_PATH=lib, SRG_DEBUG_OVERLAP="1", SRG_CODEC_SLOW_AFTER="1000000")
     p = subprocess.run([sys.executable, "-u", os.path.join(here, "fault_hooks_run.py")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout[-2000:] + p.stderr[-4000:]
