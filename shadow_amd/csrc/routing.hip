@@ -2945,7 +2945,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     size_t free_b = 0, total_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const size_t slot_bytes = (size_t)V * 64 * (wide ? 16 : two_phase ? 4 : 8);
-    const size_t ds_extra = two_phase ? (size_t)V * 64 * 4 + (size_t)std::max<uint32_t>(arcs, 1) * 8 + (size_t)V * 8 : 0;
+    const size_t ds_extra = two_phase ? (size_t)V * 64 * 4 + (size_t)std::max<uint32_t>(arcs, 1) * 16 + (size_t)V * 16 : 0;
     grid = (uint32_t)std::max<size_t>(
         1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes + ds_extra, 1)));
     const uint32_t nwv = (V + 63) / 64;
@@ -2978,8 +2978,9 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                      in_w64, min_edge_key(P.es.min_lat_inv, P.unit), nullptr, nullptr, nullptr, arcs};
         if (two_phase) {
             a.lo_slots = (float*)c.b_WL.get((size_t)grid * V * 64 * 4);
-            a.tmask = (unsigned long long*)c.b_PRED.get((size_t)grid * std::max<uint32_t>(arcs, 1) * 8);
-            a.fmask = (unsigned long long*)c.b_L0.get((size_t)grid * V * 8);
+            // tight records (16 B per in-arc slot), final-lane masks + tight-record counts (16 B per vertex)
+            a.tmask = (unsigned long long*)c.b_PRED.get((size_t)grid * std::max<uint32_t>(arcs, 1) * 16);
+            a.fmask = (unsigned long long*)c.b_L0.get((size_t)grid * V * 16);
         }
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)

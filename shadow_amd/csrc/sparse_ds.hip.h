@@ -14,9 +14,11 @@
 //            The marks are wavefront-aggregated: a 64-vertex window that receives its first mark
 //            is appended to the next sweep's window list with one ballot and one LDS atomic per
 //            wave, and a sweep walks only that list.
-//   phase 2a tight masks: per in-arc k = (u, t) the 64-bit lane mask of D[u] + w_k == D[t]
-//            (one pull of D[u] per arc).  Only these arcs can carry a lexicographic minimum
-//            (SURVEY §8a "Derived semantics"); every reachable non-source (t, lane) has one.
+//   phase 2a tight records: per in-arc k = (u, t) the 64-bit lane mask of D[u] + w_k == D[t]
+//            (one pull of D[u] per arc); the arcs tight in some lane are kept as records
+//            {u, 1 - loss, mask} at the head of t's own in-arc range (31 % of C4's arcs), so the fold
+//            walks only them.  Only these arcs can carry a lexicographic minimum (SURVEY §8a
+//            "Derived semantics"); every reachable non-source (t, lane) has one.
 //   phase 2b loss fold over the tight arcs: lane l of t is computed once every tight
 //            predecessor of t in lane l is final there, as min over them of
 //            fold(L[u][l], 1 - p_k) (the left fold of mod.rs:322-331, separately rounded).
@@ -30,8 +32,9 @@
 // 5.6 row pulls per arc (the lexicographic kernel: 6.4 pulls of 512-B rows), phase 2a 1 pull per
 // arc, phase 2b 1.12 pulls per arc; result equal to a per-lane lexicographic Dijkstra.
 //
-// Layout (HBM, per resident workgroup): D [V][64] u32, L [V][64] f32, TM [arcs] u64 tight masks,
-// F [V] u64 final-lane masks; vertex bitmaps + window lists in LDS (GB = false) or a global slice.
+// Layout (HBM, per resident workgroup): D [V][64] u32, L [V][64] f32, TR [arcs] 16-B tight records,
+// F [V] u64 final-lane masks + TC [V] u32 tight-record counts; vertex bitmaps + window lists in LDS
+// (GB = false) or a global slice.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -41,7 +44,8 @@
 namespace srg {
 
 constexpr uint32_t DS_INF = 0xFFFFFFFFu;
-constexpr uint32_t DS_WS = 128 + 3 * SP_CAP + SP_CAP / 4;  // per-wave scratch (u32): starts, offsets, list, vertex idx
+constexpr uint32_t DS_CAP = SP_CAP;  // list entries per wave
+constexpr uint32_t DS_WS = 128 + 3 * DS_CAP + DS_CAP / 4;  // per-wave scratch (u32): starts, offsets, list, vertex idx
 constexpr size_t ds_scratch_bytes() {
     return (size_t)SP_WAVES * DS_WS * 4 > 64 * 65 * 8 ? (size_t)SP_WAVES * DS_WS * 4 : (size_t)64 * 65 * 8;
 }
@@ -99,15 +103,18 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     uint32_t* w_st = scratch + wave * DS_WS;
     uint32_t* w_lo = w_st + 64;
     uint32_t* w_u = w_lo + 64;
-    uint32_t* w_w = w_u + SP_CAP;
-    uint32_t* w_b = w_w + SP_CAP;
-    unsigned char* w_i = reinterpret_cast<unsigned char*>(w_b + SP_CAP);
+    uint32_t* w_w = w_u + DS_CAP;
+    uint32_t* w_b = w_w + DS_CAP;
+    unsigned char* w_i = reinterpret_cast<unsigned char*>(w_b + DS_CAP);
     unsigned long long* blk = reinterpret_cast<unsigned long long*>(w_u);  // phase 2b pass A: 64 x u64
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
     uint32_t* D = reinterpret_cast<uint32_t*>(a.slots) + (size_t)blockIdx.x * V * 64;
     float* LO = a.lo_slots + (size_t)blockIdx.x * V * 64;
-    unsigned long long* TM = a.tmask + (size_t)blockIdx.x * a.arcs;
-    unsigned long long* FM = a.fmask + (size_t)blockIdx.x * V;
+    // tight records: vertex t's tight in-arcs at TR[in_off[t] .. in_off[t] + TC[t]) as {u, bits of
+    // 1 - loss, lane mask lo, hi} -- inside t's own arc range, so no global offsets are needed
+    uint4* TR = reinterpret_cast<uint4*>(a.tmask) + (size_t)blockIdx.x * a.arcs;
+    unsigned long long* FM = a.fmask + (size_t)blockIdx.x * V * 2;
+    uint32_t* TC = reinterpret_cast<uint32_t*>(FM + V);
     uint32_t max_sweeps = 0, max_sweeps2 = 0;
     uint32_t evals = 0, pulls2 = 0;  // (per wave, flushed per batch)
     uint32_t saturated = 0;
@@ -376,7 +383,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         max_sweeps = sweeps > max_sweeps ? sweeps : max_sweeps;
         stamp(0);
 
-        // ================= phase 2a: tight masks, final-lane init =================
+        // ================= phase 2a: tight records, final-lane init =================
         for (uint32_t w = wave; w < nw; w += SP_WAVES) {
             const uint32_t vl = w * 64 + lane;
             const bool valid = vl < V;
@@ -387,7 +394,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             w_st[lane] = st;
             w_lo[lane] = lo;
             __builtin_amdgcn_wave_barrier();
-            uint32_t dt = 0;
+            uint32_t dt = 0, tcnt = 0;  // tcnt: lane i counts vertex i's tight arcs
+            int cur = 0;
             auto process = [&](uint32_t cnt) {
                 for (uint32_t j0 = 0; j0 < cnt; j0 += G1) {
                     uint32_t row[G1];
@@ -399,7 +407,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                         const uint32_t e = j0 + q;
                         if (e >= cnt) break;
                         if (w_b[e] == SP_OWN) {
-                            const uint32_t t = w * 64 + (w_w[e] & 63u);
+                            cur = (int)(w_w[e] & 63u);
+                            const uint32_t t = w * 64 + cur;
                             dt = row[q];
                             const unsigned long long fin = __ballot(dt == DS_INF) | __ballot(my_src == t);
                             if (lane == 0) FM[t] = fin;
@@ -409,18 +418,15 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                             const bool tight =
                                 r != DS_INF && dt != DS_INF && __builtin_elementwise_add_sat(r, w_w[e]) == dt;
                             const unsigned long long m = __ballot(tight);
-                            __builtin_amdgcn_wave_barrier();
-                            if (lane == 0) {
-                                w_u[e] = (uint32_t)m;
-                                w_w[e] = (uint32_t)(m >> 32);
+                            if (m) {
+                                const uint32_t pos = (uint32_t)__builtin_amdgcn_readlane((int)tcnt, cur);
+                                if (lane == 0)
+                                    TR[w_lo[cur] + pos] = make_uint4(w_u[e], w_b[e], (uint32_t)m, (uint32_t)(m >> 32));
+                                tcnt += lane == (uint32_t)cur;
                             }
                         }
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                for (uint32_t e = lane; e < cnt; e += 64)
-                    if (w_b[e] != SP_OWN) TM[w_b[e]] = ((unsigned long long)w_w[e] << 32) | w_u[e];
-                __builtin_amdgcn_wave_barrier();
             };
             uint32_t n = 0;
             for (uint32_t f0 = 0; f0 < total; f0 += 64) {
@@ -439,13 +445,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                         const uint32_t k = w_lo[i] + slot - 1;
                         w_u[pos] = a.in_src[k];
                         w_w[pos] = a.in_w[k];
-                        w_b[pos] = k;
+                        w_b[pos] = __float_as_uint(a.in_b[k]);  // (b in [0, 1]: never SP_OWN's bits)
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
                 n += (uint32_t)__popcll(m);
-                if (n > SP_CAP - 64) {
+                if (n > DS_CAP - 64) {
                     process(n);
+                    __builtin_amdgcn_wave_barrier();
                     n = 0;
                     const uint32_t fn = f0 + 64;  // a vertex continuing past the chunk: its own row first
                     if (fn < total) {
@@ -463,6 +470,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                 }
             }
             if (n) process(n);
+            __builtin_amdgcn_wave_barrier();
+            if (valid) TC[vl] = tcnt;
         }
         // ================= phase 2b: loss fold in per-lane Kahn order =================
         __syncthreads();
@@ -504,10 +513,10 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                     nf = ~fold_now;  // reachable lanes not final yet (unreachable ones start final)
                 }
                 const uint32_t lo = nf ? a.in_off[vl] : 0u;
-                const uint32_t hi = nf ? a.in_off[vl + 1] : 0u;
+                const uint32_t tc = nf ? TC[vl] : 0u;
                 // pass A: lanes blocked by a tight predecessor that is not final there
                 uint32_t total;
-                uint32_t st = ds_prefix(hi - lo, lane, &total);
+                uint32_t st = ds_prefix(tc, lane, &total);
                 w_st[lane] = st;
                 w_lo[lane] = lo;
                 blk[lane] = 0;
@@ -522,10 +531,11 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                     }
                     const unsigned long long nfi = ds_shfl64(nf, i);
                     if (on) {
-                        const unsigned long long m = TM[k] & nfi;
+                        const uint4 rc = TR[k];
+                        const unsigned long long m = (((unsigned long long)rc.w << 32) | rc.z) & nfi;
                         if (m) {
                             const unsigned long long fu =
-                                __hip_atomic_load(&FM[a.in_src[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                __hip_atomic_load(&FM[rc.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             const unsigned long long b = m & ~fu;
                             if (b) atomicOr(&blk[i], b);
                         }
@@ -537,7 +547,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                 __builtin_amdgcn_wave_barrier();
                 if (!__ballot(comp != 0)) continue;
                 // pass B: fold the tight arcs of the completed lanes
-                st = ds_prefix(comp ? hi - lo : 0u, lane, &total);
+                st = ds_prefix(comp ? tc : 0u, lane, &total);
                 w_st[lane] = st;
                 __builtin_amdgcn_wave_barrier();
                 int cur = -1;
@@ -546,6 +556,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                 auto flush = [&]() {
                     if (cur >= 0 && ((ccur >> lane) & 1ull)) LO[(size_t)(w * 64 + cur) * 64 + lane] = acc;
                 };
+                const unsigned long long* TRm = reinterpret_cast<const unsigned long long*>(TR);
                 auto process = [&](uint32_t cnt) {
                     for (uint32_t j0 = 0; j0 < cnt; j0 += G2) {
                         float row[G2];
@@ -554,7 +565,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                         for (int q = 0; q < G2; ++q)
                             if (j0 + q < cnt) {
                                 row[q] = LO[(size_t)w_u[j0 + q] * 64 + lane];
-                                tq[q] = TM[w_b[j0 + q]];
+                                tq[q] = TRm[2 * (size_t)w_b[j0 + q] + 1];  // the record's lane mask
                             }
 #pragma unroll
                         for (int q = 0; q < G2; ++q) {
@@ -585,18 +596,20 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                         k = w_lo[i] + (f - w_st[i]);
                     }
                     const unsigned long long ci = ds_shfl64(comp, i);
-                    const bool act = on && (TM[k] & ci) != 0ull;
+                    uint4 rc = make_uint4(0u, 0u, 0u, 0u);
+                    if (on) rc = TR[k];
+                    const bool act = on && ((((unsigned long long)rc.w << 32) | rc.z) & ci) != 0ull;
                     const unsigned long long m = __ballot(act);
                     if (act) {
                         const uint32_t pos = n + ds_mbcnt(m);
-                        w_u[pos] = a.in_src[k];
-                        w_w[pos] = __float_as_uint(a.in_b[k]);
+                        w_u[pos] = rc.x;
+                        w_w[pos] = rc.y;
                         w_b[pos] = k;
                         w_i[pos] = (unsigned char)i;
                     }
                     __builtin_amdgcn_wave_barrier();
                     n += (uint32_t)__popcll(m);
-                    if (n > SP_CAP - 64) {
+                    if (n > DS_CAP - 64) {
                         process(n);
                         n = 0;
                         __builtin_amdgcn_wave_barrier();
