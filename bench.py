@@ -291,6 +291,7 @@ def workload_key(args, V, seed, world):
             + ("lb:" if args.graph != "ba" else "")
             + f"packed2:tile{args.fw_tile or 128}:"
             f"div{args.sparse_delta_div if args.sparse_delta_div is not None else 1}:g8:w2"
+            + (":ds2" if args.graph == "ba" else "")  # the two-phase sparse kernel (round 6)
             + (f":sym{args.fw_symmetric}" if args.fw_symmetric is not None else "")
             + (f":n{world}" if world > 1 else "") + (f":sim{args.simulate_rank}" if args.simulate_rank else ""))
 
@@ -308,8 +309,9 @@ def roofline_for(agg, kind, args, edges, V, wkey, sym):
         per_src = arcs * 16 + (V + 1) * 4 + V * 12
         srcs = agg["prof_relaxations"] / agg["prof_launches"]
         achieved = per_src * srcs / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic("k_sparse_bf", wkey)
-        return {"bound": "hbm", "kernel": "k_sparse_bf (batched lexicographic Bellman-Ford, delta-stepping buckets)",
+        traffic, tsrc = load_traffic("k_sparse", wkey)
+        return {"bound": "hbm", "kernel": "k_sparse_ds (two-phase: latency-only batched delta-stepping with "
+                                          "wavefront-aggregated window pushes, tight records, per-lane Kahn loss fold)",
                 "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
                 "bytes_per_source": per_src, "sources_per_launch": int(srcs), "traffic_source": tsrc,
@@ -431,7 +433,7 @@ def emit(args, V, gdesc, edges, kind, world, value, ms_per_step, agg, s, rooflin
         "dtype": "u64+f32" if kind == 1 else "u32+f32", "data": "synthetic",
         "config": {"workload": f"{gdesc}, all {V} nodes used, {entry_desc}", "entry": args.entry, "vertices": V,
                    "edges": int(edges.num_edges), "global_batch": V,
-                   "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-bf-u32"}.get(kind, str(kind)), **extra_cfg},
+                   "path": {0: "dense-u32", 1: "dense-u64", 3: "sparse-ds-u32", 4: "sparse-bf-u64"}.get(kind, str(kind)), **extra_cfg},
         "apsp_wall_ms": round(ms_per_step, 3),
         # per-step wall times of the timed loop (this rank's clock; value uses the whole loop's max over ranks)
         "step_ms": steps_ms,

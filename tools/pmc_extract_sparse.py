@@ -1,4 +1,4 @@
-"""Per-launch PMC averages of the sparse kernel k_sparse_bf from a tools/pmc_sparse.sh output
+"""Per-launch PMC averages of the sparse kernel (k_sparse_ds, two-phase; k_sparse_bf, wide labels) from a tools/pmc_sparse.sh output
 directory -> profiles/sparse_pmc_latest.json (read by bench.py --graph ba).
 
 usage: python tools/pmc_extract_sparse.py PMC_DIR SOURCE_TEXT [WORKLOAD_KEY]
@@ -21,14 +21,16 @@ def main():
     d, source = sys.argv[1], sys.argv[2]
     wkey = sys.argv[3] if len(sys.argv) > 3 else None
     acc = collections.defaultdict(list)
+    names = set()
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_sparse_bf" not in r["Kernel_Name"]:
+            if "k_sparse_ds" not in r["Kernel_Name"] and "k_sparse_bf" not in r["Kernel_Name"]:
                 continue
+            names.add(r["Kernel_Name"])
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {c: sum(v) / len(v) for c, v in acc.items()}
     fetch, write = avg.get("FETCH_SIZE", 0.0), avg.get("WRITE_SIZE", 0.0)
-    out = {"source": source, "workload_key": wkey, "kernel": "srg::k_sparse_bf(srg::SparseArgs)",
+    out = {"source": source, "workload_key": wkey, "kernel": ", ".join(sorted(names)) or None,
            "launches_averaged": len(acc.get("FETCH_SIZE", [])),
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),

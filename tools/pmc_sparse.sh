@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over one C4 (--graph ba) bench step for the sparse kernel k_sparse_bf, each pass its
+# PMC passes over one C4 (--graph ba) bench step for the sparse kernel (k_sparse_ds), each pass its
 # own run (rocprofv3 does not split passes).  usage: tools/pmc_sparse.sh OUTDIR [bench args...]
 set -e
 out=$1; shift

@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
     std::vector<uint64_t> tm(A), F(V), reach(V);
     std::vector<uint8_t> fprev(V), fcur(V), mark(V), mnext(V), pend(V);
     std::vector<uint64_t> cm(V), cmn(V), cmp(V);  // lanes changed in the last / this sweep / pending
-    double p1_lines = 0;
+    double p1_lines = 0, p1_scans = 0, p1_marked = 0, p1_hubscans = 0;
     double p1_pulls = 0, p1_sweeps = 0, p2_pulls = 0, p2_sweeps = 0, p2_scans = 0, tight_arcs = 0, tight_pairs = 0;
     long bad = 0;
     for (int bi = 0; bi < nb; ++bi) {
@@ -115,6 +115,9 @@ int main(int argc, char** argv) {
                 if (!mark[t]) continue;
                 uint32_t* lt = &L[(size_t)t * 64];
                 bool drop = false, below = false;
+                p1_marked++;
+                p1_scans += off[t + 1] - off[t];
+                if (off[t + 1] - off[t] >= 64) p1_hubscans += off[t + 1] - off[t];
                 for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
                     const uint32_t u = src[k];
                     if (!fprev[u]) continue;
@@ -260,9 +263,9 @@ int main(int argc, char** argv) {
             }
         }
     }
-    printf("{\"p1_lines_per_arc\": %.3f, \"p1_pulls_per_arc\": %.3f, \"p1_sweeps\": %.2f, \"p2_pulls_per_arc\": %.3f, \"p2_sweeps\": %.2f, "
+    printf("{\"p1_scans_per_arc\": %.3f, \"p1_hub_scans_per_arc\": %.3f, \"p1_marked_per_vertex\": %.3f, \"p1_lines_per_arc\": %.3f, \"p1_pulls_per_arc\": %.3f, \"p1_sweeps\": %.2f, \"p2_pulls_per_arc\": %.3f, \"p2_sweeps\": %.2f, "
            "\"p2_scans_per_arc\": %.3f, \"tight_arc_frac\": %.3f, \"tight_lanes_per_tight_arc\": %.2f, \"mismatches\": %ld}\n",
-           p1_lines / nb / A, p1_pulls / nb / A, p1_sweeps / nb, p2_pulls / nb / A, p2_sweeps / nb, p2_scans / nb / A, tight_arcs / nb / A,
+           p1_scans / nb / A, p1_hubscans / nb / A, p1_marked / nb / V, p1_lines / nb / A, p1_pulls / nb / A, p1_sweeps / nb, p2_pulls / nb / A, p2_sweeps / nb, p2_scans / nb / A, tight_arcs / nb / A,
            tight_pairs / std::max(1.0, tight_arcs), bad);
     return 0;
 }
