@@ -12,10 +12,11 @@ step stats
 (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o c3 -- python3 -u $GRAFT_REPO_ROOT/bench.py --no-cpu > $out/bench_c3_under_rocprof.json 2> $out/stats.err) || { echo "stats failed"; tail -20 $out/stats.err; exit 1; }
 step pmc_fw
 timeout -k 10 900 bash tools/pmc_fw.sh $out/pmc_fw > $out/pmc_fw.log 2>&1 || { echo "pmc_fw failed"; tail -20 $out/pmc_fw.log; exit 1; }
-python3 tools/pmc_extract.py $out/pmc_fw/ "rocprofv3 --pmc, r05 final (tools/pmc_fw.sh, C3 atlas_like(10000) host entry, 1 step, fw_bulk_lb bulk launches)" "atlas:10000:10000:lb:packed2:tile128:div1:g8:w2" > $out/pmc_fw_extract.log 2>&1 || { echo "extract fw failed"; tail -5 $out/pmc_fw_extract.log; exit 1; }
+python3 tools/pmc_extract.py $out/pmc_fw/ "rocprofv3 --pmc, $tag (tools/pmc_fw.sh, C3 atlas_like(10000) host entry, 1 step, fw_bulk_lb bulk launches)" "atlas:10000:10000:lb:packed2:tile128:div1:g8:w2" > $out/pmc_fw_extract.log 2>&1 || { echo "extract fw failed"; tail -5 $out/pmc_fw_extract.log; exit 1; }
 step pmc_sparse
 timeout -k 10 900 bash tools/pmc_sparse.sh $out/pmc_sparse > $out/pmc_sparse.log 2>&1 || { echo "pmc_sparse failed"; tail -20 $out/pmc_sparse.log; exit 1; }
-true  # (extracted locally from the merged CSVs)
+python3 tools/pmc_extract_sparse.py $out/pmc_sparse "rocprofv3 --pmc, $tag (tools/pmc_sparse.sh, C4 barabasi_albert(50000, 4), 1 step, k_sparse_ds two-phase)" "ba:50000:50000:packed2:tile128:div1:g8:w2:ds2" > $out/pmc_sparse_extract.log 2>&1 || { echo "extract sparse failed"; tail -5 $out/pmc_sparse_extract.log; exit 1; }
+cp profiles/sparse_pmc_latest.json profiles/fw_pmc_latest.json $out/
 step configs
 for cfg in c1 c2 c4 c5; do
   timeout -k 10 400 python3 -u bench.py --config $cfg --no-cpu > $out/bench_$cfg.json 2> $out/bench_$cfg.err || { echo "bench $cfg failed"; tail -10 $out/bench_$cfg.err; exit 1; }
