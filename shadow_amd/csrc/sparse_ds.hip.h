@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     unsigned long long* pend = mnext + nw;
     uint32_t* wl_a = reinterpret_cast<uint32_t*>(pend + nw);
     uint32_t* wl_b = wl_a + nw;
-    __shared__ uint32_t s_batch, s_changed, s_pend, s_ncur, s_nnext;
+    __shared__ uint32_t s_batch, s_changed, s_pend, s_ncur, s_nnext, s_take, s_take2;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* scratch = reinterpret_cast<uint32_t*>(GB ? smem_raw : smem_raw + ds_state_bytes(V));
     uint32_t* w_st = scratch + wave * DS_WS;
@@ -120,6 +120,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     uint32_t saturated = 0;
     uint32_t* wl_cur = wl_a;
     uint32_t* wl_next = wl_b;
+    // windows are taken dynamically, one LDS atomic per wave: a window holding a high-degree vertex
+    // takes several times the average, and a static stride left the other waves idle at the sweep's
+    // barrier
+    auto take = [&](uint32_t* ctr) {
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(ctr, 1u);
+        return (uint32_t)__shfl((int)i, 0, 64);
+    };
     // wall-clock ticks per phase (1, 2a, 2b, output) summed over the workgroup's batches (thread 0)
     __shared__ unsigned long long s_ph[5];
     if (threadIdx.x < 5) s_ph[threadIdx.x] = 0;
@@ -211,6 +219,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             s_pend = 0;
             s_nnext = 0;
             s_ncur = 0;
+            s_take2 = 0;
         }
         uint64_t bound = a.delta >= 0xFFFFFFFFull ? 0xFFFFFFFFull : a.delta;
         __syncthreads();
@@ -231,11 +240,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         sync_lists();
         uint32_t sweeps = 0;
         for (;;) {
-            if (threadIdx.x == 0) s_changed = 0;
+            if (threadIdx.x == 0) {
+                s_changed = 0;
+                s_take = 0;
+            }
             __syncthreads();
             uint32_t chg = 0;
             const uint32_t ncur = s_ncur;
-            for (uint32_t idx = wave; idx < ncur; idx += SP_WAVES) {
+            for (uint32_t idx = take(&s_take); idx < ncur; idx = take(&s_take)) {
                 const uint32_t w = wl_cur[idx];
                 const unsigned long long mk = mark[w];
                 const uint32_t vl = w * 64 + lane;
@@ -384,7 +396,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         stamp(0);
 
         // ================= phase 2a: tight records, final-lane init =================
-        for (uint32_t w = wave; w < nw; w += SP_WAVES) {
+        for (uint32_t w = take(&s_take2); w < nw; w = take(&s_take2)) {
             const uint32_t vl = w * 64 + lane;
             const bool valid = vl < V;
             const uint32_t lo = valid ? a.in_off[vl] : 0u;
@@ -498,11 +510,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         sync_lists();
         uint32_t sweeps2 = 0;
         for (;;) {
-            if (threadIdx.x == 0) s_changed = 0;
+            if (threadIdx.x == 0) {
+                s_changed = 0;
+                s_take = 0;
+            }
             __syncthreads();
             uint32_t chg = 0;
             const uint32_t ncur = s_ncur;
-            for (uint32_t idx = wave; idx < ncur; idx += SP_WAVES) {
+            for (uint32_t idx = take(&s_take); idx < ncur; idx = take(&s_take)) {
                 const uint32_t w = wl_cur[idx];
                 const unsigned long long mk = mark[w];
                 const uint32_t vl = w * 64 + lane;
