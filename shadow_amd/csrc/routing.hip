@@ -2946,8 +2946,14 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     const size_t slot_bytes = (size_t)V * 64 * (wide ? 16 : two_phase ? 4 : 8);
     const size_t ds_extra = two_phase ? (size_t)V * 64 * 4 + (size_t)std::max<uint32_t>(arcs, 1) * 16 + (size_t)V * 16 : 0;
+    // two launches (phase 1, then phases 2 + output) when every batch's latency labels fit beside the
+    // rest (C4: 782 x 12.8 MB = 10 GB): each launch gets its own register allocation
+    // (SRG_SPARSE_SPLIT=0: one fused launch, A/B)
+    const char* sp_env = std::getenv("SRG_SPARSE_SPLIT");
+    const size_t d_all = (size_t)nbatch * V * 64 * 4;
+    const bool split = two_phase && nbatch && !(sp_env && sp_env[0] == '0') && d_all <= free_b / 3;
     grid = (uint32_t)std::max<size_t>(
-        1, std::min<size_t>(grid, free_b / 2 / std::max<size_t>(slot_bytes + ds_extra, 1)));
+        1, std::min<size_t>(grid, (free_b / 2 - (split ? d_all : 0)) / std::max<size_t>((split ? 0 : slot_bytes) + ds_extra, 1)));
     const uint32_t nwv = (V + 63) / 64;
     const size_t bitmap_bytes = two_phase ? ds_state_bytes(V) : (size_t)nwv * 5 * 8;
     const size_t scr_bytes = two_phase ? ds_scratch_bytes() : sp_scratch_bytes();
@@ -2955,7 +2961,7 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     const bool gbits = c.sparse_global_bitmaps || bitmap_bytes + scr_bytes > (size_t)160 * 1024 / wpc;
     const size_t lds = (gbits ? 0 : bitmap_bytes) + scr_bytes;
     if (nbatch) {
-        unsigned long long* slots = (unsigned long long*)c.b_D.get((size_t)grid * slot_bytes);
+        unsigned long long* slots = (unsigned long long*)c.b_D.get(split ? d_all : (size_t)grid * slot_bytes);
         unsigned long long* gb = gbits ? (unsigned long long*)c.b_W.get((size_t)grid * bitmap_bytes) : nullptr;
         // 16 rows in flight was measured 2.5x slower (the row array no longer unrolls into
         // registers); 4 ties with 8 at 2 workgroups per CU
@@ -2993,7 +2999,18 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
             }
             HIP_CHECK(hipEventRecord(c.prof_events[0], st));
         }
-        kern<<<grid, SP_THREADS, lds, st>>>(a);
+        if (split) {
+            auto k1 = gbits ? k_sparse_ds<true, 8, 8, 1> : k_sparse_ds<false, 8, 8, 1>;
+            auto k2 = gbits ? k_sparse_ds<true, 8, 8, 2> : k_sparse_ds<false, 8, 8, 2>;
+            set_lds(k1, lds);
+            set_lds(k2, lds);
+            k1<<<grid, SP_THREADS, lds, st>>>(a);
+            SparseArgs a2 = a;
+            a2.queue = fl + 9;  // (zeroed with the flags)
+            k2<<<grid, SP_THREADS, lds, st>>>(a2);
+        } else {
+            kern<<<grid, SP_THREADS, lds, st>>>(a);
+        }
         HIP_CHECK(hipGetLastError());
         if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
     }
@@ -3002,8 +3019,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         c.comm->allreduce_max_u32(fl, 2, st);
         c.comm->allreduce_max_u32(fl + 5, 3, st);  // saturated, impossible, fold incomplete
     }
-    uint32_t hfl[20] = {};
-    HIP_CHECK(hipMemcpyAsync(hfl, fl, 80, hipMemcpyDeviceToHost, st));
+    uint32_t hfl[26] = {};
+    HIP_CHECK(hipMemcpyAsync(hfl, fl, 104, hipMemcpyDeviceToHost, st));
     const double ms_sssp = tm.lap();
     if (hfl[7])
         fail(SRG_ERR_INTERNAL, "the sparse build's loss fold left a used pair without a final loss");
@@ -3023,6 +3040,11 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
                 t[p] = (double)((unsigned long long)hfl[12 + 2 * p] | (unsigned long long)hfl[13 + 2 * p] << 32) / 1e5 / grid;
             std::fprintf(stderr, "sparse phases (ms per workgroup): latency %.1f, tight masks %.1f, fold %.1f, output %.1f\n",
                          t[0], t[1], t[2], t[3]);
+            double b[3];  // wave utilisation: ticks inside window visits / (16 waves x the phase's ticks)
+            for (int p = 0; p < 3; ++p)
+                b[p] = (double)((unsigned long long)hfl[20 + 2 * p] | (unsigned long long)hfl[21 + 2 * p] << 32) / 1e5 / grid /
+                       (16.0 * std::max(t[p], 1e-9));
+            std::fprintf(stderr, "sparse wave utilisation: latency %.2f, tight masks %.2f, fold %.2f\n", b[0], b[1], b[2]);
         }
     }
     if (hfl[0]) {

@@ -84,7 +84,11 @@ __device__ __forceinline__ uint32_t ds_find(const uint32_t* st, uint32_t f) {
 }
 
 // G1: label rows in flight per wave in phases 1 and 2a (u32 rows), G2: in the fold (f32 rows + masks)
-template <bool GB, int G1, int G2>
+// MODE 0: one kernel runs every phase of a batch (labels per resident workgroup); MODE 1: phase 1
+// only and MODE 2: phases 2 + the output only, as two launches with the latency labels kept per BATCH
+// in between -- each launch then gets its own register allocation (the fused kernel spills 28 VGPRs
+// at the 64-VGPR budget, phase 1 alone none: 105.9 vs 117.6 ms per workgroup, profiles/r06/sparse_split/)
+template <bool GB, int G1, int G2, int MODE = 0>
 __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
@@ -108,7 +112,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     unsigned char* w_i = reinterpret_cast<unsigned char*>(w_b + DS_CAP);
     unsigned long long* blk = reinterpret_cast<unsigned long long*>(w_u);  // phase 2b pass A: 64 x u64
     unsigned long long* tile = reinterpret_cast<unsigned long long*>(scratch);
-    uint32_t* D = reinterpret_cast<uint32_t*>(a.slots) + (size_t)blockIdx.x * V * 64;
+    uint32_t* const Dbase = reinterpret_cast<uint32_t*>(a.slots);
+    uint32_t* D = Dbase + (size_t)blockIdx.x * V * 64;
     float* LO = a.lo_slots + (size_t)blockIdx.x * V * 64;
     // tight records: vertex t's tight in-arcs at TR[in_off[t] .. in_off[t] + TC[t]) as {u, bits of
     // 1 - loss, lane mask lo, hi} -- inside t's own arc range, so no global offsets are needed
@@ -130,7 +135,14 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     };
     // wall-clock ticks per phase (1, 2a, 2b, output) summed over the workgroup's batches (thread 0)
     __shared__ unsigned long long s_ph[5];
+    __shared__ unsigned long long s_busy[3];  // wave-ticks inside window visits (phases 1, 2a, 2b)
     if (threadIdx.x < 5) s_ph[threadIdx.x] = 0;
+    if (threadIdx.x < 3) s_busy[threadIdx.x] = 0;
+    unsigned long long tv0 = 0;
+    auto vis_begin = [&]() { tv0 = wall_clock64(); };
+    auto vis_end = [&](int p) {
+        if (lane == 0) atomicAdd(&s_busy[p], wall_clock64() - tv0);
+    };
     auto stamp = [&](int p) {
         if (threadIdx.x == 0) {
             const unsigned long long t = wall_clock64();
@@ -198,13 +210,18 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     };
 
     for (;;) {
-        if (threadIdx.x == 0) s_batch = atomicAdd(a.queue, 1u);
+        if (threadIdx.x == 0) {
+            s_batch = atomicAdd(a.queue, 1u);
+            s_take2 = 0;
+        }
         __syncthreads();
         const uint32_t bt = s_batch;
         __syncthreads();
         if (bt >= a.nbatch) break;
+        if constexpr (MODE != 0) D = Dbase + (size_t)bt * V * 64;  // this batch's labels
         const uint32_t my_src = a.batch_src[bt * 64 + lane];
         stamp(-1);
+        if constexpr (MODE != 2) {
 
         // ================= phase 1: latency-only delta-stepping =================
         for (uint32_t v = wave; v < V; v += SP_WAVES) D[(size_t)v * 64 + lane] = (v == my_src) ? 0u : DS_INF;
@@ -219,7 +236,6 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             s_pend = 0;
             s_nnext = 0;
             s_ncur = 0;
-            s_take2 = 0;
         }
         uint64_t bound = a.delta >= 0xFFFFFFFFull ? 0xFFFFFFFFull : a.delta;
         __syncthreads();
@@ -248,6 +264,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             uint32_t chg = 0;
             const uint32_t ncur = s_ncur;
             for (uint32_t idx = take(&s_take); idx < ncur; idx = take(&s_take)) {
+                vis_begin();
                 const uint32_t w = wl_cur[idx];
                 const unsigned long long mk = mark[w];
                 const uint32_t vl = w * 64 + lane;
@@ -357,6 +374,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                     push_window(w, changed);
                 }
                 __builtin_amdgcn_wave_barrier();
+                vis_end(0);
             }
             if (chg && lane == 0) s_changed = 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // label stores reached L2
@@ -394,9 +412,12 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         }
         max_sweeps = sweeps > max_sweeps ? sweeps : max_sweeps;
         stamp(0);
+        }  // (MODE != 2)
+        if constexpr (MODE == 1) continue;
 
         // ================= phase 2a: tight records, final-lane init =================
         for (uint32_t w = take(&s_take2); w < nw; w = take(&s_take2)) {
+            vis_begin();
             const uint32_t vl = w * 64 + lane;
             const bool valid = vl < V;
             const uint32_t lo = valid ? a.in_off[vl] : 0u;
@@ -484,6 +505,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             if (n) process(n);
             __builtin_amdgcn_wave_barrier();
             if (valid) TC[vl] = tcnt;
+            vis_end(1);
         }
         // ================= phase 2b: loss fold in per-lane Kahn order =================
         __syncthreads();
@@ -518,6 +540,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             uint32_t chg = 0;
             const uint32_t ncur = s_ncur;
             for (uint32_t idx = take(&s_take); idx < ncur; idx = take(&s_take)) {
+                vis_begin();
                 const uint32_t w = wl_cur[idx];
                 const unsigned long long mk = mark[w];
                 const uint32_t vl = w * 64 + lane;
@@ -560,7 +583,10 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 const unsigned long long comp = nf & ~blk[lane];
                 __builtin_amdgcn_wave_barrier();
-                if (!__ballot(comp != 0)) continue;
+                if (!__ballot(comp != 0)) {
+                    vis_end(2);
+                    continue;
+                }
                 // pass B: fold the tight arcs of the completed lanes
                 st = ds_prefix(comp ? tc : 0u, lane, &total);
                 w_st[lane] = st;
@@ -640,6 +666,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                 chg = 1;
                 push_window(w, done);
                 __builtin_amdgcn_wave_barrier();
+                vis_end(2);
             }
             if (chg && lane == 0) s_changed = 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -723,6 +750,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         stamp(3);
     }
     if (threadIdx.x < 4) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[12 + 2 * threadIdx.x]), s_ph[threadIdx.x]);
+    if (threadIdx.x < 3) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[20 + 2 * threadIdx.x]), s_busy[threadIdx.x]);
     if (threadIdx.x == 0) {
         atomicMax(&a.flags[1], max_sweeps);
         atomicMax(&a.flags[8], max_sweeps2);
