@@ -2970,13 +2970,9 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         auto kern = gbits ? k_sparse_bf<SP_G, true> : k_sparse_bf<SP_G, false>;
         if (wide) kern = gbits ? k_sparse_bf<SP_G, true, 4, LabelU64> : k_sparse_bf<SP_G, false, 4, LabelU64>;
         if (two_phase) {
-            // rows in flight per wave (phases 1 / 2a, fold): SRG_DS_G = 8 | 16 | 32 (A/B)
-            const char* gs = std::getenv("SRG_DS_G");
-            const int gsel = gs ? std::atoi(gs) : 8;
-            // (8 rows: 16 and 32 spill more at the 64-VGPR budget and measured 375 / 712 ms against 293
-            // on C4, profiles/r06/sparse_ds/c4_g*.json)
+            // 8 rows in flight per wave: 16 and 32 spill at the 64-VGPR budget and measured 375 / 712 ms
+            // against 293 on C4 (profiles/r06/sparse_ds/c4_g*.json)
             kern = gbits ? k_sparse_ds<true, 8, 8> : k_sparse_ds<false, 8, 8>;
-            if (gsel == 16) kern = gbits ? k_sparse_ds<true, 16, 8> : k_sparse_ds<false, 16, 8>;
         }
         set_lds(kern, lds);
         SparseArgs a{off, in_src, in_w, in_b, out_off, out_dst, V, d_bsrc, d_brow, nbatch, slots, fl + 4, cols, n,
@@ -3002,6 +2998,8 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         if (split) {
             auto k1 = gbits ? k_sparse_ds<true, 8, 8, 1> : k_sparse_ds<false, 8, 8, 1>;
             auto k2 = gbits ? k_sparse_ds<true, 8, 8, 2> : k_sparse_ds<false, 8, 8, 2>;
+            // (phase 1 in 8-wave workgroups at 128 VGPRs with 32 rows in flight per wave, no spills, was
+            // measured slower: 151 vs 115 ms per workgroup, profiles/r06/sparse_p1w/)
             set_lds(k1, lds);
             set_lds(k2, lds);
             k1<<<grid, SP_THREADS, lds, st>>>(a);

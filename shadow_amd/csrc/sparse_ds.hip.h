@@ -88,8 +88,12 @@ __device__ __forceinline__ uint32_t ds_find(const uint32_t* st, uint32_t f) {
 // only and MODE 2: phases 2 + the output only, as two launches with the latency labels kept per BATCH
 // in between -- each launch then gets its own register allocation (the fused kernel spills 28 VGPRs
 // at the 64-VGPR budget, phase 1 alone none: 105.9 vs 117.6 ms per workgroup, profiles/r06/sparse_split/)
-template <bool GB, int G1, int G2, int MODE = 0>
-__global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
+template <bool GB, int G1, int G2, int MODE = 0, int NW = 16>
+__global__ void __launch_bounds__(NW * 64, NW == 16 ? 8 : 4) k_sparse_ds(SparseArgs a) {
+    // (NW = 8 with 128 VGPRs and 32 rows in flight per wave ran phase 1 slower: 151 vs 115 ms per
+    // workgroup -- the 16-wave form keeps twice the waves' worth of rows in flight per CU)
+    static_assert(NW == 16 || MODE == 1, "the output phase is laid out for 16 waves");
+    constexpr int WV = NW, TH = NW * 64;  // waves / threads per workgroup
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const uint32_t V = a.V;
     const uint32_t nw = (V + 63) / 64;
@@ -190,7 +194,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
     };
     // sweep boundary: mnext -> mark, window lists swapped (caller synchronises before and after)
     auto rotate_marks = [&]() {
-        for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+        for (uint32_t w = threadIdx.x; w < nw; w += TH) {
             mark[w] = mnext[w];
             mnext[w] = 0;
         }
@@ -224,8 +228,8 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         if constexpr (MODE != 2) {
 
         // ================= phase 1: latency-only delta-stepping =================
-        for (uint32_t v = wave; v < V; v += SP_WAVES) D[(size_t)v * 64 + lane] = (v == my_src) ? 0u : DS_INF;
-        for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+        for (uint32_t v = wave; v < V; v += WV) D[(size_t)v * 64 + lane] = (v == my_src) ? 0u : DS_INF;
+        for (uint32_t w = threadIdx.x; w < nw; w += TH) {
             fprev[w] = 0;
             fcur[w] = 0;
             mark[w] = 0;
@@ -241,7 +245,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         __syncthreads();
         if (wave == 0) atomicOr(&fprev[my_src >> 6], 1ull << (my_src & 63));
         // the sources' out-neighbours: one lane set per wave, each wave a few sources
-        for (uint32_t q = wave; q < 64; q += SP_WAVES) {
+        for (uint32_t q = wave; q < 64; q += WV) {
             const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)my_src, q);
             const uint32_t o0 = a.out_off[sv], o1 = a.out_off[sv + 1];
             for (uint32_t k0 = o0; k0 < o1; k0 += 64) {
@@ -383,7 +387,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             ++sweeps;
             const bool more = s_changed != 0;
-            for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+            for (uint32_t w = threadIdx.x; w < nw; w += TH) {
                 fprev[w] = fcur[w];
                 fcur[w] = 0;
             }
@@ -395,13 +399,13 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
                 // the bound moves on by one bucket
                 __syncthreads();  // every thread has read s_pend
                 bound = (a.delta >= 0xFFFFFFFFull || bound > 0xFFFFFFFFull - a.delta) ? 0xFFFFFFFFull : bound + a.delta;
-                for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+                for (uint32_t w = threadIdx.x; w < nw; w += TH) {
                     fprev[w] = pend[w];
                     pend[w] = 0;
                 }
                 __syncthreads();
                 if (threadIdx.x == 0) s_pend = 0;
-                for (uint32_t w = wave; w < nw; w += SP_WAVES) {
+                for (uint32_t w = wave; w < nw; w += WV) {
                     const unsigned long long pw = fprev[w];
                     if (pw) push_window(w, pw);
                 }
@@ -510,7 +514,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         // ================= phase 2b: loss fold in per-lane Kahn order =================
         __syncthreads();
         stamp(1);
-        for (uint32_t w = threadIdx.x; w < nw; w += SP_THREADS) {
+        for (uint32_t w = threadIdx.x; w < nw; w += TH) {
             mark[w] = 0;
             mnext[w] = 0;
         }
@@ -519,7 +523,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (uint32_t q = wave; q < 64; q += SP_WAVES) {
+        for (uint32_t q = wave; q < 64; q += WV) {
             const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)my_src, q);
             const uint32_t o0 = a.out_off[sv], o1 = a.out_off[sv + 1];
             for (uint32_t k0 = o0; k0 < o1; k0 += 64) {
@@ -693,7 +697,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             unsigned long long fm[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t j = j0 + wave + SP_WAVES * q;
+                const uint32_t j = j0 + wave + WV * q;
                 dv[q] = 0;
                 lv[q] = 0;
                 fm[q] = ~0ull;
@@ -706,7 +710,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t i = wave + SP_WAVES * q;
+                const uint32_t i = wave + WV * q;
                 tD[i * 65 + lane] = dv[q];
                 tL[i * 65 + lane] = lv[q];
                 // every reachable lane of a used column final, with a loss a tight arc gave it
@@ -716,7 +720,7 @@ __global__ void __launch_bounds__(SP_THREADS, 8) k_sparse_ds(SparseArgs a) {
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t sl = wave + SP_WAVES * q;
+                const uint32_t sl = wave + WV * q;
                 const uint32_t row = a.batch_row[bt * 64 + sl];
                 const uint32_t j = j0 + lane;
                 if (row == 0xFFFFFFFFu || j >= a.ncols) continue;
