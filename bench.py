@@ -298,7 +298,7 @@ def workload_key(args, V, seed, world):
 
 def roofline_for(agg, kind, args, edges, V, wkey, sym):
     """The dominant kernel's roofline from the HIP-event launch times the library recorded:
-    dense = the FW bulk tile kernel (VALU), sparse = k_sparse_bf (HBM)."""
+    dense = the FW bulk tile kernel (VALU), sparse = the k_sparse_ds build (HBM; its launches between two events)."""
     if not agg.get("prof_launches"):
         return None
     avg_ms = agg["prof_kernel_ms"] / agg["prof_launches"]

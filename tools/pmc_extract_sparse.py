@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,18 +21,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     d, source = sys.argv[1], sys.argv[2]
     wkey = sys.argv[3] if len(sys.argv) > 3 else None
-    acc = collections.defaultdict(list)
+    # per build: the two-phase kernel runs as two launches (MODE 1: phase 1, MODE 2: phases 2 +
+    # output) or one fused launch (MODE 0); a build's counters are the sum over its launches
+    tot = collections.defaultdict(float)
+    builds = collections.defaultdict(set)
     names = set()
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_sparse_ds" not in r["Kernel_Name"] and "k_sparse_bf" not in r["Kernel_Name"]:
+            name = r["Kernel_Name"]
+            if "k_sparse_ds" not in name and "k_sparse_bf" not in name:
                 continue
-            names.add(r["Kernel_Name"])
-            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    avg = {c: sum(v) / len(v) for c, v in acc.items()}
+            names.add(name)
+            c = r["Counter_Name"]
+            tot[c] += float(r["Counter_Value"])
+            m = re.search(r"k_sparse_ds<\s*\w+,\s*\d+,\s*\d+,\s*(\d+)", name)
+            if not (m and m.group(1) == "2"):  # one launch per build opens it
+                builds[c].add((f, r.get("Dispatch_Id", r.get("Index", ""))))
+    avg = {c: tot[c] / max(1, len(builds[c])) for c in tot}
     fetch, write = avg.get("FETCH_SIZE", 0.0), avg.get("WRITE_SIZE", 0.0)
     out = {"source": source, "workload_key": wkey, "kernel": ", ".join(sorted(names)) or None,
-           "launches_averaged": len(acc.get("FETCH_SIZE", [])),
+           "builds_averaged": len(builds.get("FETCH_SIZE", ())),
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
            "hbm_bytes_per_launch_low": int((fetch + write) * 1024),
