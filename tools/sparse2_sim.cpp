@@ -77,6 +77,18 @@ int main(int argc, char** argv) {
     double p1_lines = 0, p1_scans = 0, p1_marked = 0, p1_hubscans = 0;
     double p1_pulls = 0, p1_sweeps = 0, p2_pulls = 0, p2_sweeps = 0, p2_scans = 0, tight_arcs = 0, tight_pairs = 0;
     long bad = 0;
+    // fold pushes along tight arcs only (SIM_FILTER=1): t marks in-neighbour u (= out-neighbour,
+    // undirected) only when the arc t -> u is tight in a lane t just completed
+    const bool filt = getenv("SIM_FILTER") && atoi(getenv("SIM_FILTER"));
+    std::vector<uint32_t> twin(A);
+    for (uint32_t t = 0; t < V; ++t)
+        for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
+            const uint32_t u = src[k];  // arc u -> t at k; its twin t -> u sits in u's list with src t
+            uint32_t j = off[u];
+            while (src[j] != t) ++j;
+            twin[k] = j;
+        }
+    double p2_visits = 0, p2_useless = 0, p2_tscans = 0, p2_pushes = 0;
     for (int bi = 0; bi < nb; ++bi) {
         const uint32_t b = (uint32_t)((bi * (size_t)stride) % nbatch);
         std::fill(L.begin(), L.end(), INF);
@@ -202,12 +214,14 @@ int main(int argc, char** argv) {
                 const uint64_t nf = reach[t] & ~F[t];
                 if (!nf) continue;
                 uint64_t blocked = 0;
+                p2_visits++;
                 for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
                     p2_scans++;
+                    p2_tscans += tm[k] != 0;
                     blocked |= tm[k] & nf & ~F[src[k]];
                 }
                 const uint64_t comp = nf & ~blocked;
-                if (!comp) continue;
+                if (!comp) { p2_useless++; continue; }
                 float acc[64];
                 for (int l = 0; l < 64; ++l) acc[l] = 2.0f;
                 for (uint32_t k = off[t]; k < off[t + 1]; ++k) {
@@ -221,7 +235,8 @@ int main(int argc, char** argv) {
                     if ((comp >> l) & 1) LO[(size_t)t * 64 + l] = acc[l];
                 F[t] |= comp;
                 any = true;
-                for (uint32_t k = off[t]; k < off[t + 1]; ++k) mnext[src[k]] = 1;
+                for (uint32_t k = off[t]; k < off[t + 1]; ++k)
+                    if (!filt || (tm[twin[k]] & comp)) mnext[src[k]] = 1, p2_pushes++;
             }
             ++p2_sweeps;
             for (uint32_t v = 0; v < V; ++v) {
@@ -264,8 +279,8 @@ int main(int argc, char** argv) {
         }
     }
     printf("{\"p1_scans_per_arc\": %.3f, \"p1_hub_scans_per_arc\": %.3f, \"p1_marked_per_vertex\": %.3f, \"p1_lines_per_arc\": %.3f, \"p1_pulls_per_arc\": %.3f, \"p1_sweeps\": %.2f, \"p2_pulls_per_arc\": %.3f, \"p2_sweeps\": %.2f, "
-           "\"p2_scans_per_arc\": %.3f, \"tight_arc_frac\": %.3f, \"tight_lanes_per_tight_arc\": %.2f, \"mismatches\": %ld}\n",
+           "\"p2_scans_per_arc\": %.3f, \"tight_arc_frac\": %.3f, \"tight_lanes_per_tight_arc\": %.2f, \"mismatches\": %ld, \"p2_visits_per_vertex\": %.3f, \"p2_useless_frac\": %.3f, \"p2_tight_scans_per_arc\": %.3f, \"p2_pushes_per_arc\": %.3f}\n",
            p1_scans / nb / A, p1_hubscans / nb / A, p1_marked / nb / V, p1_lines / nb / A, p1_pulls / nb / A, p1_sweeps / nb, p2_pulls / nb / A, p2_sweeps / nb, p2_scans / nb / A, tight_arcs / nb / A,
-           tight_pairs / std::max(1.0, tight_arcs), bad);
+           tight_pairs / std::max(1.0, tight_arcs), bad, p2_visits / nb / V, p2_useless / std::max(1.0, p2_visits), p2_tscans / nb / A, p2_pushes / nb / A);
     return 0;
 }
