@@ -2987,6 +2987,12 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         // bucket width: the largest edge latency / sparse_delta_div (0 = one bucket, plain BF)
         if (c.sparse_delta_div > 0)
             a.delta = std::max<unsigned long long>(1ull, P.max_key / (unsigned long long)c.sparse_delta_div);
+        const char* dbg_env = std::getenv("SRG_DEBUG_SPARSE");
+        const bool dbg_batches = two_phase && dbg_env && dbg_env[0] == '2';
+        if (dbg_batches) {
+            a.dbg = (uint32_t*)c.b_L1.get((size_t)nbatch * 6 * 4);
+            HIP_CHECK(hipMemsetAsync(a.dbg, 0, (size_t)nbatch * 6 * 4, st));
+        }
         if (c.profiling) {
             while (c.prof_events.size() < 2) {
                 hipEvent_t e;
@@ -3011,6 +3017,31 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
         }
         HIP_CHECK(hipGetLastError());
         if (c.profiling) HIP_CHECK(hipEventRecord(c.prof_events[1], st));
+        if (dbg_batches) {  // per-batch durations (100-MHz ticks): what sets the launches' makespan
+            std::vector<uint32_t> h((size_t)nbatch * 6);
+            HIP_CHECK(hipMemcpyAsync(h.data(), a.dbg, h.size() * 4, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            for (int ph = 0; ph < 2; ++ph) {
+                std::vector<double> d(nbatch);
+                for (uint32_t b = 0; b < nbatch; ++b) {
+                    d[b] = h[b * 6 + 1 + 4 * ph] / 1e5;
+                }
+                std::vector<double> srt = d;
+                std::sort(srt.begin(), srt.end());
+                std::fprintf(stderr, "sparse batches phase %d (ms): min %.1f p10 %.1f median %.1f p90 %.1f max %.1f; by batch decile:",
+                             ph + 1, srt[0], srt[nbatch / 10], srt[nbatch / 2], srt[nbatch * 9 / 10], srt[nbatch - 1]);
+                for (int q = 0; q < 10; ++q) {
+                    double m = 0;
+                    uint32_t cnt = 0;
+                    for (uint32_t b = q * nbatch / 10; b < (q + 1) * nbatch / 10; ++b) m += d[b], ++cnt;
+                    std::fprintf(stderr, " %.1f", cnt ? m / cnt : 0.0);
+                }
+                std::fprintf(stderr, "\n");
+            }
+            std::fprintf(stderr, "sparse batches phase-1 sweeps:");
+            for (uint32_t b = 0; b < nbatch; b += std::max<uint32_t>(1, nbatch / 20)) std::fprintf(stderr, " %u", h[b * 6 + 3]);
+            std::fprintf(stderr, "\n");
+        }
     }
     // every rank agrees on the outcome before any exchange
     if (multi) {

@@ -69,7 +69,8 @@ struct LabelU32 {
     __device__ static bool is_inf(T a) { return a == LBL_INF; }
     __device__ static uint64_t lat(T a) { return a >> 32; }
     __device__ static uint32_t loss_bits(T a) { return (uint32_t)a; }
-    __device__ T ld(size_t i) const { return __builtin_nontemporal_load(&L[i]); }
+    // plain loads: C4 274-276 ms against 281-304 with the nontemporal hint (profiles/r06/sparse_cache/)
+    __device__ T ld(size_t i) const { return L[i]; }
     __device__ void st(size_t i, T v) const { L[i] = v; }
     // arc weight: the list holds the u32 key itself
     __device__ static T relax(T u, uint32_t wtag, float b, const uint64_t*) { return lbl_relax(u, wtag, b); }
@@ -92,7 +93,7 @@ struct LabelU64 {
     __device__ static uint64_t lat(T a) { return a.l; }
     __device__ static uint32_t loss_bits(T a) { return a.s; }
     __device__ T ld(size_t i) const {
-        const v2u64 v = __builtin_nontemporal_load(&L[i]);
+        const v2u64 v = L[i];
         return T{v.x, (uint32_t)v.y};
     }
     __device__ void st(size_t i, T v) const {
@@ -201,6 +202,7 @@ struct SparseArgs {
     unsigned long long* tmask;   // [gridDim.x][arcs] tight-lane masks per in-arc
     unsigned long long* fmask;   // [gridDim.x][V] final-lane masks of the loss fold
     uint32_t arcs;
+    uint32_t* dbg;  // per-batch {start, phase-1 ticks, workgroup, sweeps, phase-2 start, phase-2 ticks} (SRG_DEBUG_SPARSE=2)
 };
 
 // a vertex whose label dropped in some lanes is pushed now if some dropped lane's new latency is
