@@ -2876,10 +2876,13 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     c.own_row1 = p1;
     const uint32_t nloc = p1 - p0;
     const uint32_t nbatch = (nloc + 63) / 64;
+    const double ms_csr = std::getenv("SRG_DEBUG_SPARSE") ? tm.lap() : 0.0;  // (debug split of ms_build)
+    const auto t_host0 = std::chrono::steady_clock::now();
     std::vector<uint32_t> h_off(V + 1), h_src(arcs);
     HIP_CHECK(hipMemcpyAsync(h_off.data(), off, ((size_t)V + 1) * 4, hipMemcpyDeviceToHost, st));
     if (arcs) HIP_CHECK(hipMemcpyAsync(h_src.data(), in_src, (size_t)arcs * 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    const auto t_host1 = std::chrono::steady_clock::now();
     std::vector<uint32_t> order(V, 0xFFFFFFFFu), queue;
     queue.reserve(V);
     uint32_t next = 0;
@@ -2909,17 +2912,22 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
             if (root_pass == 0) break;
         }
     }
+    const auto t_host2 = std::chrono::steady_clock::now();
     std::vector<uint32_t> loc(nloc);
     for (uint32_t i = 0; i < nloc; ++i) loc[i] = p0 + i;
-    if (c.sparse_locality)
-        std::stable_sort(loc.begin(), loc.end(),
-                         [&](uint32_t x, uint32_t y) { return order[P.nodes_h[x]] < order[P.nodes_h[y]]; });
+    if (c.sparse_locality) {  // stable by BFS position: a counting sort over the V positions
+        std::vector<uint32_t> cnt((size_t)V + 1, 0);
+        for (uint32_t i = 0; i < nloc; ++i) ++cnt[order[P.nodes_h[p0 + i]] + 1];
+        for (uint32_t v = 0; v < V; ++v) cnt[v + 1] += cnt[v];
+        for (uint32_t i = 0; i < nloc; ++i) loc[cnt[order[P.nodes_h[p0 + i]]]++] = p0 + i;
+    }
     std::vector<uint32_t> bsrc((size_t)std::max<uint32_t>(nbatch, 1) * 64), brow(bsrc.size());
     for (uint32_t i = 0; i < (uint32_t)bsrc.size(); ++i) {
         const bool real = i < nloc;
         bsrc[i] = P.nodes_h[real ? loc[i] : (nloc ? loc[0] : 0)];
         brow[i] = real ? loc[i] : 0xFFFFFFFFu;
     }
+    const auto t_host3 = std::chrono::steady_clock::now();
     uint32_t* d_bsrc = (uint32_t*)c.b_lnodes.get(bsrc.size() * 4);
     uint32_t* d_brow = (uint32_t*)c.b_lpos.get(brow.size() * 4);
     HIP_CHECK(hipMemcpyAsync(d_bsrc, bsrc.data(), bsrc.size() * 4, hipMemcpyHostToDevice, st));
@@ -2927,7 +2935,13 @@ bool run_sparse(srg_ctx& c, const DevGraph& g, const uint32_t* nodes, uint32_t n
     uint32_t* fl = (uint32_t*)c.b_red.get(128);
     HIP_CHECK(hipMemsetAsync(fl, 0, 128, st));
     HIP_CHECK(hipGetLastError());
-    const double ms_build = tm.lap();
+    const double ms_build = tm.lap() + ms_csr;
+    if (std::getenv("SRG_DEBUG_SPARSE"))
+        std::fprintf(stderr, "sparse build: CSR %.2f ms, host order + batches %.2f ms (of %.2f): CSR to host %.2f, BFS %.2f, batches %.2f\n", ms_csr,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count(), ms_build,
+                     std::chrono::duration<double, std::milli>(t_host1 - t_host0).count(),
+                     std::chrono::duration<double, std::milli>(t_host2 - t_host1).count(),
+                     std::chrono::duration<double, std::milli>(t_host3 - t_host2).count());
 
     int dev_cus = 256;
     HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c.device));

@@ -431,7 +431,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 16 ? 8 : 4) k_sparse_ds(SparseA
             a.dbg[bt * 6 + 3] = sweeps;
         }
         }  // (MODE != 2)
-        if constexpr (MODE == 1) continue;
+        if constexpr (MODE == 1) {  // (the lane evaluations are flushed here, the rest after the output)
+            if (lane == 0 && evals) atomicAdd(reinterpret_cast<unsigned long long*>(&a.flags[2]), (unsigned long long)evals);
+            evals = 0;
+            continue;
+        }
 
         // ================= phase 2a: tight records, final-lane init =================
         for (uint32_t w = take(&s_take2); w < nw; w = take(&s_take2)) {
