@@ -2367,7 +2367,11 @@ bool run_dense(srg_ctx& c, const DevGraph& g, const Plan& pl, const uint32_t* no
         // It runs on the (idle) FW lookahead stream beside the certification, extract and
         // essential-entry count, which read W and D only; st waits for it before the entry fill.
         hipStream_t ax = c.aux_stream;  // st is synchronised (tm.lap): FW is complete
+        const auto tl0 = std::chrono::steady_clock::now();
         loss_arrive(g, P.selfloss, ax);
+        if (std::getenv("SRG_DEBUG_OVERLAP"))
+            std::fprintf(stderr, "late loss: the host waited %.2f ms for the loss thread after FW\n",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl0).count());
         if constexpr (sizeof(K) == 4) {
             unsigned long long* KW = (unsigned long long*)c.b_PRED.get(VV * 8);
             HIP_CHECK(hipMemsetAsync(KW, 0xFF, VV * 8, ax));
@@ -3629,21 +3633,34 @@ void start_late_loss(srg_ctx& c, const srg_edge_list* g, DevGraph& dg, hipStream
         constexpr int NB = 3;
         try {
             HIP_CHECK(hipSetDevice(device));
+            const bool dbg = std::getenv("SRG_DEBUG_OVERLAP") != nullptr;
+            const auto t0 = std::chrono::steady_clock::now();
+            double t_copy = 0, t_wait = 0;
             const size_t E = std::min<size_t>(g->num_edges, a1);  // this rank's slice [a0, E)
             float* dloss = const_cast<float*>(dg.loss);
             for (size_t ch = 0, e0 = a0; e0 < E; ++ch, e0 += CE) {
                 const int b = (int)(ch % NB);
+                auto ta = std::chrono::steady_clock::now();
                 if (ch >= (size_t)NB) HIP_CHECK(hipEventSynchronize(c.ev_lring[b]));
+                auto tb = std::chrono::steady_clock::now();
                 const size_t ne = std::min(CE, E - e0);
                 float* slot = (float*)c.h_lring + (size_t)b * CE;
                 c.pool->run([&](int w, int nw) {
                     const size_t a = ne * w / nw, z = ne * (w + 1) / nw;
                     std::memcpy(slot + a, g->packet_loss + e0 + a, (z - a) * 4);
                 });
+                t_wait += std::chrono::duration<double, std::milli>(tb - ta).count();
+                t_copy += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count();
                 HIP_CHECK(hipMemcpyAsync(dloss + e0, slot, ne * 4, hipMemcpyHostToDevice, c.loss_stream));
                 HIP_CHECK(hipEventRecord(c.ev_lring[b], c.loss_stream));
             }
             HIP_CHECK(hipEventRecord(L.ev_in, c.loss_stream));
+            if (dbg) {
+                HIP_CHECK(hipEventSynchronize(L.ev_in));
+                std::fprintf(stderr, "late loss thread: %.2f ms to the last DMA, host copies %.2f ms, ring waits %.2f ms\n",
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                             t_copy, t_wait);
+            }
         } catch (const Failure& f) {
             L.err = f.msg;
         } catch (const std::exception& e) {
@@ -3810,6 +3827,12 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // codec_in gives up on the first chunk that is neither)
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) &&
                            codec_in(*c, g, dg, hst, a0, a1, !want_late, all_narrow, all_seq, on_chunk);
+        // the losses start crossing now: the enqueue of the remaining pivots below can hold this
+        // thread until FW nears its end (the launch queue fills), and a loss thread started after it
+        // landed its DMA ~3 ms after FW had finished (SRG_DEBUG_OVERLAP "late loss" lines)
+        LateLoss late;
+        late.ls = c->loss_stream;
+        if (coded && want_late) start_late_loss(*c, g, dg, hst, late, a0, a1);
         if (ov.on) ov.finish();  // the FW thread has enqueued every landed chunk's work
         if (ov.on && !coded) ov.ok = false;
         const int ov_early = ov.next;  // pivots enqueued while chunks were still crossing
@@ -3819,9 +3842,6 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             std::fprintf(stderr, "fw-overlap: ok=%d pivots_during_h2d=%d of %d\n", ov.ok ? 1 : 0, ov_early, ov.nb);
             if (ov.ok) ov.report();
         }
-        LateLoss late;
-        late.ls = c->loss_stream;
-        if (coded && want_late) start_late_loss(*c, g, dg, hst, late, a0, a1);
         if (!coded) {
             const size_t cnt = std::max<size_t>(E, 1);
             dg.src = (uint32_t*)c->b_src.get(cnt * 4);
