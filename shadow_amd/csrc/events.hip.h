@@ -193,10 +193,13 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const unsigned long long
     h[threadIdx.x] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * RS_TILE;
+    // the high words only for a digit that reaches them (the last pass of a wide key): the other
+    // passes read half the bytes
+    const bool need_hi = WIDE && p + 8 > 64;
 #pragma unroll 4
     for (int r = 0; r < RS_ROUNDS; ++r) {
         const size_t i = base + (size_t)r * RS_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[rs_digit(klo[i], WIDE ? khi[i] : 0ull, p)], 1u);
+        if (i < n) atomicAdd(&h[rs_digit(p >= 64 ? 0ull : klo[i], need_hi ? khi[i] : 0ull, p)], 1u);
     }
     __syncthreads();
     hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
