@@ -3827,12 +3827,6 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
         // codec_in gives up on the first chunk that is neither)
         const bool coded = c->h2d_codec && a1 - a0 >= ((size_t)1 << 20) &&
                            codec_in(*c, g, dg, hst, a0, a1, !want_late, all_narrow, all_seq, on_chunk);
-        // the losses start crossing now: the enqueue of the remaining pivots below can hold this
-        // thread until FW nears its end (the launch queue fills), and a loss thread started after it
-        // landed its DMA ~3 ms after FW had finished (SRG_DEBUG_OVERLAP "late loss" lines)
-        LateLoss late;
-        late.ls = c->loss_stream;
-        if (coded && want_late) start_late_loss(*c, g, dg, hst, late, a0, a1);
         if (ov.on) ov.finish();  // the FW thread has enqueued every landed chunk's work
         if (ov.on && !coded) ov.ok = false;
         const int ov_early = ov.next;  // pivots enqueued while chunks were still crossing
@@ -3842,6 +3836,12 @@ int host_entry(srg_ctx* c, const srg_edge_list* g, const uint32_t* nodes, uint32
             std::fprintf(stderr, "fw-overlap: ok=%d pivots_during_h2d=%d of %d\n", ov.ok ? 1 : 0, ov_early, ov.nb);
             if (ov.ok) ov.report();
         }
+        // (started here, after the remaining pivots are enqueued -- an enqueue that holds this thread
+        // until FW nears its end -- the losses land ~3 ms after FW, but that wait overlaps GPU work:
+        // starting the thread before it measured 46.9-47.4 vs 46.5-46.6 ms, profiles/r06/late_loss/)
+        LateLoss late;
+        late.ls = c->loss_stream;
+        if (coded && want_late) start_late_loss(*c, g, dg, hst, late, a0, a1);
         if (!coded) {
             const size_t cnt = std::max<size_t>(E, 1);
             dg.src = (uint32_t*)c->b_src.get(cnt * 4);
